@@ -1,0 +1,172 @@
+"""ctypes mirror of the engine's C-ABI (include/fqengine.h).
+
+Python is plumbing here: the product is the C-ABI library ``libfqengine.so`` (HIP kernels
+for gfx950) and the C++ host tool ``fqtool``.  This module only lets bench.py / tests /
+__graft_entry__ call the same entry points a reference-side binding would.
+"""
+import ctypes
+import os
+
+FQ_MAX_ADAPTER = 128
+FQ_OK = 0
+
+FQ_ACC_FILTER = 0
+FQ_ACC_ADAPTER_READS = 32
+FQ_ACC_ADAPTER_BASES = 33
+FQ_ACC_POLYX_READS = 34
+FQ_ACC_POLYX_BASES = 39
+FQ_ACC_MERGED_PAIRS = 44
+FQ_ACC_INSERT = 48
+FQ_ST_READS, FQ_ST_LENGTH_SUM, FQ_ST_Q20, FQ_ST_Q30 = 0, 1, 2, 3
+FQ_ST_CYCLES = 16
+FQ_ST_PER_CYCLE = 16
+
+FQ_RF_NULL = 0x01
+FQ_RF_AD_OVERLAP = 0x02
+FQ_RF_AD_SEQ = 0x04
+FQ_RF_AD_NEG = 0x08
+FQ_RF_MERGED = 0x10
+FQ_RF_OVERLAP = 0x20
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+ENGINE_LIB = os.path.join(PKG_DIR, "lib", "libfqengine.so")
+HOST_LIB = os.path.join(PKG_DIR, "lib", "libfqhost.so")
+FQTOOL_BIN = os.path.join(PKG_DIR, "bin", "fqtool")
+
+
+class FqParams(ctypes.Structure):
+    _fields_ = [
+        ("paired", ctypes.c_int32),
+        ("trim_front1", ctypes.c_int32), ("trim_tail1", ctypes.c_int32),
+        ("trim_front2", ctypes.c_int32), ("trim_tail2", ctypes.c_int32),
+        ("cut_front", ctypes.c_int32), ("cut_right", ctypes.c_int32), ("cut_tail", ctypes.c_int32),
+        ("cut_front_window", ctypes.c_int32), ("cut_right_window", ctypes.c_int32),
+        ("cut_tail_window", ctypes.c_int32),
+        ("cut_front_quality", ctypes.c_int32), ("cut_right_quality", ctypes.c_int32),
+        ("cut_tail_quality", ctypes.c_int32),
+        ("polyg_enabled", ctypes.c_int32),
+        ("polyg_compare_req", ctypes.c_int32), ("polyg_max_mismatch", ctypes.c_int32),
+        ("polyg_one_mismatch_per", ctypes.c_int32),
+        ("polyx_enabled", ctypes.c_int32), ("polyx_mask", ctypes.c_int32),
+        ("polyx_compare_req", ctypes.c_int32), ("polyx_max_mismatch", ctypes.c_int32),
+        ("polyx_one_mismatch_per", ctypes.c_int32),
+        ("adapter_trimming", ctypes.c_int32),
+        ("adapter1_len", ctypes.c_int32), ("adapter2_len", ctypes.c_int32),
+        ("adapter1", ctypes.c_uint8 * FQ_MAX_ADAPTER),
+        ("adapter2", ctypes.c_uint8 * FQ_MAX_ADAPTER),
+        ("overlap_diff_limit", ctypes.c_int32), ("overlap_require", ctypes.c_int32),
+        ("insert_size_max", ctypes.c_int32),
+        ("max_len1", ctypes.c_int32), ("max_len2", ctypes.c_int32),
+        ("merge_enabled", ctypes.c_int32), ("discard_unmerged", ctypes.c_int32),
+        ("qual_filter_enabled", ctypes.c_int32),
+        ("low_qual_limit", ctypes.c_int32), ("low_qual_base_limit", ctypes.c_int32),
+        ("n_base_limit", ctypes.c_int32),
+        ("avg_qual_limit", ctypes.c_double),
+        ("length_filter_enabled", ctypes.c_int32), ("min_len", ctypes.c_int32),
+        ("max_len", ctypes.c_int32),
+        ("complexity_enabled", ctypes.c_int32),
+        ("complexity_threshold", ctypes.c_double),
+        ("max_cycles", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 7),
+    ]
+
+
+class FqBatch(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int32), ("stride", ctypes.c_int32),
+        ("seq1", ctypes.c_void_p), ("qual1", ctypes.c_void_p), ("len1", ctypes.c_void_p),
+        ("seq2", ctypes.c_void_p), ("qual2", ctypes.c_void_p), ("len2", ctypes.c_void_p),
+    ]
+
+
+class FqReadResult(ctypes.Structure):
+    _fields_ = [
+        ("start", ctypes.c_uint16), ("len", ctypes.c_uint16),
+        ("code", ctypes.c_uint8), ("flags", ctypes.c_uint8),
+        ("ad_pos", ctypes.c_uint16), ("ad_len", ctypes.c_uint16),
+        ("m_len1", ctypes.c_uint16), ("m_len2", ctypes.c_uint16),
+        ("reserved", ctypes.c_uint16),
+    ]
+
+
+RESULT_DTYPE_FIELDS = [("start", "<u2"), ("len", "<u2"), ("code", "u1"), ("flags", "u1"),
+                       ("ad_pos", "<u2"), ("ad_len", "<u2"), ("m_len1", "<u2"), ("m_len2", "<u2"),
+                       ("reserved", "<u2")]
+
+
+def acc_stats_words(max_cycles):
+    return FQ_ST_CYCLES + max_cycles * FQ_ST_PER_CYCLE
+
+
+def acc_stats_offset(insert_size_max, max_cycles, k):
+    base = FQ_ACC_INSERT + insert_size_max + 1
+    base = (base + 15) & ~15
+    return base + k * acc_stats_words(max_cycles)
+
+
+def acc_words(insert_size_max, max_cycles):
+    return acc_stats_offset(insert_size_max, max_cycles, 4)
+
+
+def default_params(paired=True, max_cycles=256):
+    """Reference defaults after Options::update (reference src/options.h, src/options.cpp:24-58)
+    with every CLI flag off (CLI11 resets bool flags to false)."""
+    p = FqParams()
+    p.paired = 1 if paired else 0
+    p.cut_front_window = p.cut_right_window = p.cut_tail_window = 4
+    p.cut_front_quality = p.cut_right_quality = p.cut_tail_quality = 20
+    p.polyg_compare_req, p.polyg_max_mismatch, p.polyg_one_mismatch_per = (1, 10, 10) if paired else (10, 1, 10)
+    p.polyx_mask = 0x1F
+    p.polyx_compare_req, p.polyx_max_mismatch, p.polyx_one_mismatch_per = 10, 1, 10
+    p.overlap_diff_limit, p.overlap_require, p.insert_size_max = 5, 30, 512
+    p.low_qual_limit = 20 + 33
+    p.low_qual_base_limit = int(0.15 * 151)
+    p.n_base_limit = 5
+    p.min_len = 15
+    p.complexity_threshold = 0.3
+    p.max_cycles = max_cycles
+    return p
+
+
+def set_adapter(p, which, seq):
+    data = seq.encode() if isinstance(seq, str) else bytes(seq)
+    if len(data) > FQ_MAX_ADAPTER:
+        raise ValueError("adapter too long")
+    arr = getattr(p, "adapter%d" % which)
+    for i, c in enumerate(data):
+        arr[i] = c
+    setattr(p, "adapter%d_len" % which, len(data))
+
+
+def load_engine(path=ENGINE_LIB):
+    """Load libfqengine.so and declare its prototypes.  Raises OSError when it is missing:
+    there is no CPU fallback."""
+    lib = ctypes.CDLL(path)
+    vp, i32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
+    lib.fq_engine_create.argtypes = [ctypes.POINTER(FqParams), ctypes.c_int, i32, i32, ctypes.POINTER(vp)]
+    lib.fq_engine_create.restype = ctypes.c_int
+    lib.fq_engine_destroy.argtypes = [vp]
+    lib.fq_engine_process.argtypes = [vp, ctypes.POINTER(FqBatch), vp]
+    lib.fq_engine_process_device.argtypes = [vp, ctypes.POINTER(FqBatch), vp, vp]
+    lib.fq_engine_acc_words.argtypes = [vp]
+    lib.fq_engine_acc_words.restype = ctypes.c_size_t
+    lib.fq_engine_acc_device_ptr.argtypes = [vp, ctypes.POINTER(vp)]
+    lib.fq_engine_read_acc.argtypes = [vp, vp, ctypes.c_size_t]
+    lib.fq_engine_reset_acc.argtypes = [vp]
+    lib.fq_engine_sync.argtypes = [vp]
+    lib.fq_engine_last_error.argtypes = [vp]
+    lib.fq_engine_last_error.restype = ctypes.c_char_p
+    lib.fq_engine_device_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_size_t]
+    lib.fq_synth_fill_device.argtypes = [ctypes.POINTER(FqBatch), u64, u64, i32, vp]
+    lib.fq_engine_last_kernel_ms.argtypes = [vp]
+    lib.fq_engine_last_kernel_ms.restype = ctypes.c_double
+    return lib
+
+
+ENGINE_SYMBOLS = [
+    "fq_engine_create", "fq_engine_destroy", "fq_engine_process", "fq_engine_process_device",
+    "fq_engine_acc_words", "fq_engine_acc_device_ptr", "fq_engine_read_acc", "fq_engine_reset_acc",
+    "fq_engine_sync", "fq_engine_last_error", "fq_engine_device_info", "fq_synth_fill_device",
+    "fq_engine_last_kernel_ms",
+]

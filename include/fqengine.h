@@ -1,0 +1,252 @@
+/*
+ * fqengine.h -- C-ABI drop-in boundary of the MI355X FASTQ preprocessing engine.
+ *
+ * The reference (Wsc000123/fqtool, a fastp fork) has no plugin/FFI API; its hot path is the
+ * per-pack worker call
+ *     bool PairEndProcessor::processPairEnd(ReadPairPack*, ThreadConfig*)
+ *         (reference src/peprocessor.h:61, body src/peprocessor.cpp:261-508)
+ *     void SingleEndProcessor::processSingleEnd(ReadPack*, ThreadConfig*)
+ *         (reference src/seprocessor.cpp:290-388)
+ * which mutates the reads of one pack in place and accumulates into the worker's
+ * ThreadConfig (Stats x4 + FilterResult, src/threadconfig.cpp:3-20) and the processor's
+ * insert-size histogram (src/peprocessor.cpp:510-523).
+ *
+ * This header replaces that seam with plain pointers and sizes (no C++ / torch types):
+ *   - fq_params       : POD snapshot of every derived Options field the loop body reads
+ *                        (src/options.h:15-386 after Options::update, src/options.cpp:24-58)
+ *   - fq_batch        : one pack of reads as SoA uint8 seq/qual rows + uint16 lengths
+ *                        (replaces ReadPairPack / ReadPack, src/peprocessor.h:28-31)
+ *   - fq_read_result  : per-read trim window + filter code + adapter/merge descriptors, i.e.
+ *                        everything the in-place std::string mutations of the loop body produce
+ *   - accumulator     : flat uint64 block = Stats x4 + FilterResult counters + insert histogram,
+ *                        sum-reducible (RCCL ncclSum/ncclUint64 across GPUs)
+ * Every entry point returns 0 on success and a negative FQ_E* code on failure; nothing
+ * throws across the ABI. The engine never falls back to a CPU path: without a usable gfx950
+ * device fq_engine_create fails with FQ_E_NO_DEVICE.
+ */
+#ifndef FQENGINE_H
+#define FQENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FQ_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------- */
+#define FQ_OK 0
+#define FQ_E_INVALID (-1)    /* bad argument / unsupported parameter combination           */
+#define FQ_E_NO_DEVICE (-2)  /* no HIP device, or not gfx950                                */
+#define FQ_E_HIP (-3)        /* a HIP runtime call failed (message in fq_engine_last_error)  */
+#define FQ_E_TOO_LONG (-4)   /* a read is longer than the engine's configured max_cycles     */
+#define FQ_E_NOMEM (-5)
+
+/* ---- filter result codes: reference src/common.h:9-30 -------------------------------- */
+#define FQ_PASS_FILTER 0
+#define FQ_FAIL_POLY_X 4
+#define FQ_FAIL_OVERLAP 8
+#define FQ_FAIL_N_BASE 12
+#define FQ_FAIL_LENGTH 16
+#define FQ_FAIL_TOO_LONG 17
+#define FQ_FAIL_QUALITY 20
+#define FQ_FAIL_COMPLEXITY 24
+#define FQ_FILTER_RESULT_TYPES 32
+
+#define FQ_MAX_ADAPTER 128 /* longest --adapter_of_read{1,2} accepted                       */
+
+/*
+ * Derived options, already in the form the reference's loop body consumes them.
+ * The host (fqtool_amd/host/options.cpp) fills this exactly as Options::update does,
+ * including the reference quirks:
+ *   - low_qual_limit already has +33 added (src/options.cpp:26),
+ *   - low_qual_base_limit = int(lowQualityRatio * 151) (src/options.cpp:44 runs before the
+ *     read-length evaluation, src/main.cpp:124-129),
+ *   - polyg_* are the EFFECTIVE (compareReq, maxMismatch, oneMismatchPer) triple: the PE call
+ *     at src/peprocessor.cpp:297 passes (maxMismatch, allowedOneMismatchForEach, minLen) into
+ *     PolyX::trimPolyG(r1, r2, compareReq, maxMismatch, allowedOneMismatchForEach, fr)
+ *     (src/polyx.h:28), the SE call at src/seprocessor.cpp:317 passes them in order.
+ */
+typedef struct fq_params {
+    int32_t paired; /* 1 = PairEndProcessor, 0 = SingleEndProcessor */
+
+    /* Filter::trimAndCut, src/filter.cpp:69-189 */
+    int32_t trim_front1, trim_tail1, trim_front2, trim_tail2; /* -f -t -F -T */
+    int32_t cut_front, cut_right, cut_tail;                   /* enable flags */
+    int32_t cut_front_window, cut_right_window, cut_tail_window;
+    int32_t cut_front_quality, cut_right_quality, cut_tail_quality; /* mean quality, no +33 */
+
+    /* PolyX::trimPolyG, src/polyx.cpp:14-38 (effective argument order, see above) */
+    int32_t polyg_enabled;
+    int32_t polyg_compare_req, polyg_max_mismatch, polyg_one_mismatch_per;
+
+    /* PolyX::trimPolyX, src/polyx.cpp:45-101 */
+    int32_t polyx_enabled;
+    int32_t polyx_mask; /* bit b set <=> base "ATCGN"[b] is in --base_to_trim */
+    int32_t polyx_compare_req, polyx_max_mismatch, polyx_one_mismatch_per;
+
+    /* adapters: src/peprocessor.cpp:301-326, src/seprocessor.cpp:321-323 */
+    int32_t adapter_trimming; /* -a */
+    int32_t adapter1_len, adapter2_len; /* 0 = not provided (adapterSeqR{1,2}Provided) */
+    uint8_t adapter1[FQ_MAX_ADAPTER];
+    uint8_t adapter2[FQ_MAX_ADAPTER];
+
+    /* OverlapAnalysis::analyze, src/overlapanalysis.cpp:7-72 */
+    int32_t overlap_diff_limit; /* --max_diff_for_overlap, default 5 */
+    int32_t overlap_require;    /* --min_overlap_len, default 30 */
+    int32_t insert_size_max;    /* 512, src/options.cpp:17 */
+
+    /* -b / -B, src/peprocessor.cpp:342-349 */
+    int32_t max_len1, max_len2;
+
+    /* -m, src/peprocessor.cpp:351-385 */
+    int32_t merge_enabled, discard_unmerged;
+
+    /* Filter::passFilter, src/filter.cpp:3-52 */
+    int32_t qual_filter_enabled;
+    int32_t low_qual_limit;      /* -Q + 33 */
+    int32_t low_qual_base_limit; /* int(-U * 151) */
+    int32_t n_base_limit;        /* -N */
+    double avg_qual_limit;       /* -e */
+    int32_t length_filter_enabled, min_len, max_len; /* -l --min_length --max_length */
+    int32_t complexity_enabled;  /* -y */
+    double complexity_threshold; /* -Y */
+
+    /* engine sizing */
+    int32_t max_cycles; /* per-cycle Stats buffer length; reads longer than this are rejected */
+    int32_t reserved[7];
+} fq_params;
+
+/* One pack of reads, row-major: read i's bases are seq[i*stride .. i*stride+len[i]). */
+typedef struct fq_batch {
+    int32_t n;      /* number of pairs (PE) or reads (SE) */
+    int32_t stride; /* bytes per row, multiple of 16, >= every len */
+    const uint8_t* seq1;
+    const uint8_t* qual1;
+    const uint16_t* len1;
+    const uint8_t* seq2; /* PE only, else NULL */
+    const uint8_t* qual2;
+    const uint16_t* len2;
+} fq_batch;
+
+/* fq_read_result.flags */
+#define FQ_RF_NULL 0x01      /* trimAndCut returned NULL (src/filter.cpp:78,100,124,160,183) */
+#define FQ_RF_AD_OVERLAP 0x02 /* trimmed by AdapterTrimmer::trimByOverlapAnalysis */
+#define FQ_RF_AD_SEQ 0x04    /* trimmed by AdapterTrimmer::trimBySequence */
+#define FQ_RF_AD_NEG 0x08    /* trimBySequence matched at pos<0: recorded adapter = adapter[ad_pos:] */
+#define FQ_RF_MERGED 0x10    /* (read-1 record) pair was merged (-m) */
+#define FQ_RF_OVERLAP 0x20   /* (read-1 record) OverlapAnalysis reported overlapped for this pair */
+
+/*
+ * Everything the loop body's in-place std::string edits leave behind, per read (16 bytes).
+ * The surviving read is original[start .. start+len).  For adapter bookkeeping
+ * (FilterResult::addAdapterTrimmed, src/filterresult.cpp:138-177) the host rebuilds the
+ * recorded adapter string from (ad_pos, ad_len): original[ad_pos .. ad_pos+ad_len), or, with
+ * FQ_RF_AD_NEG, adapter[ad_pos .. ad_pos+ad_len).  For a merged pair (FQ_RF_MERGED, read-1
+ * record) the merged read is r1[0:m_len1] + revcomp(r2)[ol : ol+m_len2] with ol = len2 - m_len2
+ * (src/overlapanalysis.cpp:74-104); the read-1 record's code is the merged read's code.
+ */
+typedef struct fq_read_result {
+    uint16_t start;
+    uint16_t len;
+    uint8_t code;  /* Filter::passFilter result, FQ_PASS_FILTER ... */
+    uint8_t flags; /* FQ_RF_* */
+    uint16_t ad_pos;
+    uint16_t ad_len;
+    uint16_t m_len1;
+    uint16_t m_len2;
+    uint16_t reserved;
+} fq_read_result;
+
+/*
+ * Flat accumulator (uint64 words).  Layout (indices into the uint64 array):
+ *   FQ_ACC_FILTER + code          FilterResult::mFilterReadStats[32]
+ *   FQ_ACC_ADAPTER_READS/BASES    FilterResult::mTrimmedAdapterReads/Bases
+ *   FQ_ACC_POLYX_READS + b        FilterResult::mTrimmedPolyXReads[5]  (b in A,T,C,G,N order)
+ *   FQ_ACC_POLYX_BASES + b        FilterResult::mTrimmedPolyXBases[5]
+ *   FQ_ACC_MERGED_PAIRS           ThreadConfig::addMergedPairs
+ *   FQ_ACC_INSERT + isize         PairEndProcessor::mInsertSizeHist[insert_size_max + 1]
+ *   fq_acc_stats_offset(k)        Stats block k in {0 pre-R1, 1 pre-R2, 2 post-R1, 3 post-R2}:
+ *        +FQ_ST_READS, +FQ_ST_LENGTH_SUM, +FQ_ST_Q20, +FQ_ST_Q30 then, from +FQ_ST_CYCLES,
+ *        [max_cycles][16] = per cycle 8 base-class counts (mCycleBaseContents[b][c], b = byte&7)
+ *        followed by 8 base-class quality sums (mCycleBaseQuality[b][c]).
+ * All counters are sums, so N engines (GPUs) combine by element-wise uint64 addition.
+ */
+#define FQ_ACC_FILTER 0
+#define FQ_ACC_ADAPTER_READS 32
+#define FQ_ACC_ADAPTER_BASES 33
+#define FQ_ACC_POLYX_READS 34
+#define FQ_ACC_POLYX_BASES 39
+#define FQ_ACC_MERGED_PAIRS 44
+#define FQ_ACC_INSERT 48
+#define FQ_ST_READS 0
+#define FQ_ST_LENGTH_SUM 1
+#define FQ_ST_Q20 2
+#define FQ_ST_Q30 3
+#define FQ_ST_CYCLES 16
+#define FQ_ST_PER_CYCLE 16
+
+static inline size_t fq_acc_stats_words(int32_t max_cycles) {
+    return (size_t)FQ_ST_CYCLES + (size_t)max_cycles * FQ_ST_PER_CYCLE;
+}
+static inline size_t fq_acc_stats_offset(int32_t insert_size_max, int32_t max_cycles, int k) {
+    size_t base = (size_t)FQ_ACC_INSERT + (size_t)(insert_size_max + 1);
+    base = (base + 15) & ~(size_t)15;
+    return base + (size_t)k * fq_acc_stats_words(max_cycles);
+}
+static inline size_t fq_acc_words(int32_t insert_size_max, int32_t max_cycles) {
+    return fq_acc_stats_offset(insert_size_max, max_cycles, 4);
+}
+
+/* ---- engine ------------------------------------------------------------------------- */
+typedef struct fq_engine fq_engine;
+
+/* fq_engine_create: validates params, selects `device` (hipSetDevice), allocates the device
+ * accumulator and staging buffers for packs of up to max_batch reads/pairs with rows of up to
+ * max_stride bytes.  Fails with FQ_E_NO_DEVICE when no gfx950 device is present. */
+int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int32_t max_stride,
+                     fq_engine** out);
+int fq_engine_destroy(fq_engine* e);
+
+/* Host-memory pack (the CLI path): H2D copy, kernels, D2H of the per-read results.
+ * `results` has n entries (SE) or 2n entries (PE: [2i] = read 1, [2i+1] = read 2).
+ * Synchronous; replaces one call of processPairEnd / processSingleEnd. */
+int fq_engine_process(fq_engine* e, const fq_batch* host_batch, fq_read_result* results);
+
+/* Device-resident pack (inputs already in HBM): enqueues the kernels on `stream`
+ * (a hipStream_t, NULL = the engine's stream) and returns without synchronising.
+ * `device_results` may be NULL when the caller needs only the accumulators. */
+int fq_engine_process_device(fq_engine* e, const fq_batch* device_batch,
+                             fq_read_result* device_results, void* stream);
+
+/* Accumulators */
+size_t fq_engine_acc_words(const fq_engine* e);
+int fq_engine_acc_device_ptr(fq_engine* e, uint64_t** dptr); /* for an RCCL all-reduce */
+int fq_engine_read_acc(fq_engine* e, uint64_t* host_acc, size_t words);
+int fq_engine_reset_acc(fq_engine* e);
+int fq_engine_sync(fq_engine* e);
+
+/* Last error message of this engine (or of the last failed create when e == NULL). */
+const char* fq_engine_last_error(const fq_engine* e);
+
+/* Device id the engine runs on; gfx arch name of that device. */
+int fq_engine_device_info(const fq_engine* e, int* device, char* arch, size_t arch_len);
+
+/* ---- synthetic workload ------------------------------------------------ *
+ * Fills a device-resident PE (seq2 != NULL) or SE batch with the seeded synthetic reads of
+ * the benchmark configs: counter-based (splitmix64 keyed on seed and global read index), so
+ * shards generate independently; `first_index` is the global index of the batch's first
+ * pair/read.  Lengths are written too.  Asynchronous on `stream`. */
+int fq_synth_fill_device(const fq_batch* device_batch, uint64_t seed, uint64_t first_index,
+                         int32_t read_len, void* stream);
+
+/* Kernel timing of the engine's last process_device call (HIP events on the launch stream),
+ * in milliseconds; 0 when unavailable. */
+double fq_engine_last_kernel_ms(const fq_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FQENGINE_H */
