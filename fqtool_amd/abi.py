@@ -154,6 +154,7 @@ def load_engine(path=ENGINE_LIB):
     lib.fq_engine_acc_device_ptr.argtypes = [vp, ctypes.POINTER(vp)]
     lib.fq_engine_read_acc.argtypes = [vp, vp, ctypes.c_size_t]
     lib.fq_engine_reset_acc.argtypes = [vp]
+    lib.fq_engine_set_acc_buffer.argtypes = [vp, vp]
     lib.fq_engine_sync.argtypes = [vp]
     lib.fq_engine_last_error.argtypes = [vp]
     lib.fq_engine_last_error.restype = ctypes.c_char_p
@@ -167,6 +168,6 @@ def load_engine(path=ENGINE_LIB):
 ENGINE_SYMBOLS = [
     "fq_engine_create", "fq_engine_destroy", "fq_engine_process", "fq_engine_process_device",
     "fq_engine_acc_words", "fq_engine_acc_device_ptr", "fq_engine_read_acc", "fq_engine_reset_acc",
-    "fq_engine_sync", "fq_engine_last_error", "fq_engine_device_info", "fq_synth_fill_device",
+    "fq_engine_sync", "fq_engine_set_acc_buffer", "fq_engine_last_error", "fq_engine_device_info", "fq_synth_fill_device",
     "fq_engine_last_kernel_ms",
 ]

@@ -1,0 +1,289 @@
+// device_ops.h -- per-read operations of the hot path as gfx950 device functions.
+//
+// Each function restates one reference function (file:line cited) on a read *view*: the
+// read's bytes stay where they are in HBM (row-major fq_batch rows) and trimming only moves
+// (start, len).  Quality bytes are signed char, as std::string's char on x86-64.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fqengine.h"
+
+namespace fqdev {
+
+struct View {
+    const uint8_t* s;  // row base: seq
+    const uint8_t* q;  // row base: qual
+    int start;         // surviving window [start, start+len)
+    int len;
+};
+
+// Accumulator layout of include/fqengine.h, usable in device code.
+__device__ __forceinline__ size_t acc_stats_words(int max_cycles) {
+    return (size_t)FQ_ST_CYCLES + (size_t)max_cycles * FQ_ST_PER_CYCLE;
+}
+__device__ __forceinline__ size_t acc_stats_offset(int insert_size_max, int max_cycles, int k) {
+    size_t base = (size_t)FQ_ACC_INSERT + (size_t)(insert_size_max + 1);
+    base = (base + 15) & ~(size_t)15;
+    return base + (size_t)k * acc_stats_words(max_cycles);
+}
+
+__device__ __forceinline__ int qv(const uint8_t* q, int i) { return (int)(int8_t)q[i]; }
+
+__device__ __forceinline__ uint8_t comp(uint8_t c) {
+    // Seq::reverseComplement, reference src/seq.h:24-48
+    switch (c) {
+        case 'A': case 'a': return 'T';
+        case 'T': case 't': return 'A';
+        case 'C': case 'c': return 'G';
+        case 'G': case 'g': return 'C';
+        default: return 'N';
+    }
+}
+
+// Filter::passFilter, reference src/filter.cpp:3-52
+__device__ inline int pass_filter(const fq_params& p, const uint8_t* seq, const uint8_t* qual, int rlen,
+                                  bool is_null) {
+    if (is_null || rlen == 0) return FQ_FAIL_LENGTH;
+    int low = 0, nb = 0, tq = 0;
+    if (p.qual_filter_enabled || p.length_filter_enabled) {
+        for (int i = 0; i < rlen; ++i) {
+            int q = qv(qual, i);
+            tq += q - 33;
+            nb += seq[i] == 'N';
+            low += q < p.low_qual_limit;
+        }
+    }
+    if (p.qual_filter_enabled) {
+        if (low > p.low_qual_base_limit) return FQ_FAIL_QUALITY;
+        if (p.avg_qual_limit > 0 && p.avg_qual_limit > (double)tq / rlen) return FQ_FAIL_QUALITY;
+    }
+    if (p.qual_filter_enabled && nb > p.n_base_limit) return FQ_FAIL_N_BASE;
+    if (p.length_filter_enabled) {
+        if (rlen < p.min_len) return FQ_FAIL_LENGTH;
+        if (p.max_len > 0 && rlen > p.max_len) return FQ_FAIL_TOO_LONG;
+    }
+    if (p.complexity_enabled) {  // Filter::passLowComplexityFliter, src/filter.cpp:54-67
+        bool ok = false;
+        if (rlen > 1) {
+            int diff = 0;
+            for (int i = 0; i < rlen - 1; ++i) diff += seq[i] != seq[i + 1];
+            ok = (double)diff / (rlen - 1) >= p.complexity_threshold;
+        }
+        if (!ok) return FQ_FAIL_COMPLEXITY;
+    }
+    return FQ_PASS_FILTER;
+}
+
+// (double)T/(double)w >= X  <=>  T >= X*w for integer T, X and 1 <= w <= 1000 (the quotient is
+// correctly rounded and X - 1/w is never rounded up to X), so the sliding windows of
+// Filter::trimAndCut are evaluated exactly in integers.
+__device__ __forceinline__ bool win_ge(int total, int w, int x) { return total >= x * w; }
+
+// Filter::trimAndCut, reference src/filter.cpp:69-189. Returns false for NULL.
+__device__ inline bool trim_and_cut(const fq_params& p, const uint8_t* seq, const uint8_t* qual, int l,
+                                    int front, int tail, int& out_start, int& out_len) {
+    const bool enF = p.cut_front, enR = p.cut_right, enT = p.cut_tail;
+    if (front == 0 && tail == 0 && !enF && !enR && !enT) {
+        out_start = 0;
+        out_len = l;
+        return true;
+    }
+    int rlen = l - front - tail;
+    if (rlen < 0) return false;
+    if (!enF && !enR && !enT) {
+        out_start = front;  // resize(rlen) when front == 0, else substr(front, rlen)
+        out_len = rlen;
+        return true;
+    }
+    if (enF) {
+        const int w = p.cut_front_window, thr = 33 + p.cut_front_quality;
+        int s = front;
+        if (l - front - tail - w <= 0) return false;
+        int tot = 0;
+        for (int i = 0; i < w - 1; ++i) tot += qv(qual, s + i);
+        for (s = front; s + w < l - tail; ++s) {
+            tot += qv(qual, s + w - 1);
+            if (s > front) tot -= qv(qual, s - 1);
+            if (win_ge(tot, w, thr)) break;
+        }
+        if (s > 0) s = s + w - 1;
+        while (s < l && seq[s] == 'N') ++s;
+        front = s;
+        rlen = l - front - tail;
+    }
+    if (enR) {
+        const int w = p.cut_right_window, thr = 33 + p.cut_right_quality;
+        int s = front;
+        if (l - front - tail - w <= 0) return false;
+        int tot = 0;
+        bool found = false;
+        for (int i = 0; i < w - 1; ++i) tot += qv(qual, s + i);
+        for (s = front; s + w < l - tail; ++s) {
+            tot += qv(qual, s + w - 1);
+            if (s > front) tot -= qv(qual, s - 1);
+            if (!win_ge(tot, w, thr)) {
+                found = true;
+                break;
+            }
+        }
+        if (found) {
+            while (s < l - 1 && qv(qual, s) >= thr) ++s;
+            rlen = s - front;
+        }
+    }
+    if (!enR && enT) {
+        const int w = p.cut_tail_window, thr = 33 + p.cut_tail_quality;
+        if (l - front - tail - w <= 0) return false;
+        int tot = 0;
+        int t = l - tail - 1;
+        for (int i = 0; i < w - 1; ++i) tot += qv(qual, t - i);
+        for (t = l - tail - 1; t - w >= front; --t) {
+            tot += qv(qual, t - w + 1);
+            if (t < l - tail - 1) tot -= qv(qual, t + 1);
+            if (win_ge(tot, w, thr)) break;
+        }
+        if (t < l - 1) t = t - w + 1;
+        while (t >= 0 && seq[t] == 'N') --t;
+        rlen = t - front + 1;
+    }
+    if (rlen <= 0 || front >= l - 1) return false;
+    out_start = front;
+    out_len = min(rlen, l - front);
+    return true;
+}
+
+// PolyX::trimPolyG, reference src/polyx.cpp:14-38. Returns new length; bases < 0: not recorded.
+__device__ inline int trim_polyg(const uint8_t* d, int rlen, int compareReq, int maxMM, int per, int& bases) {
+    int mismatch = 0, i = 0, firstG = rlen - 1;
+    for (i = 0; i < rlen; ++i) {
+        if (d[rlen - i - 1] != 'G') ++mismatch;
+        else firstG = rlen - i - 1;
+        int allowed = min(maxMM, max(1, (i + 1) / per));
+        if (mismatch > allowed) break;
+    }
+    bases = -1;
+    if (i + 1 >= compareReq) {
+        bases = rlen - firstG;
+        return (firstG > rlen || firstG < 0) ? rlen : firstG;  // Read::resize, src/read.h:181-187
+    }
+    return rlen;
+}
+
+// PolyX::trimPolyX, reference src/polyx.cpp:45-101
+__device__ inline int trim_polyx(const uint8_t* d, int rlen, int mask, int compareReq, int maxMM, int per,
+                                 int& poly_out, int& bases) {
+    int cnt[5] = {0, 0, 0, 0, 0};
+    int pos = 0;
+    for (pos = 0; pos < rlen; ++pos) {
+        uint8_t c = d[rlen - 1 - pos];
+        int k = c == 'A' ? 0 : c == 'T' ? 1 : c == 'C' ? 2 : c == 'G' ? 3 : 4;
+#pragma unroll
+        for (int b = 0; b < 5; ++b) cnt[b] += (k == b);
+        int cmp = pos + 1;
+        int allowed = min(maxMM, max(1, cmp / per));
+        bool brk = true;
+#pragma unroll
+        for (int b = 0; b < 5; ++b)
+            if (((mask >> b) & 1) && cmp - cnt[b] <= allowed) brk = false;
+        if (brk) break;
+    }
+    poly_out = -1;
+    bases = 0;
+    if (pos + 1 >= compareReq) {
+        int poly = 0, maxCount = -1;
+#pragma unroll
+        for (int b = 0; b < 5; ++b)
+            if (((mask >> b) & 1) && cnt[b] > maxCount) {
+                maxCount = cnt[b];
+                poly = b;
+            }
+        const uint8_t polyBase = poly == 0 ? 'A' : poly == 1 ? 'T' : poly == 2 ? 'C' : poly == 3 ? 'G' : 'N';
+        pos = min(rlen - 1, pos);
+        while (pos > 0 && d[rlen - pos - 1] != polyBase) --pos;
+        int target = rlen - pos - 1;
+        poly_out = poly;
+        bases = pos + 1;
+        return (target > rlen || target < 0) ? rlen : target;
+    }
+    return rlen;
+}
+
+struct Overlap {
+    int overlapped, offset, len, diff;
+};
+
+// OverlapAnalysis::analyze, reference src/overlapanalysis.cpp:7-72, on views.
+// revcomp(s2)[i] = comp(s2[len2-1-i]) is formed on the fly.
+__device__ inline Overlap analyze(const uint8_t* s1, int len1, const uint8_t* s2, int len2, int limit,
+                                  int require) {
+    const int ccr = 50;
+    Overlap r;
+    for (int offset = 0; offset < len1 - require; ++offset) {
+        int ol = min(len1 - offset, len2);
+        int diff = 0, i = 0;
+        for (i = 0; i < ol; ++i) {
+            if (s1[offset + i] != comp(s2[len2 - 1 - i])) {
+                ++diff;
+                if (diff >= limit && i < ccr) break;
+            }
+        }
+        if (diff < limit || (diff >= limit && i > ccr)) {
+            r.overlapped = 1;
+            r.offset = offset;
+            r.len = ol;
+            r.diff = diff;
+            return r;
+        }
+    }
+    for (int offset = 0; offset > require - len2; --offset) {
+        int ol = min(len1, len2 + offset);
+        int diff = 0, i = 0;
+        for (i = 0; i < ol; ++i) {
+            if (s1[i] != comp(s2[len2 - 1 - (i - offset)])) {
+                ++diff;
+                if (diff >= limit && i < ccr) break;
+            }
+        }
+        if (diff < limit || (diff >= limit && i > ccr)) {
+            r.overlapped = 1;
+            r.offset = offset;
+            r.len = ol;
+            r.diff = diff;
+            return r;
+        }
+    }
+    r.overlapped = r.offset = r.len = r.diff = 0;
+    return r;
+}
+
+// AdapterTrimmer::trimBySequence search, reference src/adaptertrimmer.cpp:29-90
+__device__ inline bool trim_by_sequence(const uint8_t* r, int rlen, const uint8_t* ad, int alen, int& pos_out) {
+    if (alen < 4) return false;
+    int start = 0;
+    if (alen >= 16) start = -4;
+    else if (alen >= 12) start = -3;
+    else if (alen >= 8) start = -2;
+    for (int pos = start; pos < rlen - 4; ++pos) {
+        int cmplen = min(rlen - pos, alen);
+        int allowed = cmplen / 8;
+        int mm = 0;
+        bool matched = true;
+        for (int i = max(0, -pos); i < cmplen; ++i) {
+            if (ad[i] != r[i + pos]) {
+                if (++mm > allowed) {
+                    matched = false;
+                    break;
+                }
+            }
+        }
+        if (matched) {
+            pos_out = pos;
+            return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace fqdev

@@ -1,0 +1,276 @@
+// engine.hip -- the C-ABI (include/fqengine.h) over the gfx950 kernels.
+//
+// No CPU fallback: creation fails with FQ_E_NO_DEVICE unless a gfx950 device is present.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "engine_internal.h"
+
+struct fq_engine {
+    fq_params p;
+    int device = 0;
+    int cus = 0;
+    char arch[64] = {0};
+    int32_t max_batch = 0, max_stride = 0;
+    hipStream_t stream = nullptr;
+    unsigned long long* acc = nullptr;      // accumulator in use
+    unsigned long long* own_acc = nullptr;  // the engine's own buffer
+    size_t acc_words = 0;
+    int* err = nullptr;
+    // staging for the host-memory path
+    uint8_t* d_rows = nullptr;  // 4 x max_batch x max_stride
+    uint16_t* d_lens = nullptr;  // 2 x max_batch
+    fq_read_result* d_res = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string last_error;
+};
+
+static std::string g_create_error;
+
+static int fail(fq_engine* e, int code, const std::string& msg) {
+    if (e) e->last_error = msg;
+    else g_create_error = msg;
+    return code;
+}
+
+static int hip_fail(fq_engine* e, hipError_t err, const char* what) {
+    return fail(e, FQ_E_HIP, std::string(what) + ": " + hipGetErrorString(err));
+}
+
+#define HIP_TRY(e, call)                                       \
+    do {                                                       \
+        hipError_t _err = (call);                              \
+        if (_err != hipSuccess) return hip_fail(e, _err, #call); \
+    } while (0)
+
+static int validate_params(const fq_params* p, std::string& why) {
+    if (p->max_cycles < 1 || p->max_cycles > 4096) return why = "max_cycles must be in [1, 4096]", FQ_E_INVALID;
+    if (p->insert_size_max < 0 || p->insert_size_max > 100000) return why = "bad insert_size_max", FQ_E_INVALID;
+    if (p->cut_front && p->cut_front_window < 1) return why = "cut_front window must be >= 1", FQ_E_INVALID;
+    if (p->cut_right && p->cut_right_window < 1) return why = "cut_right window must be >= 1", FQ_E_INVALID;
+    if (p->cut_tail && p->cut_tail_window < 1) return why = "cut_tail window must be >= 1", FQ_E_INVALID;
+    if (p->polyg_enabled && p->polyg_one_mismatch_per < 1) return why = "polyG one-mismatch-per must be >= 1", FQ_E_INVALID;
+    if (p->polyx_enabled && p->polyx_one_mismatch_per < 1) return why = "polyX one-mismatch-per must be >= 1", FQ_E_INVALID;
+    if (p->adapter1_len < 0 || p->adapter1_len > FQ_MAX_ADAPTER || p->adapter2_len < 0 ||
+        p->adapter2_len > FQ_MAX_ADAPTER)
+        return why = "bad adapter length", FQ_E_INVALID;
+    return FQ_OK;
+}
+
+extern "C" {
+
+int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int32_t max_stride, fq_engine** out) {
+    if (!params || !out || max_batch < 0 || max_stride < 0 || (max_stride & 15))
+        return fail(nullptr, FQ_E_INVALID, "fq_engine_create: bad arguments (stride must be a multiple of 16)");
+    *out = nullptr;
+    std::string why;
+    if (validate_params(params, why) != FQ_OK) return fail(nullptr, FQ_E_INVALID, why);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(nullptr, FQ_E_NO_DEVICE, "no HIP device visible (the engine has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(nullptr, FQ_E_NO_DEVICE, "device id out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return fail(nullptr, FQ_E_NO_DEVICE, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, FQ_E_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", engine is built for gfx950");
+    fq_engine* e = new fq_engine();
+    e->p = *params;
+    e->device = device;
+    e->cus = prop.multiProcessorCount;
+    std::snprintf(e->arch, sizeof e->arch, "%s", prop.gcnArchName);
+    e->max_batch = max_batch;
+    e->max_stride = max_stride;
+    e->acc_words = fq_acc_words(params->insert_size_max, params->max_cycles);
+    auto bail = [&](int rc) {
+        g_create_error = e->last_error;
+        fq_engine_destroy(e);
+        return rc;
+    };
+    hipError_t he;
+    if ((he = hipSetDevice(device)) != hipSuccess) return bail(hip_fail(e, he, "hipSetDevice"));
+    if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess)
+        return bail(hip_fail(e, he, "hipStreamCreate"));
+    if ((he = hipMalloc(&e->own_acc, e->acc_words * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc acc"));
+    e->acc = e->own_acc;
+    if ((he = hipMalloc(&e->err, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc err"));
+    if ((he = hipMemset(e->acc, 0, e->acc_words * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
+    if ((he = hipMemset(e->err, 0, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
+    if (max_batch > 0 && max_stride > 0) {
+        const size_t rows = (size_t)4 * max_batch * max_stride;
+        if ((he = hipMalloc(&e->d_rows, rows)) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc rows"));
+        if ((he = hipMalloc(&e->d_lens, (size_t)2 * max_batch * sizeof(uint16_t))) != hipSuccess)
+            return bail(hip_fail(e, he, "hipMalloc lens"));
+        if ((he = hipMalloc(&e->d_res, (size_t)2 * max_batch * sizeof(fq_read_result))) != hipSuccess)
+            return bail(hip_fail(e, he, "hipMalloc results"));
+    }
+    if ((he = hipEventCreate(&e->ev0)) != hipSuccess) return bail(hip_fail(e, he, "hipEventCreate"));
+    if ((he = hipEventCreate(&e->ev1)) != hipSuccess) return bail(hip_fail(e, he, "hipEventCreate"));
+    if (fq_pack_kernel_lds_bytes(e->p) > 160 * 1024)
+        return bail(fail(e, FQ_E_INVALID, "max_cycles too large for the LDS-privatised accumulators"));
+    if ((he = fq_pack_kernel_set_lds(e->p)) != hipSuccess) return bail(hip_fail(e, he, "hipFuncSetAttribute"));
+    *out = e;
+    return FQ_OK;
+}
+
+int fq_engine_destroy(fq_engine* e) {
+    if (!e) return FQ_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->own_acc) (void)hipFree(e->own_acc);
+    if (e->err) (void)hipFree(e->err);
+    if (e->d_rows) (void)hipFree(e->d_rows);
+    if (e->d_lens) (void)hipFree(e->d_lens);
+    if (e->d_res) (void)hipFree(e->d_res);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return FQ_OK;
+}
+
+static int grid_for(const fq_engine* e, int n) {
+    const size_t lds = fq_pack_kernel_lds_bytes(e->p);
+    int per_cu = (int)((160 * 1024) / (lds ? lds : 1));
+    if (per_cu < 1) per_cu = 1;
+    if (per_cu > 8) per_cu = 8;
+    const int cap = e->cus * per_cu;
+    const int need = (n + 255) / 256;
+    return need < cap ? (need > 0 ? need : 1) : cap;
+}
+
+static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStream_t s) {
+    if (db.n <= 0) return FQ_OK;
+    HIP_TRY(e, hipEventRecord(e->ev0, s));
+    HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, grid_for(e, db.n), s));
+    HIP_TRY(e, hipEventRecord(e->ev1, s));
+    e->timed = true;
+    return FQ_OK;
+}
+
+static int check_err(fq_engine* e) {
+    int h = 0;
+    HIP_TRY(e, hipMemcpy(&h, e->err, sizeof(int), hipMemcpyDeviceToHost));
+    if (h) {
+        HIP_TRY(e, hipMemset(e->err, 0, sizeof(int)));
+        return fail(e, FQ_E_TOO_LONG, "a read is longer than max_cycles or the row stride");
+    }
+    return FQ_OK;
+}
+
+int fq_engine_process(fq_engine* e, const fq_batch* hb, fq_read_result* results) {
+    if (!e || !hb || !results) return FQ_E_INVALID;
+    const bool pe = e->p.paired;
+    if (hb->n < 0 || hb->n > e->max_batch || hb->stride <= 0 || hb->stride > e->max_stride || (hb->stride & 15))
+        return fail(e, FQ_E_INVALID, "batch exceeds the engine's max_batch/max_stride (or stride % 16 != 0)");
+    if (!hb->seq1 || !hb->qual1 || !hb->len1 || (pe && (!hb->seq2 || !hb->qual2 || !hb->len2)))
+        return fail(e, FQ_E_INVALID, "missing batch arrays");
+    for (int i = 0; i < hb->n; ++i) {
+        if (hb->len1[i] > e->p.max_cycles || hb->len1[i] > hb->stride ||
+            (pe && (hb->len2[i] > e->p.max_cycles || hb->len2[i] > hb->stride)))
+            return fail(e, FQ_E_TOO_LONG, "read longer than max_cycles / stride");
+    }
+    HIP_TRY(e, hipSetDevice(e->device));
+    const size_t rowbytes = (size_t)hb->n * hb->stride;
+    const size_t plane = (size_t)e->max_batch * e->max_stride;
+    fq_batch db;
+    db.n = hb->n;
+    db.stride = hb->stride;
+    db.seq1 = e->d_rows;
+    db.qual1 = e->d_rows + plane;
+    db.len1 = e->d_lens;
+    db.seq2 = pe ? e->d_rows + 2 * plane : nullptr;
+    db.qual2 = pe ? e->d_rows + 3 * plane : nullptr;
+    db.len2 = pe ? e->d_lens + e->max_batch : nullptr;
+    hipStream_t s = e->stream;
+    HIP_TRY(e, hipMemcpyAsync((void*)db.seq1, hb->seq1, rowbytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(e, hipMemcpyAsync((void*)db.qual1, hb->qual1, rowbytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(e, hipMemcpyAsync((void*)db.len1, hb->len1, (size_t)hb->n * 2, hipMemcpyHostToDevice, s));
+    if (pe) {
+        HIP_TRY(e, hipMemcpyAsync((void*)db.seq2, hb->seq2, rowbytes, hipMemcpyHostToDevice, s));
+        HIP_TRY(e, hipMemcpyAsync((void*)db.qual2, hb->qual2, rowbytes, hipMemcpyHostToDevice, s));
+        HIP_TRY(e, hipMemcpyAsync((void*)db.len2, hb->len2, (size_t)hb->n * 2, hipMemcpyHostToDevice, s));
+    }
+    int rc = launch(e, db, e->d_res, s);
+    if (rc != FQ_OK) return rc;
+    const size_t nres = (size_t)hb->n * (pe ? 2 : 1);
+    HIP_TRY(e, hipMemcpyAsync(results, e->d_res, nres * sizeof(fq_read_result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(e, hipStreamSynchronize(s));
+    return check_err(e);
+}
+
+int fq_engine_process_device(fq_engine* e, const fq_batch* db, fq_read_result* dres, void* stream) {
+    if (!e || !db) return FQ_E_INVALID;
+    if (db->n < 0 || db->stride <= 0 || (db->stride & 15) || !db->seq1 || !db->qual1 || !db->len1 ||
+        (e->p.paired && (!db->seq2 || !db->qual2 || !db->len2)))
+        return fail(e, FQ_E_INVALID, "bad device batch");
+    HIP_TRY(e, hipSetDevice(e->device));
+    return launch(e, *db, dres, stream ? (hipStream_t)stream : e->stream);
+}
+
+size_t fq_engine_acc_words(const fq_engine* e) { return e ? e->acc_words : 0; }
+
+int fq_engine_acc_device_ptr(fq_engine* e, uint64_t** dptr) {
+    if (!e || !dptr) return FQ_E_INVALID;
+    *dptr = reinterpret_cast<uint64_t*>(e->acc);
+    return FQ_OK;
+}
+
+int fq_engine_read_acc(fq_engine* e, uint64_t* host, size_t words) {
+    if (!e || !host || words < e->acc_words) return FQ_E_INVALID;
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());
+    HIP_TRY(e, hipMemcpy(host, e->acc, e->acc_words * 8, hipMemcpyDeviceToHost));
+    return check_err(e);
+}
+
+int fq_engine_set_acc_buffer(fq_engine* e, uint64_t* device_acc) {
+    if (!e) return FQ_E_INVALID;
+    e->acc = device_acc ? reinterpret_cast<unsigned long long*>(device_acc) : e->own_acc;
+    return FQ_OK;
+}
+
+int fq_engine_reset_acc(fq_engine* e) {
+    if (!e) return FQ_E_INVALID;
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipMemsetAsync(e->acc, 0, e->acc_words * 8, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return FQ_OK;
+}
+
+int fq_engine_sync(fq_engine* e) {
+    if (!e) return FQ_E_INVALID;
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());
+    return check_err(e);
+}
+
+const char* fq_engine_last_error(const fq_engine* e) { return e ? e->last_error.c_str() : g_create_error.c_str(); }
+
+int fq_engine_device_info(const fq_engine* e, int* device, char* arch, size_t arch_len) {
+    if (!e) return FQ_E_INVALID;
+    if (device) *device = e->device;
+    if (arch && arch_len) std::snprintf(arch, arch_len, "%s", e->arch);
+    return FQ_OK;
+}
+
+int fq_synth_fill_device(const fq_batch* db, uint64_t seed, uint64_t first_index, int32_t read_len, void* stream) {
+    if (!db || read_len <= 0 || read_len > db->stride || !db->seq1 || !db->qual1 || !db->len1)
+        return FQ_E_INVALID;
+    hipError_t he = fq_launch_synth(*db, seed, first_index, read_len, (hipStream_t)stream);
+    return he == hipSuccess ? FQ_OK : FQ_E_HIP;
+}
+
+double fq_engine_last_kernel_ms(const fq_engine* e) {
+    if (!e || !e->timed) return 0.0;
+    float ms = 0.f;
+    if (hipEventSynchronize(e->ev1) != hipSuccess) return 0.0;
+    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) != hipSuccess) return 0.0;
+    return ms;
+}
+
+}  // extern "C"

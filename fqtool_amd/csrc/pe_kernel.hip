@@ -1,0 +1,384 @@
+// pe_kernel.hip -- the per-pack hot path on gfx950.
+//
+// One lane owns one pair (PE) or one read (SE) and runs the loop body of
+// PairEndProcessor::processPairEnd (reference src/peprocessor.cpp:261-508) /
+// SingleEndProcessor::processSingleEnd (src/seprocessor.cpp:290-388) on read *views* over the
+// row-major batch in HBM; trimming only moves (start, len), nothing is copied.
+//
+// Accumulation (the ThreadConfig-owned Stats x4 + FilterResult and the insert histogram):
+// every workgroup privatises all counters in LDS and flushes them once with 64-bit global
+// atomics.  The per-cycle Stats histograms are [stats][cycle][17] u32 (8 base-class counts +
+// 8 base-class quality sums biased by +128 so partial sums never go negative, padded to 17
+// words so consecutive cycles land on different banks); each lane walks its read starting at a
+// lane-dependent rotation, so the 64 lanes of a wave update 64 different cycles per step.
+#include <hip/hip_runtime.h>
+
+#include "device_ops.h"
+#include "engine_internal.h"
+
+using namespace fqdev;
+
+namespace {
+
+constexpr int kRec = 17;  // LDS words per (stats, cycle) record
+
+struct Smem {
+    uint32_t* hist;         // [4][C][17]
+    unsigned long long* c;  // small u64 counters, indexed like the global accumulator head
+    unsigned long long* scal;  // [4][4] reads, length_sum, q20, q30
+};
+
+__device__ __forceinline__ void lds_add64(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
+
+// Stats::statRead, reference src/stats.cpp:237-295, on a window of a row (cycle i = data[i]).
+template <typename Fetch>
+__device__ inline void stat_read(uint32_t* hist, unsigned long long* scal, int len, int skew, Fetch fetch) {
+    if (len <= 0) {
+        lds_add64(&scal[0], 1ull);
+        return;
+    }
+    int rot = skew % len;
+    uint32_t q20 = 0, q30 = 0;
+    for (int i = 0; i < len; ++i) {
+        int c = i + rot;
+        if (c >= len) c -= len;
+        uint8_t b;
+        int q;
+        fetch(c, b, q);
+        const int cls = b & 7;
+        q20 += q > '5';
+        q30 += q > '?';
+        uint32_t* rec = hist + c * kRec;
+        atomicAdd(&rec[cls], 1u);
+        atomicAdd(&rec[8 + cls], (uint32_t)(q + 128));
+    }
+    lds_add64(&scal[0], 1ull);
+    lds_add64(&scal[1], (unsigned long long)len);
+    lds_add64(&scal[2], (unsigned long long)q20);
+    lds_add64(&scal[3], (unsigned long long)q30);
+}
+
+__device__ __forceinline__ void row_stat(const Smem& sm, int k, int C, const uint8_t* s, const uint8_t* q,
+                                         int len, int skew) {
+    stat_read(sm.hist + (size_t)k * C * kRec, sm.scal + 4 * k, len, skew, [&](int i, uint8_t& b, int& qq) {
+        b = s[i];
+        qq = qv(q, i);
+    });
+}
+
+__device__ __forceinline__ void store_result(fq_read_result* out, const fq_read_result& r) {
+    *reinterpret_cast<uint4*>(out) = *reinterpret_cast<const uint4*>(&r);
+}
+
+__device__ __forceinline__ fq_read_result make_result(bool nonnull, int start, int len) {
+    fq_read_result r;
+    r.start = nonnull ? (uint16_t)start : 0;
+    r.len = nonnull ? (uint16_t)len : 0;
+    r.code = 0;
+    r.flags = nonnull ? 0 : FQ_RF_NULL;
+    r.ad_pos = r.ad_len = r.m_len1 = r.m_len2 = r.reserved = 0;
+    return r;
+}
+
+__device__ inline void apply_polyg(const fq_params& p, const Smem& sm, const uint8_t* s, int st, int& n) {
+    int bases;
+    n = trim_polyg(s + st, n, p.polyg_compare_req, p.polyg_max_mismatch, p.polyg_one_mismatch_per, bases);
+    if (bases >= 0) {
+        lds_add64(&sm.c[FQ_ACC_POLYX_READS + 3], 1ull);
+        lds_add64(&sm.c[FQ_ACC_POLYX_BASES + 3], (unsigned long long)(long long)bases);
+    }
+}
+
+__device__ inline void apply_polyx(const fq_params& p, const Smem& sm, const uint8_t* s, int st, int& n) {
+    int poly, bases;
+    n = trim_polyx(s + st, n, p.polyx_mask, p.polyx_compare_req, p.polyx_max_mismatch, p.polyx_one_mismatch_per,
+                   poly, bases);
+    if (poly >= 0) {
+        lds_add64(&sm.c[FQ_ACC_POLYX_READS + poly], 1ull);
+        lds_add64(&sm.c[FQ_ACC_POLYX_BASES + poly], (unsigned long long)(long long)bases);
+    }
+}
+
+__device__ inline void apply_adapter_seq(const Smem& sm, const uint8_t* s, int st, int& n, const uint8_t* ad,
+                                         int alen, fq_read_result& rr) {
+    int pos;
+    if (!trim_by_sequence(s + st, n, ad, alen, pos)) return;
+    int ad_len;
+    if (pos < 0) {
+        ad_len = alen + pos;
+        rr.flags |= FQ_RF_AD_SEQ | FQ_RF_AD_NEG;
+        rr.ad_pos = (uint16_t)(-pos);
+        n = 0;
+    } else {
+        ad_len = n - pos;
+        rr.flags |= FQ_RF_AD_SEQ;
+        rr.ad_pos = (uint16_t)(st + pos);
+        n = pos;
+    }
+    rr.ad_len = (uint16_t)ad_len;
+    if (ad_len > 0) {  // FilterResult::addAdapterTrimmed(str, isR2), src/filterresult.cpp:138-157
+        lds_add64(&sm.c[FQ_ACC_ADAPTER_READS], 1ull);
+        lds_add64(&sm.c[FQ_ACC_ADAPTER_BASES], (unsigned long long)ad_len);
+    }
+}
+
+template <bool PAIRED>
+__global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
+                                                      unsigned long long* __restrict__ acc, int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int C = p.max_cycles;
+    const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
+    Smem sm;
+    sm.c = reinterpret_cast<unsigned long long*>(lds);
+    sm.scal = sm.c + ((nsmall + 1) & ~1);
+    sm.hist = reinterpret_cast<uint32_t*>(sm.scal + 16);
+    const int total_words = 2 * (((nsmall + 1) & ~1) + 16) + 4 * C * kRec;
+    for (int i = threadIdx.x; i < total_words; i += blockDim.x) lds[i] = 0;
+    __syncthreads();
+
+    const int skew = threadIdx.x & 63;
+    const size_t stride = (size_t)b.stride;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < b.n; idx += gridDim.x * blockDim.x) {
+        const uint8_t* s1 = b.seq1 + idx * stride;
+        const uint8_t* q1 = b.qual1 + idx * stride;
+        const int l1 = b.len1[idx];
+        if (!PAIRED) {
+            if (l1 > C || l1 > b.stride) {
+                atomicOr(err, 1);
+                continue;
+            }
+            row_stat(sm, 0, C, s1, q1, l1, skew);  // src/seprocessor.cpp:298
+            int st = 0, n = 0;
+            bool nn = trim_and_cut(p, s1, q1, l1, p.trim_front1, p.trim_tail1, st, n);
+            fq_read_result rr = make_result(nn, st, n);
+            if (nn && p.polyg_enabled) apply_polyg(p, sm, s1, st, n);
+            if (nn && p.adapter_trimming && p.adapter1_len > 0) apply_adapter_seq(sm, s1, st, n, p.adapter1, p.adapter1_len, rr);
+            if (nn && p.polyx_enabled) apply_polyx(p, sm, s1, st, n);
+            if (nn && p.max_len1 > 0 && p.max_len1 < n) n = p.max_len1;
+            const int code = pass_filter(p, s1 + st, q1 + st, n, !nn);
+            lds_add64(&sm.c[FQ_ACC_FILTER + code], 1ull);
+            if (nn && code == FQ_PASS_FILTER) row_stat(sm, 2, C, s1 + st, q1 + st, n, skew);
+            rr.start = nn ? (uint16_t)st : 0;
+            rr.len = nn ? (uint16_t)n : 0;
+            rr.code = (uint8_t)code;
+            if (res) store_result(&res[idx], rr);
+            continue;
+        }
+        const uint8_t* s2 = b.seq2 + idx * stride;
+        const uint8_t* q2 = b.qual2 + idx * stride;
+        const int l2 = b.len2[idx];
+        if (l1 > C || l2 > C || l1 > b.stride || l2 > b.stride) {
+            atomicOr(err, 1);
+            continue;
+        }
+        row_stat(sm, 0, C, s1, q1, l1, skew);  // src/peprocessor.cpp:276-277
+        row_stat(sm, 1, C, s2, q2, l2, skew);
+        int st1 = 0, n1 = 0, st2 = 0, n2 = 0;  // :292-293
+        const bool nn1 = trim_and_cut(p, s1, q1, l1, p.trim_front1, p.trim_tail1, st1, n1);
+        const bool nn2 = trim_and_cut(p, s2, q2, l2, p.trim_front2, p.trim_tail2, st2, n2);
+        fq_read_result r1 = make_result(nn1, st1, n1), r2 = make_result(nn2, st2, n2);
+        const bool both = nn1 && nn2;
+        if (both && p.polyg_enabled) {  // :295-299
+            apply_polyg(p, sm, s1, st1, n1);
+            apply_polyg(p, sm, s2, st2, n2);
+        }
+        if (both) {  // :302-333 -- insert size for every pair (reference with -w 1)
+            Overlap ov = analyze(s1 + st1, n1, s2 + st2, n2, p.overlap_diff_limit, p.overlap_require);
+            int isize = p.insert_size_max;  // :510-523
+            if (ov.overlapped) isize = ov.offset > 0 ? n1 + n2 - ov.len : ov.len;
+            if (isize > p.insert_size_max) isize = p.insert_size_max;
+            lds_add64(&sm.c[FQ_ACC_INSERT + isize], 1ull);
+            if (p.adapter_trimming) {
+                const int ol = ov.len;  // AdapterTrimmer::trimByOverlapAnalysis, src/adaptertrimmer.cpp:14-27
+                if (ov.diff <= 5 && ov.overlapped && ov.offset < 0 && ol > n1 / 3) {
+                    r1.flags |= FQ_RF_AD_OVERLAP;
+                    r1.ad_pos = (uint16_t)(st1 + ol);
+                    r1.ad_len = (uint16_t)(n1 - ol);
+                    r2.flags |= FQ_RF_AD_OVERLAP;
+                    r2.ad_pos = (uint16_t)(st2 + ol);
+                    r2.ad_len = (uint16_t)(n2 - ol);
+                    lds_add64(&sm.c[FQ_ACC_ADAPTER_READS], 2ull);
+                    lds_add64(&sm.c[FQ_ACC_ADAPTER_BASES], (unsigned long long)((n1 - ol) + (n2 - ol)));
+                    n1 = ol;
+                    n2 = ol;
+                } else {
+                    if (p.adapter1_len > 0) apply_adapter_seq(sm, s1, st1, n1, p.adapter1, p.adapter1_len, r1);
+                    if (p.adapter2_len > 0) apply_adapter_seq(sm, s2, st2, n2, p.adapter2, p.adapter2_len, r2);
+                }
+            }
+        }
+        if (both && p.polyx_enabled) {  // :335-340
+            apply_polyx(p, sm, s1, st1, n1);
+            apply_polyx(p, sm, s2, st2, n2);
+        }
+        if (both) {  // :342-349
+            if (p.max_len1 > 0 && p.max_len1 < n1) n1 = p.max_len1;
+            if (p.max_len2 > 0 && p.max_len2 < n2) n2 = p.max_len2;
+        }
+        bool mergeProcessed = false;
+        if (p.merge_enabled && both) {  // :351-385
+            Overlap ov = analyze(s1 + st1, n1, s2 + st2, n2, p.overlap_diff_limit, p.overlap_require);
+            if (ov.overlapped) {
+                r1.flags |= FQ_RF_OVERLAP | FQ_RF_MERGED;
+                int code = FQ_FAIL_LENGTH;  // OverlapAnalysis::merge returns NULL for overlapLen 0
+                if (ov.len) {
+                    const int ol = ov.len;
+                    int m1 = min(ol + max(0, ov.offset), n1);
+                    int m2 = ov.offset > 0 ? max(0, n2 - ol) : 0;
+                    r1.m_len1 = (uint16_t)m1;
+                    r1.m_len2 = (uint16_t)m2;
+                    const int mlen = m1 + m2;
+                    const uint8_t* a_s = s1 + st1;
+                    const uint8_t* a_q = q1 + st1;
+                    const uint8_t* b_s = s2 + st2;
+                    const uint8_t* b_q = q2 + st2;
+                    // merged base i: r1[i] for i < m1, else revcomp(r2)[ol + i - m1]
+                    auto fetch = [&](int i, uint8_t& bb, int& qq) {
+                        if (i < m1) {
+                            bb = a_s[i];
+                            qq = qv(a_q, i);
+                        } else {
+                            const int src = n2 - 1 - (ol + i - m1);
+                            bb = comp(b_s[src]);
+                            qq = qv(b_q, src);
+                        }
+                    };
+                    // Filter::passFilter on the merged read
+                    if (mlen == 0) {
+                        code = FQ_FAIL_LENGTH;
+                    } else {
+                        int low = 0, nb = 0, tq = 0;
+                        if (p.qual_filter_enabled || p.length_filter_enabled) {
+                            for (int i = 0; i < mlen; ++i) {
+                                uint8_t bb;
+                                int qq;
+                                fetch(i, bb, qq);
+                                tq += qq - 33;
+                                nb += bb == 'N';
+                                low += qq < p.low_qual_limit;
+                            }
+                        }
+                        code = FQ_PASS_FILTER;
+                        if (p.qual_filter_enabled && low > p.low_qual_base_limit) code = FQ_FAIL_QUALITY;
+                        else if (p.qual_filter_enabled && p.avg_qual_limit > 0 && p.avg_qual_limit > (double)tq / mlen)
+                            code = FQ_FAIL_QUALITY;
+                        else if (p.qual_filter_enabled && nb > p.n_base_limit) code = FQ_FAIL_N_BASE;
+                        else if (p.length_filter_enabled && mlen < p.min_len) code = FQ_FAIL_LENGTH;
+                        else if (p.length_filter_enabled && p.max_len > 0 && mlen > p.max_len) code = FQ_FAIL_TOO_LONG;
+                        else if (p.complexity_enabled) {
+                            bool ok = false;
+                            if (mlen > 1) {
+                                int diff = 0;
+                                uint8_t prev;
+                                int qq;
+                                fetch(0, prev, qq);
+                                for (int i = 1; i < mlen; ++i) {
+                                    uint8_t cur;
+                                    fetch(i, cur, qq);
+                                    diff += cur != prev;
+                                    prev = cur;
+                                }
+                                ok = (double)diff / (mlen - 1) >= p.complexity_threshold;
+                            }
+                            if (!ok) code = FQ_FAIL_COMPLEXITY;
+                        }
+                    }
+                    if (code == FQ_PASS_FILTER) {
+                        if (mlen > C) {
+                            atomicOr(err, 1);
+                        } else {
+                            stat_read(sm.hist + (size_t)2 * C * kRec, sm.scal + 8, mlen, skew, fetch);
+                            lds_add64(&sm.c[FQ_ACC_MERGED_PAIRS], 1ull);
+                        }
+                    }
+                }
+                lds_add64(&sm.c[FQ_ACC_FILTER + code], 2ull);
+                r1.code = r2.code = (uint8_t)code;
+                mergeProcessed = true;
+            } else if (!p.discard_unmerged) {
+                const int c1 = pass_filter(p, s1 + st1, q1 + st1, n1, false);
+                lds_add64(&sm.c[FQ_ACC_FILTER + c1], 1ull);
+                if (c1 == FQ_PASS_FILTER) row_stat(sm, 2, C, s1 + st1, q1 + st1, n1, skew);
+                const int c2 = pass_filter(p, s2 + st2, q2 + st2, n2, false);
+                lds_add64(&sm.c[FQ_ACC_FILTER + c2], 1ull);
+                if (c2 == FQ_PASS_FILTER) row_stat(sm, 3, C, s2 + st2, q2 + st2, n2, skew);
+                r1.code = (uint8_t)c1;
+                r2.code = (uint8_t)c2;
+                mergeProcessed = true;
+            }
+        }
+        if (!mergeProcessed) {  // :387-429
+            const int c1 = pass_filter(p, s1 + st1, q1 + st1, n1, !nn1);
+            const int c2 = pass_filter(p, s2 + st2, q2 + st2, n2, !nn2);
+            lds_add64(&sm.c[FQ_ACC_FILTER + max(c1, c2)], 2ull);
+            if (nn1 && c1 == FQ_PASS_FILTER && nn2 && c2 == FQ_PASS_FILTER && !p.merge_enabled) {
+                row_stat(sm, 2, C, s1 + st1, q1 + st1, n1, skew);
+                row_stat(sm, 3, C, s2 + st2, q2 + st2, n2, skew);
+            }
+            r1.code = (uint8_t)c1;
+            r2.code = (uint8_t)c2;
+        }
+        r1.start = nn1 ? (uint16_t)st1 : 0;
+        r1.len = nn1 ? (uint16_t)n1 : 0;
+        r2.start = nn2 ? (uint16_t)st2 : 0;
+        r2.len = nn2 ? (uint16_t)n2 : 0;
+        if (res) {
+            store_result(&res[2 * (size_t)idx], r1);
+            store_result(&res[2 * (size_t)idx + 1], r2);
+        }
+    }
+    __syncthreads();
+
+    // flush: small counters, stats scalars, per-cycle histograms
+    for (int i = threadIdx.x; i < nsmall; i += blockDim.x) {
+        unsigned long long v = sm.c[i];
+        if (v) atomicAdd(&acc[i], v);
+    }
+    const size_t st_base = acc_stats_offset(p.insert_size_max, C, 0);
+    const size_t st_words = acc_stats_words(C);
+    if (threadIdx.x < 16) {
+        const int k = threadIdx.x >> 2, f = threadIdx.x & 3;
+        unsigned long long v = sm.scal[threadIdx.x];
+        if (v) atomicAdd(&acc[st_base + k * st_words + f], v);
+    }
+    for (int i = threadIdx.x; i < 4 * C; i += blockDim.x) {
+        const int k = i / C, c = i - k * C;
+        const uint32_t* rec = sm.hist + (size_t)i * kRec;
+        unsigned long long* dst = acc + st_base + k * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const uint32_t cnt = rec[f];
+            if (cnt) {
+                atomicAdd(&dst[f], (unsigned long long)cnt);
+                const long long qsum = (long long)rec[8 + f] - 161ll * (long long)cnt;  // undo the +128 bias, -33
+                atomicAdd(&dst[8 + f], (unsigned long long)qsum);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+size_t fq_pack_kernel_lds_bytes(const fq_params& p) {
+    const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
+    return (size_t)(2 * (((nsmall + 1) & ~1) + 16) + 4 * p.max_cycles * kRec) * sizeof(uint32_t);
+}
+
+hipError_t fq_launch_pack_kernel(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
+                                 int* err, int grid, hipStream_t stream) {
+    const size_t lds = fq_pack_kernel_lds_bytes(p);
+    if (p.paired)
+        hipLaunchKernelGGL(fq_pack_kernel<true>, dim3(grid), dim3(256), lds, stream, p, b, res, acc, err);
+    else
+        hipLaunchKernelGGL(fq_pack_kernel<false>, dim3(grid), dim3(256), lds, stream, p, b, res, acc, err);
+    return hipGetLastError();
+}
+
+hipError_t fq_pack_kernel_set_lds(const fq_params& p) {
+    const size_t lds = fq_pack_kernel_lds_bytes(p);
+    hipError_t e = hipFuncSetAttribute((const void*)fq_pack_kernel<true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)fq_pack_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds);
+}

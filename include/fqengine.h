@@ -225,6 +225,10 @@ int fq_engine_process_device(fq_engine* e, const fq_batch* device_batch,
 size_t fq_engine_acc_words(const fq_engine* e);
 int fq_engine_acc_device_ptr(fq_engine* e, uint64_t** dptr); /* for an RCCL all-reduce */
 int fq_engine_read_acc(fq_engine* e, uint64_t* host_acc, size_t words);
+/* Use a caller-owned, zero-initialised device buffer of fq_engine_acc_words() uint64 words as
+ * the accumulator (e.g. a torch tensor that is then all-reduced over RCCL); NULL restores the
+ * engine's own buffer. */
+int fq_engine_set_acc_buffer(fq_engine* e, uint64_t* device_acc);
 int fq_engine_reset_acc(fq_engine* e);
 int fq_engine_sync(fq_engine* e);
 

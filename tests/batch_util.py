@@ -1,0 +1,174 @@
+"""Helpers shared by the parity tests: numpy-backed fq_batch packs and config presets."""
+import ctypes
+import random
+
+import numpy as np
+
+from fqtool_amd import abi
+
+AD1 = "AGATCGGAAGAGCACACGTCTGAACTCCAGTCA"
+AD2 = "AGATCGGAAGAGCGTCGTGTAGGGAAAGAGTGT"
+
+
+class Pack:
+    """Row-major pack: rows of `stride` bytes, like the engine's fq_batch."""
+
+    def __init__(self, n, stride, paired):
+        self.n, self.stride, self.paired = n, stride, paired
+        self.seq1 = np.zeros((n, stride), np.uint8)
+        self.qual1 = np.zeros((n, stride), np.uint8)
+        self.len1 = np.zeros(n, np.uint16)
+        if paired:
+            self.seq2 = np.zeros((n, stride), np.uint8)
+            self.qual2 = np.zeros((n, stride), np.uint8)
+            self.len2 = np.zeros(n, np.uint16)
+
+    def set(self, i, mate, seq, qual):
+        assert len(seq) == len(qual) <= self.stride
+        s = getattr(self, "seq%d" % mate)
+        q = getattr(self, "qual%d" % mate)
+        s[i, : len(seq)] = np.frombuffer(seq, np.uint8)
+        q[i, : len(qual)] = np.frombuffer(qual, np.uint8)
+        getattr(self, "len%d" % mate)[i] = len(seq)
+
+    def batch(self):
+        b = abi.FqBatch()
+        b.n, b.stride = self.n, self.stride
+        b.seq1, b.qual1, b.len1 = self.seq1.ctypes.data, self.qual1.ctypes.data, self.len1.ctypes.data
+        if self.paired:
+            b.seq2, b.qual2, b.len2 = self.seq2.ctypes.data, self.qual2.ctypes.data, self.len2.ctypes.data
+        return b
+
+    def result_array(self):
+        return np.zeros(self.n * (2 if self.paired else 1), dtype=np.dtype(abi.RESULT_DTYPE_FIELDS))
+
+
+def synth_pack(oracle, n, paired, seed=20261015, first=0, L=150, stride=160):
+    pk = Pack(n, stride, paired)
+    b = pk.batch()
+    oracle.orc_synth_fill(ctypes.byref(b), seed, first, L)
+    return pk
+
+
+def rand_read(rng, n):
+    seq = bytes(rng.choice(b"ACGTN" if rng.random() < 0.9 else b"ACGTNacgtRYK") for _ in range(n))
+    qual = bytes(33 + rng.randint(2, 41) if rng.random() > 0.02 else rng.choice([25, 32, 126, 200])
+                 for _ in range(n))
+    return seq, qual
+
+
+def edge_pack(n, paired, stride=160, seed=7):
+    """Ragged and hostile reads: empty, very short, all-N, exotic bytes, polyG runs, adapters."""
+    rng = random.Random(seed)
+    pk = Pack(n, stride, paired)
+    for i in range(n):
+        for m in ((1, 2) if paired else (1,)):
+            L = rng.choice([0, 1, 3, 4, 5, 10, 29, 30, 31, 49, 50, 51, 100, 149, 150, 151, stride])
+            seq, qual = rand_read(rng, L)
+            kind = rng.random()
+            if kind < 0.1:
+                seq = b"N" * L
+            elif kind < 0.2 and L > 20:
+                g = rng.randint(1, L)
+                seq = seq[: L - g] + b"G" * g
+            elif kind < 0.35 and L > 40:
+                ad = (AD1 if m == 1 else AD2).encode()
+                k = rng.randint(0, L - 1)
+                seq = (seq[:k] + ad + b"G" * L)[:L]
+            pk.set(i, m, seq, qual)
+    if paired:  # make ~1/3 of the pairs truly overlapping
+        for i in range(0, n, 3):
+            L = int(pk.len1[i])
+            if L < 40:
+                continue
+            comp = bytes.maketrans(b"ACGTacgt", b"TGCATGCA")
+            s1 = bytes(pk.seq1[i, :L])
+            ins = rng.randint(L // 2, L + 60)
+            frag = s1 + bytes(rng.choice(b"ACGT") for _ in range(max(0, ins - L)))
+            frag = frag[:ins]
+            r2 = frag.translate(comp)[::-1][:L]
+            r2 = (r2 + AD2.encode() + b"G" * L)[:L]
+            pk.set(i, 2, r2, bytes(pk.qual2[i, :L]))
+    return pk
+
+
+def config(name, max_cycles=256):
+    """Parameter presets: the BASELINE configs plus extra option coverage."""
+    paired = name not in ("C2", "SE_adapter", "SE_all")
+    p = abi.default_params(paired=paired, max_cycles=max_cycles)
+    p.qual_filter_enabled = 1  # every config has -q
+    if name == "C2":
+        pass
+    elif name in ("C1", "C3"):
+        p.adapter_trimming = 1
+        p.polyg_enabled = 1
+    elif name == "C3b":
+        p.adapter_trimming = 1
+        p.polyg_enabled = 1
+        abi.set_adapter(p, 1, AD1)
+        abi.set_adapter(p, 2, AD2)
+    elif name == "C4":
+        p.adapter_trimming = 1
+        p.polyg_enabled = 1
+        p.cut_right = 1
+        p.merge_enabled = 1
+    elif name == "C5":
+        p.adapter_trimming = 1
+        p.polyg_enabled = 1
+        p.polyx_enabled = 1
+        p.cut_right = 1
+    elif name == "PE_all":
+        p.adapter_trimming = 1
+        abi.set_adapter(p, 1, AD1[:20])
+        abi.set_adapter(p, 2, "AGATCGGAAGAGC")
+        p.polyg_enabled = 1
+        p.polyx_enabled = 1
+        p.polyx_mask = 0b01101
+        p.cut_front = 1
+        p.cut_tail = 1
+        p.cut_front_window, p.cut_tail_window = 3, 5
+        p.cut_front_quality, p.cut_tail_quality = 25, 15
+        p.trim_front1, p.trim_tail1, p.trim_front2, p.trim_tail2 = 2, 1, 0, 3
+        p.max_len1, p.max_len2 = 120, 0
+        p.length_filter_enabled, p.min_len, p.max_len = 1, 30, 140
+        p.complexity_enabled, p.complexity_threshold = 1, 0.4
+        p.avg_qual_limit = 25.5
+        p.n_base_limit = 3
+    elif name == "PE_merge_discard":
+        p.merge_enabled = 1
+        p.discard_unmerged = 1
+        p.cut_right = 1
+        p.cut_right_window = 7
+        p.length_filter_enabled = 1
+        p.overlap_diff_limit, p.overlap_require = 3, 20
+    elif name == "SE_adapter":
+        p.adapter_trimming = 1
+        abi.set_adapter(p, 1, AD1)
+        p.polyg_enabled = 1
+        p.polyx_enabled = 1
+        p.cut_right = 1
+    elif name == "SE_all":
+        p.adapter_trimming = 1
+        abi.set_adapter(p, 1, "AGATCGGA")
+        p.polyx_enabled = 1
+        p.polyx_mask = 0b11111
+        p.cut_front = p.cut_tail = 1
+        p.trim_front1, p.trim_tail1 = 3, 2
+        p.length_filter_enabled, p.min_len, p.max_len = 1, 20, 100
+        p.complexity_enabled = 1
+        p.low_qual_base_limit = 10
+    else:
+        raise KeyError(name)
+    return p
+
+
+ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all"]
+
+
+def run_oracle(oracle, p, pk):
+    res = pk.result_array()
+    acc = np.zeros(abi.acc_words(p.insert_size_max, p.max_cycles), np.uint64)
+    b = pk.batch()
+    rc = oracle.orc_process_batch(ctypes.byref(p), ctypes.byref(b), res.ctypes.data, acc.ctypes.data)
+    assert rc == 0, rc
+    return res, acc

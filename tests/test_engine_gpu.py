@@ -1,0 +1,148 @@
+"""Parity of the HIP engine (libfqengine.so, through its C-ABI) with the CPU restatement.
+
+Every per-read result record and every accumulator word must be identical (integer/byte
+work: bit-exact, no tolerance).  Runs on the MI355X box only (`-m gpu`).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from fqtool_amd import abi
+from batch_util import ALL_CONFIGS, Pack, config, edge_pack, run_oracle, synth_pack
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng_lib():
+    return abi.load_engine()
+
+
+def make_engine(lib, p, max_batch=8192, max_stride=160):
+    h = ctypes.c_void_p()
+    rc = lib.fq_engine_create(ctypes.byref(p), 0, max_batch, max_stride, ctypes.byref(h))
+    assert rc == 0, lib.fq_engine_last_error(None)
+    return h
+
+
+def run_engine(lib, p, pk):
+    h = make_engine(lib, p, max_batch=max(pk.n, 1), max_stride=pk.stride)
+    try:
+        res = pk.result_array()
+        b = pk.batch()
+        rc = lib.fq_engine_process(h, ctypes.byref(b), res.ctypes.data)
+        assert rc == 0, lib.fq_engine_last_error(h)
+        acc = np.zeros(lib.fq_engine_acc_words(h), np.uint64)
+        rc = lib.fq_engine_read_acc(h, acc.ctypes.data, acc.size)
+        assert rc == 0, lib.fq_engine_last_error(h)
+        return res, acc
+    finally:
+        lib.fq_engine_destroy(h)
+
+
+def assert_same(p, res_o, acc_o, res_e, acc_e):
+    if not np.array_equal(res_o, res_e):
+        bad = np.nonzero(res_o != res_e)[0]
+        i = int(bad[0])
+        raise AssertionError(f"{len(bad)} result records differ; first #{i}: oracle={res_o[i]} engine={res_e[i]}")
+    if not np.array_equal(acc_o, acc_e):
+        bad = np.nonzero(acc_o != acc_e)[0]
+        raise AssertionError(f"{len(bad)} accumulator words differ; first idx {bad[:8]}: "
+                             f"oracle={acc_o[bad[:8]]} engine={acc_e[bad[:8]]}")
+
+
+@pytest.mark.parametrize("name", ALL_CONFIGS)
+def test_synthetic_parity(eng_lib, oracle, name):
+    p = config(name, max_cycles=512)
+    pk = synth_pack(oracle, 6000, bool(p.paired), first=12345)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+@pytest.mark.parametrize("name", ALL_CONFIGS)
+def test_edge_case_parity(eng_lib, oracle, name):
+    p = config(name, max_cycles=512)
+    pk = edge_pack(3000, bool(p.paired), seed=hash(name) & 0xFFFF)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+def test_empty_pack(eng_lib, oracle):
+    p = config("C3", max_cycles=256)
+    pk = Pack(0, 160, True)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert not acc_e.any()
+
+
+def test_device_synth_matches_host(eng_lib, oracle):
+    import torch
+
+    n, stride, L = 5000, 160, 150
+    dev = torch.device("cuda:0")
+    bufs = [torch.zeros(n * stride, dtype=torch.uint8, device=dev) for _ in range(4)]
+    lens = [torch.zeros(n, dtype=torch.int16, device=dev) for _ in range(2)]
+    b = abi.FqBatch()
+    b.n, b.stride = n, stride
+    b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
+    b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
+    assert eng_lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 777, L, None) == 0
+    torch.cuda.synchronize()
+    pk = synth_pack(oracle, n, True, first=777, L=L, stride=stride)
+    got = [t.cpu().numpy().reshape(n, stride)[:, :L] for t in bufs]
+    exp = [pk.seq1[:, :L], pk.qual1[:, :L], pk.seq2[:, :L], pk.qual2[:, :L]]
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    assert (lens[0].cpu().numpy() == L).all() and (lens[1].cpu().numpy() == L).all()
+
+
+def test_device_path_accumulates_like_host_path(eng_lib, oracle):
+    """process_device on HBM-resident synthetic data == oracle on the same bytes, split over
+    several launches (accumulation across calls)."""
+    import torch
+
+    p = config("C3", max_cycles=256)
+    n, stride, L = 20000, 160, 150
+    dev = torch.device("cuda:0")
+    bufs = [torch.zeros(n * stride, dtype=torch.uint8, device=dev) for _ in range(4)]
+    lens = [torch.zeros(n, dtype=torch.int16, device=dev) for _ in range(2)]
+    res_d = torch.zeros(n * 2 * 16, dtype=torch.uint8, device=dev)
+    b = abi.FqBatch()
+    b.n, b.stride = n, stride
+    b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
+    b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
+    assert eng_lib.fq_synth_fill_device(ctypes.byref(b), 99, 0, L, None) == 0
+    torch.cuda.synchronize()
+    h = make_engine(eng_lib, p, max_batch=0, max_stride=0)
+    try:
+        half = n // 2
+        for lo, hi in ((0, half), (half, n)):
+            sub = abi.FqBatch()
+            sub.n, sub.stride = hi - lo, stride
+            sub.seq1, sub.qual1 = b.seq1 + lo * stride, b.qual1 + lo * stride
+            sub.seq2, sub.qual2 = b.seq2 + lo * stride, b.qual2 + lo * stride
+            sub.len1, sub.len2 = b.len1 + lo * 2, b.len2 + lo * 2
+            assert eng_lib.fq_engine_process_device(h, ctypes.byref(sub), res_d.data_ptr() + lo * 32, None) == 0
+        assert eng_lib.fq_engine_sync(h) == 0
+        acc = np.zeros(eng_lib.fq_engine_acc_words(h), np.uint64)
+        assert eng_lib.fq_engine_read_acc(h, acc.ctypes.data, acc.size) == 0
+    finally:
+        eng_lib.fq_engine_destroy(h)
+    pk = synth_pack(oracle, n, True, seed=99, L=L, stride=stride)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e = res_d.cpu().numpy().view(res_o.dtype)
+    assert_same(p, res_o, acc_o, res_e, acc)
+
+
+def test_too_long_read_is_rejected(eng_lib, oracle):
+    p = config("C3", max_cycles=100)
+    pk = synth_pack(oracle, 10, True)
+    h = make_engine(eng_lib, p, max_batch=10, max_stride=160)
+    try:
+        res = pk.result_array()
+        rc = eng_lib.fq_engine_process(h, ctypes.byref(pk.batch()), res.ctypes.data)
+        assert rc == -4
+    finally:
+        eng_lib.fq_engine_destroy(h)
