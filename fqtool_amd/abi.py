@@ -142,6 +142,13 @@ def set_adapter(p, which, seq):
 def load_engine(path=ENGINE_LIB):
     """Load libfqengine.so and declare its prototypes.  Raises OSError when it is missing:
     there is no CPU fallback."""
+    # torch bundles its own HIP runtime (libamdhip64.so.7 / libhsa-runtime64.so.1); loading it
+    # first makes the engine bind to that same runtime instead of a second copy from /opt/rocm
+    # (two HIP runtimes in one process cannot share device memory or the device).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     vp, i32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
     lib.fq_engine_create.argtypes = [ctypes.POINTER(FqParams), ctypes.c_int, i32, i32, ctypes.POINTER(vp)]

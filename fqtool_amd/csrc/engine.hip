@@ -209,7 +209,7 @@ int fq_engine_process_device(fq_engine* e, const fq_batch* db, fq_read_result* d
         (e->p.paired && (!db->seq2 || !db->qual2 || !db->len2)))
         return fail(e, FQ_E_INVALID, "bad device batch");
     HIP_TRY(e, hipSetDevice(e->device));
-    return launch(e, *db, dres, stream ? (hipStream_t)stream : e->stream);
+    return launch(e, *db, dres, (hipStream_t)stream);  // NULL is the HIP default stream
 }
 
 size_t fq_engine_acc_words(const fq_engine* e) { return e ? e->acc_words : 0; }

@@ -216,7 +216,7 @@ int fq_engine_destroy(fq_engine* e);
 int fq_engine_process(fq_engine* e, const fq_batch* host_batch, fq_read_result* results);
 
 /* Device-resident pack (inputs already in HBM): enqueues the kernels on `stream`
- * (a hipStream_t, NULL = the engine's stream) and returns without synchronising.
+ * (a hipStream_t; NULL = the HIP default stream) and returns without synchronising.
  * `device_results` may be NULL when the caller needs only the accumulators. */
 int fq_engine_process_device(fq_engine* e, const fq_batch* device_batch,
                              fq_read_result* device_results, void* stream);
