@@ -25,7 +25,7 @@ for s in $STEPS; do
     bench)
         run bench 900 python bench.py ${BENCH_ARGS:-} || exit $? ;;
     prof)
-        run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} || exit $? ;;
+        run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
 done
