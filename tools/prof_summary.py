@@ -10,7 +10,8 @@ import sys
 def from_db(path):
     c = sqlite3.connect(path)
     rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
-    return [(n, int(k), float(t), float(a), float(p)) for n, k, t, a, p in rows]
+    # the rocpd top_kernels view reports microseconds; normalise to ns like the CSV
+    return [(n, int(k), float(t) * 1e3, float(a) * 1e3, float(p)) for n, k, t, a, p in rows]
 
 
 def from_csv(path):
