@@ -42,19 +42,11 @@ __device__ __forceinline__ uint8_t comp(uint8_t c) {
     }
 }
 
-// Filter::passFilter, reference src/filter.cpp:3-52
-__device__ inline int pass_filter(const fq_params& p, const uint8_t* seq, const uint8_t* qual, int rlen,
-                                  bool is_null) {
-    if (is_null || rlen == 0) return FQ_FAIL_LENGTH;
-    int low = 0, nb = 0, tq = 0;
-    if (p.qual_filter_enabled || p.length_filter_enabled) {
-        for (int i = 0; i < rlen; ++i) {
-            int q = qv(qual, i);
-            tq += q - 33;
-            nb += seq[i] == 'N';
-            low += q < p.low_qual_limit;
-        }
-    }
+// The decision part of Filter::passFilter (reference src/filter.cpp:29-51) from the three
+// counts of its scan; `diffs` lazily counts seq[i] != seq[i+1] for the complexity filter
+// (Filter::passLowComplexityFliter, src/filter.cpp:54-67).
+template <class Diffs>
+__device__ inline int filter_verdict(const fq_params& p, int rlen, int low, int nb, int tq, Diffs diffs) {
     if (p.qual_filter_enabled) {
         if (low > p.low_qual_base_limit) return FQ_FAIL_QUALITY;
         if (p.avg_qual_limit > 0 && p.avg_qual_limit > (double)tq / rlen) return FQ_FAIL_QUALITY;
@@ -64,16 +56,52 @@ __device__ inline int pass_filter(const fq_params& p, const uint8_t* seq, const 
         if (rlen < p.min_len) return FQ_FAIL_LENGTH;
         if (p.max_len > 0 && rlen > p.max_len) return FQ_FAIL_TOO_LONG;
     }
-    if (p.complexity_enabled) {  // Filter::passLowComplexityFliter, src/filter.cpp:54-67
+    if (p.complexity_enabled) {
         bool ok = false;
-        if (rlen > 1) {
-            int diff = 0;
-            for (int i = 0; i < rlen - 1; ++i) diff += seq[i] != seq[i + 1];
-            ok = (double)diff / (rlen - 1) >= p.complexity_threshold;
-        }
+        if (rlen > 1) ok = (double)diffs() / (rlen - 1) >= p.complexity_threshold;
         if (!ok) return FQ_FAIL_COMPLEXITY;
     }
     return FQ_PASS_FILTER;
+}
+
+// Accessors: every operation below reads bytes through functors seq(i) -> uint8_t and
+// qual(i) -> int (signed char value), so the same restatement runs on HBM rows (v1 kernel)
+// and on LDS-staged columns (v2 kernel).
+struct PtrQual {
+    const uint8_t* p;
+    __device__ __forceinline__ int operator()(int i) const { return (int)(int8_t)p[i]; }
+};
+struct Bytes {
+    const uint8_t* p;
+    __device__ __forceinline__ uint8_t operator()(int i) const { return p[i]; }
+};
+template <class A>
+struct Offset {  // window view: a(off + i)
+    A a;
+    int off;
+    __device__ __forceinline__ auto operator()(int i) const { return a(off + i); }
+};
+template <class A>
+__device__ __forceinline__ Offset<A> at(A a, int off) { return Offset<A>{a, off}; }
+
+// Filter::passFilter, reference src/filter.cpp:3-52
+template <class SQ, class QQ>
+__device__ inline int pass_filter_t(const fq_params& p, SQ seq, QQ qual, int rlen, bool is_null) {
+    if (is_null || rlen == 0) return FQ_FAIL_LENGTH;
+    int low = 0, nb = 0, tq = 0;
+    if (p.qual_filter_enabled || p.length_filter_enabled) {
+        for (int i = 0; i < rlen; ++i) {
+            int q = qual(i);
+            tq += q - 33;
+            nb += seq(i) == 'N';
+            low += q < p.low_qual_limit;
+        }
+    }
+    return filter_verdict(p, rlen, low, nb, tq, [&]() {
+        int diff = 0;
+        for (int i = 0; i < rlen - 1; ++i) diff += seq(i) != seq(i + 1);
+        return diff;
+    });
 }
 
 // (double)T/(double)w >= X  <=>  T >= X*w for integer T, X and 1 <= w <= 1000 (the quotient is
@@ -82,8 +110,9 @@ __device__ inline int pass_filter(const fq_params& p, const uint8_t* seq, const 
 __device__ __forceinline__ bool win_ge(int total, int w, int x) { return total >= x * w; }
 
 // Filter::trimAndCut, reference src/filter.cpp:69-189. Returns false for NULL.
-__device__ inline bool trim_and_cut(const fq_params& p, const uint8_t* seq, const uint8_t* qual, int l,
-                                    int front, int tail, int& out_start, int& out_len) {
+template <class SQ, class QQ>
+__device__ inline bool trim_and_cut_t(const fq_params& p, SQ seq, QQ qual, int l, int front, int tail,
+                                      int& out_start, int& out_len) {
     const bool enF = p.cut_front, enR = p.cut_right, enT = p.cut_tail;
     if (front == 0 && tail == 0 && !enF && !enR && !enT) {
         out_start = 0;
@@ -102,14 +131,14 @@ __device__ inline bool trim_and_cut(const fq_params& p, const uint8_t* seq, cons
         int s = front;
         if (l - front - tail - w <= 0) return false;
         int tot = 0;
-        for (int i = 0; i < w - 1; ++i) tot += qv(qual, s + i);
+        for (int i = 0; i < w - 1; ++i) tot += qual(s + i);
         for (s = front; s + w < l - tail; ++s) {
-            tot += qv(qual, s + w - 1);
-            if (s > front) tot -= qv(qual, s - 1);
+            tot += qual(s + w - 1);
+            if (s > front) tot -= qual(s - 1);
             if (win_ge(tot, w, thr)) break;
         }
         if (s > 0) s = s + w - 1;
-        while (s < l && seq[s] == 'N') ++s;
+        while (s < l && seq(s) == 'N') ++s;
         front = s;
         rlen = l - front - tail;
     }
@@ -119,17 +148,17 @@ __device__ inline bool trim_and_cut(const fq_params& p, const uint8_t* seq, cons
         if (l - front - tail - w <= 0) return false;
         int tot = 0;
         bool found = false;
-        for (int i = 0; i < w - 1; ++i) tot += qv(qual, s + i);
+        for (int i = 0; i < w - 1; ++i) tot += qual(s + i);
         for (s = front; s + w < l - tail; ++s) {
-            tot += qv(qual, s + w - 1);
-            if (s > front) tot -= qv(qual, s - 1);
+            tot += qual(s + w - 1);
+            if (s > front) tot -= qual(s - 1);
             if (!win_ge(tot, w, thr)) {
                 found = true;
                 break;
             }
         }
         if (found) {
-            while (s < l - 1 && qv(qual, s) >= thr) ++s;
+            while (s < l - 1 && qual(s) >= thr) ++s;
             rlen = s - front;
         }
     }
@@ -138,14 +167,14 @@ __device__ inline bool trim_and_cut(const fq_params& p, const uint8_t* seq, cons
         if (l - front - tail - w <= 0) return false;
         int tot = 0;
         int t = l - tail - 1;
-        for (int i = 0; i < w - 1; ++i) tot += qv(qual, t - i);
+        for (int i = 0; i < w - 1; ++i) tot += qual(t - i);
         for (t = l - tail - 1; t - w >= front; --t) {
-            tot += qv(qual, t - w + 1);
-            if (t < l - tail - 1) tot -= qv(qual, t + 1);
+            tot += qual(t - w + 1);
+            if (t < l - tail - 1) tot -= qual(t + 1);
             if (win_ge(tot, w, thr)) break;
         }
         if (t < l - 1) t = t - w + 1;
-        while (t >= 0 && seq[t] == 'N') --t;
+        while (t >= 0 && seq(t) == 'N') --t;
         rlen = t - front + 1;
     }
     if (rlen <= 0 || front >= l - 1) return false;
@@ -155,10 +184,11 @@ __device__ inline bool trim_and_cut(const fq_params& p, const uint8_t* seq, cons
 }
 
 // PolyX::trimPolyG, reference src/polyx.cpp:14-38. Returns new length; bases < 0: not recorded.
-__device__ inline int trim_polyg(const uint8_t* d, int rlen, int compareReq, int maxMM, int per, int& bases) {
+template <class SQ>
+__device__ inline int trim_polyg_t(SQ d, int rlen, int compareReq, int maxMM, int per, int& bases) {
     int mismatch = 0, i = 0, firstG = rlen - 1;
     for (i = 0; i < rlen; ++i) {
-        if (d[rlen - i - 1] != 'G') ++mismatch;
+        if (d(rlen - i - 1) != 'G') ++mismatch;
         else firstG = rlen - i - 1;
         int allowed = min(maxMM, max(1, (i + 1) / per));
         if (mismatch > allowed) break;
@@ -172,12 +202,13 @@ __device__ inline int trim_polyg(const uint8_t* d, int rlen, int compareReq, int
 }
 
 // PolyX::trimPolyX, reference src/polyx.cpp:45-101
-__device__ inline int trim_polyx(const uint8_t* d, int rlen, int mask, int compareReq, int maxMM, int per,
-                                 int& poly_out, int& bases) {
+template <class SQ>
+__device__ inline int trim_polyx_t(SQ d, int rlen, int mask, int compareReq, int maxMM, int per, int& poly_out,
+                                   int& bases) {
     int cnt[5] = {0, 0, 0, 0, 0};
     int pos = 0;
     for (pos = 0; pos < rlen; ++pos) {
-        uint8_t c = d[rlen - 1 - pos];
+        uint8_t c = d(rlen - 1 - pos);
         int k = c == 'A' ? 0 : c == 'T' ? 1 : c == 'C' ? 2 : c == 'G' ? 3 : 4;
 #pragma unroll
         for (int b = 0; b < 5; ++b) cnt[b] += (k == b);
@@ -201,13 +232,29 @@ __device__ inline int trim_polyx(const uint8_t* d, int rlen, int mask, int compa
             }
         const uint8_t polyBase = poly == 0 ? 'A' : poly == 1 ? 'T' : poly == 2 ? 'C' : poly == 3 ? 'G' : 'N';
         pos = min(rlen - 1, pos);
-        while (pos > 0 && d[rlen - pos - 1] != polyBase) --pos;
+        while (pos > 0 && d(rlen - pos - 1) != polyBase) --pos;
         int target = rlen - pos - 1;
         poly_out = poly;
         bases = pos + 1;
         return (target > rlen || target < 0) ? rlen : target;
     }
     return rlen;
+}
+
+// Pointer-based wrappers (v1 kernel).
+__device__ inline int pass_filter(const fq_params& p, const uint8_t* seq, const uint8_t* qual, int rlen, bool is_null) {
+    return pass_filter_t(p, Bytes{seq}, PtrQual{qual}, rlen, is_null);
+}
+__device__ inline bool trim_and_cut(const fq_params& p, const uint8_t* seq, const uint8_t* qual, int l, int front,
+                                    int tail, int& st, int& n) {
+    return trim_and_cut_t(p, Bytes{seq}, PtrQual{qual}, l, front, tail, st, n);
+}
+__device__ inline int trim_polyg(const uint8_t* d, int rlen, int compareReq, int maxMM, int per, int& bases) {
+    return trim_polyg_t(Bytes{d}, rlen, compareReq, maxMM, per, bases);
+}
+__device__ inline int trim_polyx(const uint8_t* d, int rlen, int mask, int compareReq, int maxMM, int per, int& poly,
+                                 int& bases) {
+    return trim_polyx_t(Bytes{d}, rlen, mask, compareReq, maxMM, per, poly, bases);
 }
 
 struct Overlap {
@@ -259,7 +306,8 @@ __device__ inline Overlap analyze(const uint8_t* s1, int len1, const uint8_t* s2
 }
 
 // AdapterTrimmer::trimBySequence search, reference src/adaptertrimmer.cpp:29-90
-__device__ inline bool trim_by_sequence(const uint8_t* r, int rlen, const uint8_t* ad, int alen, int& pos_out) {
+template <class SQ>
+__device__ inline bool trim_by_sequence_t(SQ r, int rlen, const uint8_t* ad, int alen, int& pos_out) {
     if (alen < 4) return false;
     int start = 0;
     if (alen >= 16) start = -4;
@@ -271,7 +319,7 @@ __device__ inline bool trim_by_sequence(const uint8_t* r, int rlen, const uint8_
         int mm = 0;
         bool matched = true;
         for (int i = max(0, -pos); i < cmplen; ++i) {
-            if (ad[i] != r[i + pos]) {
+            if (ad[i] != r(i + pos)) {
                 if (++mm > allowed) {
                     matched = false;
                     break;
@@ -284,6 +332,9 @@ __device__ inline bool trim_by_sequence(const uint8_t* r, int rlen, const uint8_
         }
     }
     return false;
+}
+__device__ inline bool trim_by_sequence(const uint8_t* r, int rlen, const uint8_t* ad, int alen, int& pos_out) {
+    return trim_by_sequence_t(Bytes{r}, rlen, ad, alen, pos_out);
 }
 
 }  // namespace fqdev

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -25,6 +26,10 @@ struct fq_engine {
     uint16_t* d_lens = nullptr;  // 2 x max_batch
     fq_read_result* d_res = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool fast = false;          // pe_fast kernel usable for these params
+    int* slow_tiles = nullptr;  // tile list handed from the fast to the general kernel
+    int* slow_count = nullptr;
+    size_t slow_cap = 0;
     bool timed = false;
     std::string last_error;
 };
@@ -113,6 +118,12 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     if (fq_pack_kernel_lds_bytes(e->p) > 160 * 1024)
         return bail(fail(e, FQ_E_INVALID, "max_cycles too large for the LDS-privatised accumulators"));
     if ((he = fq_pack_kernel_set_lds(e->p)) != hipSuccess) return bail(hip_fail(e, he, "hipFuncSetAttribute"));
+    const char* force_general = std::getenv("FQ_ENGINE_GENERAL_ONLY");
+    e->fast = fq_pe_fast_supported(e->p) && !(force_general && force_general[0] == '1');
+    if (e->fast) {
+        if ((he = fq_pe_fast_prepare()) != hipSuccess) return bail(hip_fail(e, he, "hipFuncSetAttribute fast"));
+        if ((he = hipMalloc(&e->slow_count, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc"));
+    }
     *out = e;
     return FQ_OK;
 }
@@ -126,6 +137,8 @@ int fq_engine_destroy(fq_engine* e) {
     if (e->d_rows) (void)hipFree(e->d_rows);
     if (e->d_lens) (void)hipFree(e->d_lens);
     if (e->d_res) (void)hipFree(e->d_res);
+    if (e->slow_tiles) (void)hipFree(e->slow_tiles);
+    if (e->slow_count) (void)hipFree(e->slow_count);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -145,6 +158,24 @@ static int grid_for(const fq_engine* e, int n) {
 
 static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStream_t s) {
     if (db.n <= 0) return FQ_OK;
+    if (e->fast) {
+        const size_t ntiles = ((size_t)db.n + 31) / 32;
+        if (ntiles > e->slow_cap) {
+            HIP_TRY(e, hipStreamSynchronize(s));
+            if (e->slow_tiles) HIP_TRY(e, hipFree(e->slow_tiles));
+            e->slow_tiles = nullptr;
+            e->slow_cap = 0;
+            HIP_TRY(e, hipMalloc(&e->slow_tiles, ntiles * sizeof(int)));
+            e->slow_cap = ntiles;
+        }
+        HIP_TRY(e, hipMemsetAsync(e->slow_count, 0, sizeof(int), s));
+        HIP_TRY(e, hipEventRecord(e->ev0, s));
+        HIP_TRY(e, fq_launch_pe_fast(e->p, db, dres, e->acc, e->slow_tiles, e->slow_count, e->cus, s));
+        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, e->cus, s, e->slow_tiles, e->slow_count));
+        HIP_TRY(e, hipEventRecord(e->ev1, s));
+        e->timed = true;
+        return FQ_OK;
+    }
     HIP_TRY(e, hipEventRecord(e->ev0, s));
     HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, grid_for(e, db.n), s));
     HIP_TRY(e, hipEventRecord(e->ev1, s));

@@ -124,7 +124,8 @@ __device__ inline void apply_adapter_seq(const Smem& sm, const uint8_t* s, int s
 
 template <bool PAIRED>
 __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
-                                                      unsigned long long* __restrict__ acc, int* __restrict__ err) {
+                                                      unsigned long long* __restrict__ acc, int* __restrict__ err,
+                                                      const int* __restrict__ tiles, const int* __restrict__ ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int C = p.max_cycles;
     const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
@@ -138,7 +139,11 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
 
     const int skew = threadIdx.x & 63;
     const size_t stride = (size_t)b.stride;
-    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < b.n; idx += gridDim.x * blockDim.x) {
+    // all pairs of the pack, or (tile-list mode) the 32-pair tiles the fast kernel handed over
+    const int total = tiles ? *ntiles * 32 : b.n;
+    for (int item = blockIdx.x * blockDim.x + threadIdx.x; item < total; item += gridDim.x * blockDim.x) {
+        const int idx = tiles ? tiles[item >> 5] * 32 + (item & 31) : item;
+        if (idx >= b.n) continue;
         const uint8_t* s1 = b.seq1 + idx * stride;
         const uint8_t* q1 = b.qual1 + idx * stride;
         const int l1 = b.len1[idx];
@@ -365,12 +370,13 @@ size_t fq_pack_kernel_lds_bytes(const fq_params& p) {
 }
 
 hipError_t fq_launch_pack_kernel(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
-                                 int* err, int grid, hipStream_t stream) {
+                                 int* err, int grid, hipStream_t stream, const int* tiles, const int* ntiles) {
     const size_t lds = fq_pack_kernel_lds_bytes(p);
     if (p.paired)
-        hipLaunchKernelGGL(fq_pack_kernel<true>, dim3(grid), dim3(256), lds, stream, p, b, res, acc, err);
+        hipLaunchKernelGGL(fq_pack_kernel<true>, dim3(grid), dim3(256), lds, stream, p, b, res, acc, err, tiles, ntiles);
     else
-        hipLaunchKernelGGL(fq_pack_kernel<false>, dim3(grid), dim3(256), lds, stream, p, b, res, acc, err);
+        hipLaunchKernelGGL(fq_pack_kernel<false>, dim3(grid), dim3(256), lds, stream, p, b, res, acc, err, tiles,
+                           ntiles);
     return hipGetLastError();
 }
 

@@ -19,6 +19,14 @@ def eng_lib():
     return abi.load_engine()
 
 
+@pytest.fixture(params=["fast", "general"])
+def mode(request, monkeypatch):
+    """Run each parity case through the default dispatch (gfx950 fast kernels, falling back per
+    tile) and through the general kernel only."""
+    monkeypatch.setenv("FQ_ENGINE_GENERAL_ONLY", "1" if request.param == "general" else "0")
+    return request.param
+
+
 def make_engine(lib, p, max_batch=8192, max_stride=160):
     h = ctypes.c_void_p()
     rc = lib.fq_engine_create(ctypes.byref(p), 0, max_batch, max_stride, ctypes.byref(h))
@@ -53,7 +61,7 @@ def assert_same(p, res_o, acc_o, res_e, acc_e):
 
 
 @pytest.mark.parametrize("name", ALL_CONFIGS)
-def test_synthetic_parity(eng_lib, oracle, name):
+def test_synthetic_parity(eng_lib, oracle, name, mode):
     p = config(name, max_cycles=512)
     pk = synth_pack(oracle, 6000, bool(p.paired), first=12345)
     res_o, acc_o = run_oracle(oracle, p, pk)
@@ -62,9 +70,31 @@ def test_synthetic_parity(eng_lib, oracle, name):
 
 
 @pytest.mark.parametrize("name", ALL_CONFIGS)
-def test_edge_case_parity(eng_lib, oracle, name):
+def test_edge_case_parity(eng_lib, oracle, name, mode):
     p = config(name, max_cycles=512)
     pk = edge_pack(3000, bool(p.paired), seed=hash(name) & 0xFFFF)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+@pytest.mark.parametrize("name", ["C3", "C3b", "C5", "PE_all"])
+def test_mixed_fast_and_handoff_tiles(eng_lib, oracle, name):
+    """Mostly clean synthetic tiles plus scattered tiles with IUPAC bases, quality bytes >= 128
+    and over-long reads: the fast kernel hands those tiles to the general kernel."""
+    p = config(name, max_cycles=512)
+    pk = synth_pack(oracle, 8000, True, first=555, stride=176)
+    rng = np.random.default_rng(3)
+    for i in rng.choice(8000, 40, replace=False):
+        kind = i % 3
+        if kind == 0:
+            pk.seq1[i, rng.integers(0, 150)] = ord("R")
+        elif kind == 1:
+            pk.qual2[i, rng.integers(0, 150)] = 200
+        else:
+            pk.seq2[i, 150:170] = ord("A")
+            pk.qual2[i, 150:170] = ord("I")
+            pk.len2[i] = 170
     res_o, acc_o = run_oracle(oracle, p, pk)
     res_e, acc_e = run_engine(eng_lib, p, pk)
     assert_same(p, res_o, acc_o, res_e, acc_e)
