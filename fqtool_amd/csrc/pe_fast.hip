@@ -168,6 +168,9 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
 
     const int mate = lane >> 5, pl = lane & 31;
     const int mlane = lane ^ 32;
+    // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
+    // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics
+    const int abl = p.reserved[0];
     const bool removed_mode = p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front;
     const int ntiles = (b.n + 31) >> 5;
     const int nchunks = min(kCodeW, b.stride >> 4);
@@ -265,7 +268,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         rr.ad_pos = rr.ad_len = rr.m_len1 = rr.m_len2 = rr.reserved = 0;
 
         // ---------------- polyG (src/peprocessor.cpp:295-299) ----------------
-        if (both && p.polyg_enabled) {
+        if (both && p.polyg_enabled && !(abl & 8)) {
             int bases;
             n = trim_polyg_t(at(seq, st), n, p.polyg_compare_req, p.polyg_max_mismatch, p.polyg_one_mismatch_per, bases);
             if (bases >= 0) {
@@ -275,7 +278,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         }
 
         // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
-        if (both) {
+        if (both && !(abl & 1)) {
             const int st_o = __shfl_xor(st, 32), n_o = __shfl_xor(n, 32), L_o = __shfl_xor(L, 32);
             const int st1 = mate ? st_o : st, n1 = mate ? n_o : n;
             const int st2 = mate ? st : st_o, n2 = mate ? n : n_o, L2 = mate ? L : L_o;
@@ -377,7 +380,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         int code = FQ_FAIL_LENGTH;
         if (nn && n > 0) {
             int low = 0, tq = 0, nb = 0;
-            if (p.qual_filter_enabled || p.length_filter_enabled) {
+            if ((p.qual_filter_enabled || p.length_filter_enabled) && !(abl & 2)) {
                 const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
                 const int end = st + n;
                 for (int c = st >> 4; c < ((end + 15) >> 4); ++c) {
@@ -411,7 +414,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         if (mate == 0 && valid) sadd(&small[FQ_ACC_FILTER + max(code, code_o)], 2ull);  // addFilterResult: +2
 
         // ---------------- Stats (pass B): pre, and removed/post ----------------
-        if (valid) {
+        if (valid && !(abl & 4)) {
             const int nd = (L + 3) >> 2;
             const int rot = nd ? lane % nd : 0;
             uint32_t q20 = 0, q30 = 0, a20 = 0, a30 = 0;
@@ -432,7 +435,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
                 a30 += __popc(t30 & am);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    if ((vm >> (8 * j)) & 1u) {
+                    if (((vm >> (8 * j)) & 1u) && !(abl & 16)) {
                         const uint32_t cls = (sw >> (8 * j)) & 7u;
                         const uint32_t slot = (cls * 3u) & 7u;
                         const unsigned long long v = kCount1 | (unsigned long long)(((qw >> (8 * j)) & 0xFFu) ^ 0x80u);
@@ -459,6 +462,8 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
             }
             s_aux[2] += a20;
             s_aux[3] += a30;
+        }
+        if (valid) {
 
             rr.start = nn ? (uint16_t)st : 0;
             rr.len = nn ? (uint16_t)n : 0;

@@ -1,0 +1,34 @@
+"""Profiling aid: time the fast PE kernel with phases switched off (fq_params.reserved[0] bits,
+see pe_fast.hip).  Outputs are NOT valid in ablated runs; only the timings matter."""
+import ctypes, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from fqtool_amd import abi
+
+lib = abi.load_engine()
+dev = torch.device("cuda:0")
+n, stride = int(os.environ.get("PAIRS", 20_000_000)), 160
+bufs = [torch.empty(n * stride, dtype=torch.uint8, device=dev) for _ in range(4)]
+lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
+b = abi.FqBatch(); b.n, b.stride = n, stride
+b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
+b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
+assert lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 0, 150, None) == 0
+res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+torch.cuda.synchronize()
+variants = [("full", 0), ("no_overlap", 1), ("no_filter", 2), ("no_stats", 4), ("no_polyg", 8),
+            ("no_lds_atomics", 16), ("no_overlap_filter_stats", 7), ("stage_only", 15)]
+results = {}
+for rep in range(3):
+    for name, bits in variants:
+        p = abi.default_params(True, 256); p.qual_filter_enabled = 1; p.adapter_trimming = 1; p.polyg_enabled = 1
+        p.reserved[0] = bits
+        h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
+        lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_engine_sync(h)
+        lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_engine_sync(h)
+        ms = lib.fq_engine_last_kernel_ms(h)
+        results.setdefault(name, []).append(ms)
+        lib.fq_engine_destroy(h)
+for name, _ in variants:
+    v = sorted(results[name])
+    print(f"{name:28s} median {v[len(v)//2]:8.2f} ms  min {v[0]:8.2f}  -> {n / (v[len(v)//2] / 1e3) / 1e9:.2f} G pairs/s", flush=True)
