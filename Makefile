@@ -12,7 +12,30 @@ ENGINE_SRCS := $(CSRC)/engine.hip $(CSRC)/pe_kernel.hip $(CSRC)/pe_fast.hip $(CS
 ENGINE_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(ENGINE_SRCS))
 ENGINE_HDRS := include/fqengine.h $(CSRC)/engine_internal.h $(CSRC)/device_ops.h
 
-all: engine oracle
+CXX        ?= g++
+HOSTFLAGS  ?= -std=c++17 -O2 -fPIC -Wall -Wextra -pthread
+HOSTDIR    := fqtool_amd/host
+HOST_SRCS  := $(HOSTDIR)/json.cpp $(HOSTDIR)/options.cpp $(HOSTDIR)/fastq.cpp $(HOSTDIR)/evaluator.cpp \
+              $(HOSTDIR)/report.cpp $(HOSTDIR)/processor.cpp $(HOSTDIR)/capi.cpp
+HOST_OBJS  := $(patsubst $(HOSTDIR)/%.cpp,$(OBJDIR)/host_%.o,$(HOST_SRCS))
+HOST_HDRS  := $(wildcard $(HOSTDIR)/*.h) $(HOSTDIR)/known_adapters.inc include/fqengine.h
+BINDIR     := fqtool_amd/bin
+
+all: engine host oracle
+
+host: $(LIBDIR)/libfqhost.so $(BINDIR)/fqtool
+
+$(OBJDIR)/host_%.o: $(HOSTDIR)/%.cpp $(HOST_HDRS)
+	@mkdir -p $(OBJDIR)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIBDIR)/libfqhost.so: $(HOST_OBJS) $(LIBDIR)/libfqengine.so
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(HOSTFLAGS) -shared -o $@ $(HOST_OBJS) -L$(LIBDIR) -lfqengine -Wl,-rpath,'$$ORIGIN' -lz
+
+$(BINDIR)/fqtool: $(HOSTDIR)/main.cpp $(LIBDIR)/libfqhost.so
+	@mkdir -p $(BINDIR)
+	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(LIBDIR) -lfqhost -lfqengine -Wl,-rpath,'$$ORIGIN/../lib' -lz
 
 engine: $(LIBDIR)/libfqengine.so
 
@@ -30,4 +53,4 @@ oracle:
 clean:
 	rm -rf build $(LIBDIR) fqtool_amd/bin oracle/build
 
-.PHONY: all engine oracle clean
+.PHONY: all engine host oracle clean

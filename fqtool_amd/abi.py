@@ -178,3 +178,45 @@ ENGINE_SYMBOLS = [
     "fq_engine_sync", "fq_engine_set_acc_buffer", "fq_engine_last_error", "fq_engine_device_info", "fq_synth_fill_device",
     "fq_engine_last_kernel_ms",
 ]
+
+
+def load_host(path=HOST_LIB):
+    """Load libfqhost.so (include/fqhost.h) after the engine (it links libfqengine.so)."""
+    load_engine()
+    lib = ctypes.CDLL(path)
+    vp, ci, cs = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    argv_t = ctypes.POINTER(ctypes.c_char_p)
+    lib.fqh_run.argtypes = [ci, argv_t]
+    lib.fqh_json_double.argtypes = [ctypes.c_double, ctypes.c_char_p, cs]
+    lib.fqh_merged_name.argtypes = [ctypes.c_char_p, ci, ci, ctypes.c_char_p, cs]
+    lib.fqh_evaluate_read_len.argtypes = [ctypes.c_char_p]
+    lib.fqh_detect_adapter.argtypes = [ctypes.c_char_p, ci, ctypes.c_char_p, cs]
+    lib.fqh_report_json.argtypes = [ci, ctypes.c_char_p, vp, ci, ctypes.c_char_p]
+    lib.fqh_report_json.restype = vp
+    lib.fqh_free.argtypes = [vp]
+    lib.fqh_session_open.argtypes = [ci, argv_t, ctypes.POINTER(vp)]
+    lib.fqh_session_error.argtypes = [vp]
+    lib.fqh_session_error.restype = ctypes.c_char_p
+    lib.fqh_session_params.argtypes = [vp, ci, ctypes.POINTER(FqParams)]
+    lib.fqh_session_next.argtypes = [vp, ci, ctypes.POINTER(FqBatch)]
+    lib.fqh_session_consume.argtypes = [vp, vp, ci]
+    lib.fqh_session_add_acc.argtypes = [vp, vp, ci]
+    lib.fqh_session_finish.argtypes = [vp]
+    lib.fqh_session_finish.restype = vp
+    lib.fqh_session_close.argtypes = [vp]
+    return lib
+
+
+def take_string(lib, ptr):
+    """Copy and free a malloc'd string returned by libfqhost."""
+    s = ctypes.string_at(ptr).decode()
+    lib.fqh_free(ptr)
+    return s
+
+
+HOST_SYMBOLS = [
+    "fqh_run", "fqh_json_double", "fqh_merged_name", "fqh_evaluate_read_len", "fqh_detect_adapter",
+    "fqh_report_json", "fqh_free", "fqh_session_open", "fqh_session_error", "fqh_session_params",
+    "fqh_session_next", "fqh_session_consume", "fqh_session_add_acc", "fqh_session_finish",
+    "fqh_session_close",
+]

@@ -1,0 +1,186 @@
+// capi.cpp -- C entry points of the host library (libfqhost.so) for tests and bindings.
+#include <cstdlib>
+#include <fstream>
+#include <memory>
+#include <cstring>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "evaluator.h"
+#include "json.h"
+#include "options.h"
+#include "processor.h"
+#include "report.h"
+#include "../../include/fqhost.h"
+
+using namespace fqhost;
+
+namespace {
+int copy_out(const std::string& s, char* buf, size_t n) {
+    if (!buf || n == 0) return -1;
+    const size_t k = std::min(n - 1, s.size());
+    std::memcpy(buf, s.data(), k);
+    buf[k] = '\0';
+    return (int)s.size();
+}
+}  // namespace
+
+extern "C" {
+
+int fqh_run(int argc, char** argv) { return run_tool(argc, argv); }
+
+int fqh_json_double(double v, char* buf, size_t n) { return copy_out(json_double(v), buf, n); }
+
+int fqh_merged_name(const char* name, int len1, int len2, char* buf, size_t n) {
+    return copy_out(merged_name(name, len1, len2), buf, n);
+}
+
+int fqh_detect_adapter(const char* path, int trim_tail1, char* buf, size_t n) {
+    try {
+        return copy_out(detect_adapter(path, trim_tail1), buf, n);
+    } catch (...) {
+        return -1;
+    }
+}
+
+int fqh_evaluate_read_len(const char* path) {
+    try {
+        return evaluate_read_len(path);
+    } catch (...) {
+        return -1;
+    }
+}
+
+// JSON report from an accumulator block, for an argv (NUL-separated, argc entries) and adapter
+// side information as text lines "D1\tSEQ" / "D2\tSEQ" (detected adapters) and
+// "1\tSEQ\tCOUNT" / "2\tSEQ\tCOUNT" (adapter string counts).  Returns a malloc'd string.
+char* fqh_report_json(int argc, const char* argv_blob, const uint64_t* acc, int max_cycles, const char* side) {
+    try {
+        std::vector<std::string> args;
+        const char* p = argv_blob;
+        for (int i = 0; i < argc; ++i) {
+            args.emplace_back(p);
+            p += args.back().size() + 1;
+        }
+        std::vector<char*> argv;
+        for (auto& a : args) argv.push_back(&a[0]);
+        Options o = parse_cli(argc, argv.data());
+        o.update(argc, argv.data());
+        AdapterCounts ac;
+        std::istringstream in(side ? side : "");
+        std::string line;
+        while (std::getline(in, line)) {
+            std::istringstream ls(line);
+            std::string tag, seq;
+            size_t cnt = 0;
+            std::getline(ls, tag, '\t');
+            std::getline(ls, seq, '\t');
+            if (tag == "D1") o.detected_adapter1 = seq;
+            else if (tag == "D2") o.detected_adapter2 = seq;
+            else if (tag == "1" || tag == "2") {
+                ls >> cnt;
+                (tag == "1" ? ac.r1 : ac.r2)[seq] += cnt;
+            }
+        }
+        HostAcc h(o.insert_size_max);
+        h.add(acc, max_cycles);
+        const std::string s = build_report(o, h, ac).dump(4);
+        char* out = (char*)std::malloc(s.size() + 1);
+        std::memcpy(out, s.c_str(), s.size() + 1);
+        return out;
+    } catch (const std::exception& e) {
+        const std::string s = std::string("ERROR: ") + e.what();
+        char* out = (char*)std::malloc(s.size() + 1);
+        std::memcpy(out, s.c_str(), s.size() + 1);
+        return out;
+    }
+}
+
+void fqh_free(char* p) { std::free(p); }
+
+// ---- host session: the tool's pipeline with the per-pack engine call left to the caller ----
+struct fqh_session {
+    Options o;
+    std::unique_ptr<PackReader> reader;
+    Pack pk;
+    std::unique_ptr<OutputSet> outs;
+    HostAcc acc;
+    AdapterCounts ac;
+    std::string err;
+    fqh_session() : acc(512) {}
+};
+
+const char* fqh_session_error(const fqh_session* s) { return s ? s->err.c_str() : ""; }
+
+int fqh_session_open(int argc, char** argv, fqh_session** out) {
+    std::unique_ptr<fqh_session> s(new fqh_session());
+    try {
+        s->o = prepare_options(argc, argv);
+        s->acc = HostAcc(s->o.insert_size_max);
+        s->reader.reset(new PackReader(s->o.in1, s->o.in2, s->o.interleaved, s->o.phred64));
+        s->outs.reset(new OutputSet(s->o));
+    } catch (const std::exception& e) {
+        s->err = e.what();
+        *out = s.release();
+        return -1;
+    }
+    *out = s.release();
+    return 0;
+}
+
+int fqh_session_params(fqh_session* s, int max_cycles, fq_params* out) {
+    *out = s->o.to_params(max_cycles);
+    return 0;
+}
+
+// next pack of up to max_n records; 1 = got one, 0 = end of input, -1 = error
+int fqh_session_next(fqh_session* s, int max_n, fq_batch* out) {
+    try {
+        s->pk = Pack();
+        if (!s->reader->next(s->pk, (size_t)max_n)) return 0;
+        *out = s->pk.batch();
+        return 1;
+    } catch (const std::exception& e) {
+        s->err = e.what();
+        return -1;
+    }
+}
+
+// formats the current pack from its per-read records, counts adapter strings and writes the
+// output files like the tool
+int fqh_session_consume(fqh_session* s, const fq_read_result* res, int max_cycles) {
+    try {
+        const fq_params p = s->o.to_params(max_cycles);
+        if (s->o.adapter_trimming) s->ac.add(s->pk, res, p);
+        PackOutput out;
+        format_pack(s->o, s->pk, res, out);
+        s->outs->write(std::move(out));
+        return 0;
+    } catch (const std::exception& e) {
+        s->err = e.what();
+        return -1;
+    }
+}
+
+int fqh_session_add_acc(fqh_session* s, const uint64_t* acc, int max_cycles) {
+    s->acc.add(acc, max_cycles);
+    return 0;
+}
+
+// closes the output files and writes the JSON report (-J); returns the report text
+char* fqh_session_finish(fqh_session* s) {
+    s->outs->close();
+    const std::string t = build_report(s->o, s->acc, s->ac).dump(4);
+    {
+        std::ofstream js(s->o.json_file, std::ios::binary);
+        js << t;
+    }
+    char* r = (char*)std::malloc(t.size() + 1);
+    std::memcpy(r, t.c_str(), t.size() + 1);
+    return r;
+}
+
+void fqh_session_close(fqh_session* s) { delete s; }
+
+}  // extern "C"

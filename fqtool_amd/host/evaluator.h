@@ -1,0 +1,14 @@
+// evaluator.h -- host pre-pass: Evaluator::evaluateReadLen / evaluateAdapterSeq
+// (reference src/evaluator.cpp:84-109, :229-446).
+#pragma once
+
+#include <string>
+
+namespace fqhost {
+
+// longest of the first 1000 reads
+int evaluate_read_len(const std::string& path);
+// detected adapter of one mate file ("" when none), trim_tail1 = -t as the reference passes it
+std::string detect_adapter(const std::string& path, int trim_tail1);
+
+}  // namespace fqhost

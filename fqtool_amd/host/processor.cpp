@@ -1,0 +1,397 @@
+// processor.cpp -- see processor.h.
+#include "processor.h"
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <iostream>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "evaluator.h"
+
+namespace fqhost {
+namespace {
+
+// COMMONCONST::FAILED_TYPES, reference src/common.h:21-29
+const char* failed_type(int code) {
+    switch (code) {
+        case 0: return "passed";
+        case 4: return "failed_polyx_filter";
+        case 8: return "failed_bad_overlap";
+        case 12: return "failed_too_many_n_bases";
+        case 16: return "failed_too_short";
+        case 17: return "failed_too_long";
+        case 20: return "failed_quality_filter";
+        case 24: return "failed_low_complexity";
+        default: return "";
+    }
+}
+
+char comp(char c) {
+    switch (c) {
+        case 'A': case 'a': return 'T';
+        case 'T': case 't': return 'A';
+        case 'C': case 'c': return 'G';
+        case 'G': case 'g': return 'C';
+        default: return 'N';
+    }
+}
+
+// A read as the loop body sees it after its in-place edits.
+struct View {
+    const std::string* name;
+    const std::string* strand;
+    const char* seq;
+    const char* qual;
+    int len;
+};
+
+View view(const Pack& pk, int m, int i, const fq_read_result* r) {
+    const char* s = reinterpret_cast<const char*>(pk.seq[m].data()) + (size_t)i * pk.stride;
+    const char* q = reinterpret_cast<const char*>(pk.qual[m].data()) + (size_t)i * pk.stride;
+    View v{&pk.name[m][(size_t)i], &pk.strand[m][(size_t)i], s, q, (int)pk.len[m][(size_t)i]};
+    if (r && !(r->flags & FQ_RF_NULL)) {  // trimmed in place; a NULL read keeps the original
+        v.seq += r->start;
+        v.qual += r->start;
+        v.len = r->len;
+    }
+    return v;
+}
+
+// Read::toString / toStringWithTag, reference src/read.h:166-178
+void append_read(std::string& out, const View& v, const char* tag = nullptr) {
+    out += *v.name;
+    if (tag) {
+        out += ' ';
+        out += tag;
+    }
+    out += '\n';
+    out.append(v.seq, (size_t)v.len);
+    out += '\n';
+    out += *v.strand;
+    out += '\n';
+    out.append(v.qual, (size_t)v.len);
+    out += '\n';
+}
+
+}  // namespace
+
+std::string merged_name(const std::string& name, int len1, int len2) {
+    const std::string tag = "_merged_" + std::to_string(len1) + "_" + std::to_string(len2);
+    const size_t pos = name.find_first_of(' ');
+    if (pos == std::string::npos) return tag;
+    return name.substr(0, pos - 1) + tag + name.substr(pos);
+}
+
+void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out) {
+    const bool has_unpaired_left = !o.unpaired1.empty();
+    const bool has_failed = !o.failed_out.empty();
+    if (!pk.paired) {  // src/seprocessor.cpp:337-350
+        for (int i = 0; i < pk.n; ++i) {
+            const fq_read_result& r = res[i];
+            const View v = view(pk, 0, i, &r);
+            if (!(r.flags & FQ_RF_NULL) && r.code == FQ_PASS_FILTER) append_read(out.out1, v);
+            else if (has_failed) append_read(out.failed, v, failed_type(r.code));
+        }
+        return;
+    }
+    for (int i = 0; i < pk.n; ++i) {  // src/peprocessor.cpp:351-429
+        const fq_read_result& a = res[2 * (size_t)i];
+        const fq_read_result& b = res[2 * (size_t)i + 1];
+        const bool nn1 = !(a.flags & FQ_RF_NULL), nn2 = !(b.flags & FQ_RF_NULL);
+        const View v1 = view(pk, 0, i, &a), v2 = view(pk, 1, i, &b);
+        bool merge_processed = false;
+        if (o.merge && nn1 && nn2) {
+            if (a.flags & FQ_RF_MERGED) {
+                if (a.code == FQ_PASS_FILTER) {  // OverlapAnalysis::merge, src/overlapanalysis.cpp:74-104
+                    const int m1 = a.m_len1, m2 = a.m_len2, ol = v2.len - m2;
+                    std::string seq(v1.seq, (size_t)m1), qual(v1.qual, (size_t)m1);
+                    for (int j = 0; j < m2; ++j) {
+                        const int src = v2.len - 1 - (ol + j);
+                        seq += comp(v2.seq[src]);
+                        qual += v2.qual[src];
+                    }
+                    const std::string name = merged_name(*v1.name, m1, m2);
+                    View mv{&name, v1.strand, seq.data(), qual.data(), (int)seq.size()};
+                    append_read(out.merged, mv);
+                }
+                merge_processed = true;
+            } else if (!o.discard_unmerged) {
+                if (a.code == FQ_PASS_FILTER) append_read(out.merged, v1);
+                if (b.code == FQ_PASS_FILTER) append_read(out.merged, v2);
+                merge_processed = true;
+            }
+        }
+        if (merge_processed) continue;
+        const bool p1 = nn1 && a.code == FQ_PASS_FILTER, p2 = nn2 && b.code == FQ_PASS_FILTER;
+        if (p1 && p2) {
+            append_read(out.out1, v1);
+            append_read(out.out2, v2);
+        } else if (p1) {
+            if (has_unpaired_left) {
+                append_read(out.unpaired1, v1);
+                if (has_failed) append_read(out.failed, v2, failed_type(b.code));
+            } else if (has_failed) {
+                append_read(out.failed, v1, "paired_read_is_failing");
+                append_read(out.failed, v2, failed_type(b.code));
+            }
+        } else if (p2) {
+            if (has_unpaired_left) {  // the reference checks the LEFT writer here (src/peprocessor.cpp:417)
+                append_read(out.unpaired2, v2);
+                if (has_failed) append_read(out.failed, v1, failed_type(b.code));  // sic: result2 (:420)
+            } else if (has_failed) {
+                append_read(out.failed, v1, failed_type(a.code));
+                append_read(out.failed, v2, "paired_read_is_failing");
+            }
+        }
+    }
+}
+
+namespace {
+
+template <class T>
+class Queue {  // bounded FIFO between pipeline threads
+   public:
+    explicit Queue(size_t cap) : cap_(cap) {}
+    void push(T v) {
+        std::unique_lock<std::mutex> l(m_);
+        not_full_.wait(l, [&] { return q_.size() < cap_; });
+        q_.push_back(std::move(v));
+        not_empty_.notify_one();
+    }
+    bool pop(T& v) {
+        std::unique_lock<std::mutex> l(m_);
+        not_empty_.wait(l, [&] { return !q_.empty() || closed_; });
+        if (q_.empty()) return false;
+        v = std::move(q_.front());
+        q_.pop_front();
+        not_full_.notify_one();
+        return true;
+    }
+    void close() {
+        std::lock_guard<std::mutex> l(m_);
+        closed_ = true;
+        not_empty_.notify_all();
+    }
+
+   private:
+    size_t cap_;
+    std::deque<T> q_;
+    bool closed_ = false;
+    std::mutex m_;
+    std::condition_variable not_full_, not_empty_;
+};
+
+}  // namespace
+
+// WriterThread (src/writerthread.cpp): one thread per output file, strings written in order
+class AsyncWriter {
+   public:
+    AsyncWriter(const std::string& path, int level) : w_(path, level), q_(16), t_([this] { loop(); }) {}
+    ~AsyncWriter() {
+        q_.close();
+        t_.join();
+    }
+    void write(std::string s) {
+        if (!s.empty()) q_.push(std::move(s));
+    }
+
+   private:
+    void loop() {
+        std::string s;
+        while (q_.pop(s)) w_.write(s);
+    }
+    Writer w_;
+    Queue<std::string> q_;
+    std::thread t_;
+};
+
+OutputSet::OutputSet(const Options& o) : paired_(o.paired()) {
+    if (paired_) {
+        if (!o.unpaired1.empty()) wu1_.reset(new AsyncWriter(o.unpaired1, o.compression));
+        if (!o.unpaired2.empty() && o.unpaired2 != o.unpaired1) wu2_.reset(new AsyncWriter(o.unpaired2, o.compression));
+        if (o.merge && !o.merge_out.empty()) wm_.reset(new AsyncWriter(o.merge_out, o.compression));
+    }
+    if (!o.failed_out.empty()) wf_.reset(new AsyncWriter(o.failed_out, o.compression));
+    if (!o.out1.empty()) {
+        w1_.reset(new AsyncWriter(o.out1, o.compression));
+        if (paired_ && !o.out2.empty()) w2_.reset(new AsyncWriter(o.out2, o.compression));
+    }
+}
+
+OutputSet::~OutputSet() { close(); }
+
+void OutputSet::write(PackOutput&& out) {
+    if (wm_) wm_->write(std::move(out.merged));
+    if (wf_) wf_->write(std::move(out.failed));
+    if (w1_ && (!paired_ || w2_)) {  // PE writes the pair outputs only with both writers (:469)
+        w1_->write(std::move(out.out1));
+        if (w2_) w2_->write(std::move(out.out2));
+    }
+    if (wu1_) wu1_->write(std::move(out.unpaired1));
+    if (wu2_) wu2_->write(std::move(out.unpaired2));
+}
+
+void OutputSet::close() {
+    w1_.reset();
+    w2_.reset();
+    wu1_.reset();
+    wu2_.reset();
+    wf_.reset();
+    wm_.reset();
+}
+
+namespace {
+
+struct Engine {
+    fq_engine* e = nullptr;
+    int max_cycles = 0;
+    int max_batch = 0;
+    int max_stride = 0;
+    ~Engine() {
+        if (e) fq_engine_destroy(e);
+    }
+};
+
+int round16(int x) { return (x + 15) & ~15; }
+
+void make_engine(Engine& eng, const Options& o, int max_cycles, int max_batch, int max_stride) {
+    if (eng.e) {
+        fq_engine_destroy(eng.e);
+        eng.e = nullptr;
+    }
+    fq_params p = o.to_params(max_cycles);
+    const int rc = fq_engine_create(&p, o.device, max_batch, max_stride, &eng.e);
+    if (rc != FQ_OK) throw std::runtime_error(std::string("fq_engine_create: ") + fq_engine_last_error(nullptr));
+    eng.max_cycles = max_cycles;
+    eng.max_batch = max_batch;
+    eng.max_stride = max_stride;
+}
+
+void drain(Engine& eng, HostAcc& acc) {
+    if (!eng.e) return;
+    std::vector<uint64_t> buf(fq_engine_acc_words(eng.e));
+    if (fq_engine_read_acc(eng.e, buf.data(), buf.size()) != FQ_OK)
+        throw std::runtime_error(std::string("fq_engine_read_acc: ") + fq_engine_last_error(eng.e));
+    acc.add(buf.data(), eng.max_cycles);
+    fq_engine_reset_acc(eng.e);
+}
+
+void log(const std::string& s) {
+    std::time_t t = std::time(nullptr);
+    char d[64];
+    std::strftime(d, sizeof d, "[%Y-%m-%d %H:%M:%S] ", std::localtime(&t));
+    std::cerr << d << s << std::endl;
+}
+
+}  // namespace
+
+Options prepare_options(int argc, char** argv) {
+    Options o = parse_cli(argc, argv);
+    try {  // Options::validate failures end in error_exit (src/util.h), exit status 255
+        o.update(argc, argv);
+        o.validate();
+    } catch (const CliError& e) {
+        throw std::runtime_error(e.what());
+    }
+    // Evaluator pre-pass, src/main.cpp:126-143
+    if (!o.in1.empty()) o.est_seq_len1 = evaluate_read_len(o.in1);
+    if (!o.in2.empty()) o.est_seq_len2 = evaluate_read_len(o.in2);
+    if (o.detect_pe_adapter) {
+        // an interleaved input has no read2 file: opening "" fails as in the reference
+        o.detected_adapter1 = detect_adapter(o.in1, o.tail1);
+        o.detected_adapter2 = detect_adapter(o.in2, o.tail1);
+    }
+    return o;
+}
+
+int run_tool(int argc, char** argv) {
+    Options o;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        o = prepare_options(argc, argv);
+    } catch (const CliError& e) {  // App::exit + FailureMessage::simple (src/CLI.hpp)
+        if (e.code == 0) std::cout << e.what() << std::endl;
+        else std::cerr << e.what() << "\nRun with --help for more information." << std::endl;
+        return e.code;
+    } catch (const std::exception& e) {
+        std::cerr << "ERROR: " << e.what() << std::endl;
+        return 255;
+    }
+    try {
+        const bool paired = o.paired();
+        const size_t pack_n = std::max<size_t>(o.max_reads_in_pack, 262144);
+        int est = std::max(o.est_seq_len1, paired ? o.est_seq_len2 : 0);
+        Engine eng;
+        make_engine(eng, o, std::max(16, round16(o.merge ? 2 * est : est)), (int)pack_n, round16(std::max(est, 16)));
+        OutputSet outs(o);
+        // reader thread -> engine + formatting (this thread) -> writer threads
+        Queue<std::unique_ptr<Pack>> packs(2);
+        std::exception_ptr reader_err;
+        std::thread reader([&] {
+            try {
+                PackReader pr(o.in1, o.in2, o.interleaved, o.phred64);
+                for (;;) {
+                    std::unique_ptr<Pack> pk(new Pack());
+                    if (!pr.next(*pk, pack_n)) break;
+                    packs.push(std::move(pk));
+                }
+            } catch (...) {
+                reader_err = std::current_exception();
+            }
+            packs.close();
+        });
+        HostAcc acc(o.insert_size_max);
+        AdapterCounts ac;
+        std::vector<fq_read_result> res;
+        std::unique_ptr<Pack> pk;
+        uint64_t reads = 0;
+        double engine_s = 0;
+        while (packs.pop(pk)) {
+            int max1 = 0, max2 = 0;
+            for (uint16_t l : pk->len[0]) max1 = std::max(max1, (int)l);
+            if (paired)
+                for (uint16_t l : pk->len[1]) max2 = std::max(max2, (int)l);
+            const int need = o.merge ? max1 + max2 : std::max(max1, max2);
+            if (need > eng.max_cycles || pk->stride > eng.max_stride || pk->n > eng.max_batch) {
+                drain(eng, acc);  // keep what the old engine accumulated, then grow it
+                make_engine(eng, o, std::max(eng.max_cycles, round16(need)), std::max(eng.max_batch, pk->n),
+                            std::max(eng.max_stride, pk->stride));
+            }
+            res.resize((size_t)pk->n * (paired ? 2 : 1));
+            const fq_batch b = pk->batch();
+            const auto e0 = std::chrono::steady_clock::now();
+            if (fq_engine_process(eng.e, &b, res.data()) != FQ_OK)
+                throw std::runtime_error(std::string("fq_engine_process: ") + fq_engine_last_error(eng.e));
+            engine_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - e0).count();
+            const fq_params p = o.to_params(eng.max_cycles);
+            if (o.adapter_trimming) ac.add(*pk, res.data(), p);
+            PackOutput out;
+            format_pack(o, *pk, res.data(), out);
+            outs.write(std::move(out));
+            reads += (uint64_t)pk->n * (paired ? 2 : 1);
+        }
+        reader.join();
+        if (reader_err) std::rethrow_exception(reader_err);
+        drain(eng, acc);
+        outs.close();
+        const Json rep = build_report(o, acc, ac);
+        std::ofstream js(o.json_file, std::ios::binary);
+        js << rep.dump(4);
+        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        log("fqtool-amd: " + std::to_string(reads) + " reads, wall " + std::to_string(wall) + " s, engine " +
+            std::to_string(engine_s) + " s; JSON report " + o.json_file + " (no HTML report in this build)");
+    } catch (const std::exception& e) {
+        std::cerr << "ERROR: " << e.what() << std::endl;
+        return 255;
+    }
+    return 0;
+}
+
+}  // namespace fqhost

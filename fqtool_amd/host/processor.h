@@ -1,0 +1,56 @@
+// processor.h -- the host pipeline around the engine: the reference's
+// Processor / PairEndProcessor / SingleEndProcessor plumbing (src/processor.cpp:10-19,
+// src/peprocessor.cpp:99-247, src/seprocessor.cpp) with the per-pack loop body delegated to the
+// gfx950 engine through the C-ABI (include/fqengine.h).
+//
+// Threads: one reader (FASTQ parse + pack build), the engine caller (H2D, kernels, D2H, output
+// formatting in input order -- identical to the reference run with -w 1), one writer per output
+// file.  Packs are processed strictly in input order.
+#pragma once
+
+#include <memory>
+#include <string>
+
+#include "fastq.h"
+#include "options.h"
+#include "report.h"
+
+namespace fqhost {
+
+// Output text of one pack, per destination (src/peprocessor.cpp:262-269)
+struct PackOutput {
+    std::string out1, out2, unpaired1, unpaired2, failed, merged;
+};
+
+class AsyncWriter;
+
+// The output files of a run and the rule for which text goes where
+// (PairEndProcessor::initOutput / SingleEndProcessor::initOutput and the tail of the pack loops,
+// src/peprocessor.cpp:39-61, :457-492; src/seprocessor.cpp).  Each file has its own writer thread.
+class OutputSet {
+   public:
+    explicit OutputSet(const Options& o);
+    ~OutputSet();
+    void write(PackOutput&& out);
+    void close();  // flushes and closes every file
+
+   private:
+    bool paired_;
+    std::unique_ptr<AsyncWriter> w1_, w2_, wu1_, wu2_, wf_, wm_;
+};
+
+// Builds the output text of one processed pack from the engine's per-read records, exactly as
+// the loop body of processPairEnd / processSingleEnd appends to its strings.
+void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out);
+
+// OverlapAnalysis::merge name rule (src/overlapanalysis.cpp:93-101)
+std::string merged_name(const std::string& name, int len1, int len2);
+
+// CLI parse + Options::update/validate + the Evaluator pre-pass (read length estimate,
+// PE adapter detection), src/main.cpp:100-143.  Throws CliError / std::runtime_error.
+Options prepare_options(int argc, char** argv);
+
+// The whole tool: returns the process exit code.
+int run_tool(int argc, char** argv);
+
+}  // namespace fqhost

@@ -1,0 +1,252 @@
+// report.cpp -- see report.h.
+#include "report.h"
+
+#include <algorithm>
+#include <numeric>
+
+#include "fastq.h"
+
+namespace fqhost {
+
+HostAcc::HostAcc(int insert_size_max) : ism_(insert_size_max) {
+    head_.assign((size_t)FQ_ACC_INSERT + (size_t)insert_size_max + 1, 0);
+}
+
+void HostAcc::add(const uint64_t* acc, int max_cycles) {
+    for (size_t i = 0; i < head_.size(); ++i) head_[i] += acc[i];
+    if (max_cycles > cap_) {
+        for (auto& v : cyc_) v.resize((size_t)max_cycles * 16, 0);
+        cap_ = max_cycles;
+    }
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t* st = acc + fq_acc_stats_offset(ism_, max_cycles, k);
+        for (int f = 0; f < 4; ++f) st_[k][f] += st[f];
+        const uint64_t* cy = st + FQ_ST_CYCLES;
+        for (size_t i = 0; i < (size_t)max_cycles * 16; ++i) cyc_[k][i] += cy[i];
+    }
+}
+
+void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_params& p) {
+    const int mates = pk.paired ? 2 : 1;
+    for (int i = 0; i < pk.n; ++i) {
+        for (int m = 0; m < mates; ++m) {
+            const fq_read_result& r = res[(size_t)i * mates + m];
+            if (!(r.flags & (FQ_RF_AD_OVERLAP | FQ_RF_AD_SEQ)) || r.ad_len == 0) continue;
+            std::string s;
+            if (r.flags & FQ_RF_AD_NEG) {
+                const uint8_t* ad = m ? p.adapter2 : p.adapter1;
+                s.assign(reinterpret_cast<const char*>(ad) + r.ad_pos, r.ad_len);
+            } else {
+                s.assign(reinterpret_cast<const char*>(pk.seq[m].data()) + (size_t)i * pk.stride + r.ad_pos, r.ad_len);
+            }
+            ++(m ? r2 : r1)[s];
+        }
+    }
+}
+
+namespace {
+
+// Stats::summarize + reportJson for one accumulator block (src/stats.cpp:147-228, :392-430)
+struct Summary {
+    uint64_t reads = 0, bases = 0, q20 = 0, q30 = 0, gc = 0, length_sum = 0;
+    int cycles = 0;
+    Json json;
+    int mean_length() const { return reads ? (int)(length_sum / reads) : 0; }
+};
+
+Summary summarize(const HostAcc& a, int k) {
+    Summary s;
+    s.reads = a.stat(k, FQ_ST_READS);
+    s.length_sum = a.stat(k, FQ_ST_LENGTH_SUM);
+    s.q20 = a.stat(k, FQ_ST_Q20);
+    s.q30 = a.stat(k, FQ_ST_Q30);
+    auto total_base = [&](int c) {
+        uint64_t t = 0;
+        for (int b = 0; b < 8; ++b) t += a.cyc(k, c, b);
+        return t;
+    };
+    auto total_qual = [&](int c) {
+        uint64_t t = 0;
+        for (int b = 0; b < 8; ++b) t += a.cyc(k, c, 8 + b);
+        return t;
+    };
+    int c = 0;
+    for (c = 0; c < a.cycles_capacity(); ++c) {
+        const uint64_t tb = total_base(c);
+        s.bases += tb;
+        if (tb == 0) break;
+    }
+    s.cycles = c;
+    const int A = 'A' & 7, T = 'T' & 7, C = 'C' & 7, G = 'G' & 7, N = 'N' & 7;
+    uint64_t content_g = 0, content_c = 0;
+    for (int i = 0; i < s.cycles; ++i) {
+        content_g += a.cyc(k, i, G);
+        content_c += a.cyc(k, i, C);
+    }
+    s.gc = content_g + content_c;
+    Json qc = Json::object(), cc = Json::object();
+    Json mean = Json::array();
+    std::vector<double> meanv((size_t)s.cycles);
+    for (int i = 0; i < s.cycles; ++i) {
+        meanv[(size_t)i] = (double)total_qual(i) / (double)total_base(i);
+        mean.push(Json::d(meanv[(size_t)i]));
+    }
+    const char names[5] = {'A', 'T', 'C', 'G', 'N'};
+    const int cls[5] = {A, T, C, G, N};
+    for (int j = 0; j < 5; ++j) {
+        Json qv = Json::array(), cv = Json::array();
+        for (int i = 0; i < s.cycles; ++i) {
+            const uint64_t cnt = a.cyc(k, i, cls[j]);
+            qv.push(Json::d(cnt == 0 ? meanv[(size_t)i] : (double)a.cyc(k, i, 8 + cls[j]) / (double)cnt));
+            cv.push(Json::d((double)cnt / (double)total_base(i)));
+        }
+        if (names[j] != 'N') qc[std::string(1, names[j])] = qv;
+        cc[std::string(1, names[j])] = cv;
+    }
+    qc["Mean"] = mean;
+    Json gcv = Json::array();
+    for (int i = 0; i < s.cycles; ++i)
+        gcv.push(Json::d((double)(a.cyc(k, i, G) + a.cyc(k, i, C)) / (double)total_base(i)));
+    cc["GC"] = gcv;
+    s.json["TotalReads"] = Json::u(s.reads);
+    s.json["TotalBases"] = Json::u(s.bases);
+    s.json["Q20Bases"] = Json::u(s.q20);
+    s.json["Q30Bases"] = Json::u(s.q30);
+    s.json["TotalCycles"] = Json::i(s.cycles);
+    s.json["QualityCurves"] = qc;
+    s.json["ContentCurves"] = cc;
+    return s;
+}
+
+// FilterResult::reportAdaptersJsonDetails, src/filterresult.cpp:231-251 (null when no adapters)
+Json adapter_details(const std::map<std::string, size_t>& m) {
+    size_t total = 0;
+    for (auto& e : m) total += e.second;
+    Json j;
+    if (total == 0) return j;
+    const double dt = (double)total;
+    size_t reported = 0;
+    for (auto& e : m) {
+        if (e.second / dt < 0.01) continue;
+        j[e.first] = Json::u(e.second);
+        reported += e.second;
+    }
+    if (total - reported > 0) j["Others"] = Json::u(total - reported);
+    return j;
+}
+
+}  // namespace
+
+Json build_report(const Options& o, const HostAcc& a, const AdapterCounts& ac) {
+    const bool paired = o.paired();
+    Summary pre1 = summarize(a, 0), post1 = summarize(a, 2);
+    Summary pre2, post2;
+    if (paired) {
+        pre2 = summarize(a, 1);
+        post2 = summarize(a, 3);
+    }
+    // JsonReporter::report, src/jsonreporter.cpp:23-162
+    long pre_reads = (long)(pre1.reads + pre2.reads), pre_bases = (long)(pre1.bases + pre2.bases);
+    long pre_q20 = (long)(pre1.q20 + pre2.q20), pre_q30 = (long)(pre1.q30 + pre2.q30), pre_gc = (long)(pre1.gc + pre2.gc);
+    long post_reads = (long)(post1.reads + post2.reads), post_bases = (long)(post1.bases + post2.bases);
+    long post_q20 = (long)(post1.q20 + post2.q20), post_q30 = (long)(post1.q30 + post2.q30),
+         post_gc = (long)(post1.gc + post2.gc);
+    auto rate = [](long num, long den) { return den == 0 ? 0.0 : (double)num / den; };
+    Json rep = Json::object();
+    Json before = Json::object();
+    before["TotalReads"] = Json::i(pre_reads);
+    before["TotalBases"] = Json::i(pre_bases);
+    before["Q20Bases"] = Json::i(pre_q20);
+    before["Q30Bases"] = Json::i(pre_q30);
+    before["Q20BaseRate"] = Json::d(rate(pre_q20, pre_bases));
+    before["Q30BaseRate"] = Json::d(rate(pre_q30, pre_bases));
+    before["Read1Length"] = Json::i(pre1.mean_length());
+    if (paired) before["Read2Length"] = Json::i(pre2.mean_length());
+    before["GCRate"] = Json::d(rate(pre_gc, pre_bases));
+    rep["Summary"]["BeforeFiltering"] = before;
+    Json after = Json::object();
+    after["TotalReads"] = Json::i(post_reads);
+    after["TotalBases"] = Json::i(post_bases);
+    after["Q20Bases"] = Json::i(post_q20);
+    after["Q30Bases"] = Json::i(post_q30);
+    after["Q20BaseRate"] = Json::d(rate(post_q20, post_bases));
+    after["Q30BaseRate"] = Json::d(rate(post_q30, post_bases));
+    after["Read1Length"] = Json::i(post1.mean_length());
+    if (paired) after["Read2Length"] = Json::i(post2.mean_length());
+    after["GCRate"] = Json::d(rate(post_gc, post_bases));
+    rep["Summary"]["AfterFiltering"] = after;
+
+    Json fr = Json::object();  // FilterResult::reportJsonBasic, src/filterresult.cpp:204-222
+    fr["PassedFilterReads"] = Json::u(a.filter(FQ_PASS_FILTER));
+    fr["LowQualityReads"] = Json::u(a.filter(FQ_FAIL_QUALITY));
+    fr["TooManyNReads"] = Json::u(a.filter(FQ_FAIL_N_BASE));
+    if (o.complexity_filter) fr["LowComplexityReads"] = Json::u(a.filter(FQ_FAIL_COMPLEXITY));
+    if (o.length_filter) {
+        fr["TooShortReads"] = Json::u(a.filter(FQ_FAIL_LENGTH));
+        if (o.max_len > 0) fr["TooLongReads"] = Json::u(a.filter(FQ_FAIL_TOO_LONG));
+    }
+    rep["FilterResult"] = fr;
+
+    if (paired) {  // insert size, src/jsonreporter.cpp:107-114 + getPeakInsertSize src/peprocessor.cpp:249-259
+        const int ism = a.insert_size_max();
+        Json ins = Json::object();
+        int peak = 0;
+        long maxc = -1;
+        Json hist = Json::array();
+        for (int i = 0; i < ism; ++i) {
+            const long v = (long)a.head()[FQ_ACC_INSERT + i];
+            if (v > maxc) {
+                peak = i;
+                maxc = v;
+            }
+            hist.push(Json::i((int32_t)v));
+        }
+        ins["Peak"] = Json::i(peak);
+        ins["Unknown"] = Json::i((long)a.head()[FQ_ACC_INSERT + ism]);
+        ins["Histogram"] = hist;
+        rep["InsertSize"] = ins;
+    }
+
+    if (o.adapter_trimming) {  // FilterResult::reportAdaptersJsonSummary, src/filterresult.cpp:296-318
+        Json at = Json::object();
+        at["AdapterTrimmedReads"] = Json::u(a.head()[FQ_ACC_ADAPTER_READS]);
+        at["AdapterTrimmedBases"] = Json::u(a.head()[FQ_ACC_ADAPTER_BASES]);
+        at["Read1AdapterSequence"] = Json::s(!o.adapter1.empty() ? o.adapter1 : o.detected_adapter1);
+        if (paired) at["Read2AdapterSequence"] = Json::s(!o.adapter2.empty() ? o.adapter2 : o.detected_adapter2);
+        at["Read1AdapterCounts"] = adapter_details(ac.r1);
+        if (paired) at["Read2AdapterCounts"] = adapter_details(ac.r2);
+        rep["AdapterTrim"] = at;
+    }
+
+    if (o.polyx || o.polyg) {  // FilterResult::reportPolyXTrimJson, src/filterresult.cpp:380-397
+        Json px = Json::object();
+        const char atcg[5] = {'A', 'T', 'C', 'G', 'N'};
+        uint64_t rsum = 0, bsum = 0;
+        Json pr = Json::object(), pb = Json::object();
+        for (int b = 0; b < 5; ++b) {
+            const uint64_t r = a.head()[FQ_ACC_POLYX_READS + b], bs = a.head()[FQ_ACC_POLYX_BASES + b];
+            rsum += r;
+            bsum += bs;
+            pr[std::string(1, atcg[b])] = Json::u(r);
+            pb[std::string(1, atcg[b])] = Json::u(bs);
+        }
+        // std::accumulate(..., 0) keeps an int: the totals wrap at 32 bits
+        px["TotalPolyxTrimmedReads"] = Json::i((int32_t)(uint32_t)rsum);
+        px["PolyxTrimmedReads"] = pr;
+        px["TotalPolyxTrimmedBases"] = Json::i((int32_t)(uint32_t)bsum);
+        px["PolyxTrimmedBases"] = pb;
+        rep["PolyxTrimming"] = px;
+    }
+    rep["Read1BeforeFiltering"] = pre1.json;
+    if (paired) rep["Read2BeforeFiltering"] = pre2.json;
+    rep[o.merge ? "MergedAndFiltered" : "Read1AfterFiltering"] = post1.json;
+    if (paired && !o.merge) rep["Read2AfterFiltering"] = post2.json;
+    Json sw = Json::object();
+    sw["CWD"] = Json::s(o.cwd);
+    sw["Command"] = Json::s(o.command);
+    sw["Version"] = Json::s(o.version);
+    rep["Software"] = sw;
+    return rep;
+}
+
+}  // namespace fqhost

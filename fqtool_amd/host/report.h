@@ -1,0 +1,52 @@
+// report.h -- accumulators -> the reference's JSON report.
+//
+// HostAcc keeps the engine's flat accumulator (include/fqengine.h layout) with a growable cycle
+// count so packs with longer reads can be absorbed by re-creating the engine.  build_report
+// restates Stats::summarize / reportJson (src/stats.cpp:147-228, :392-430),
+// FilterResult::reportJson* (src/filterresult.cpp:204-397) and JsonReporter::report
+// (src/jsonreporter.cpp:23-162).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/fqengine.h"
+#include "json.h"
+#include "options.h"
+
+namespace fqhost {
+
+struct Pack;
+
+class HostAcc {
+   public:
+    explicit HostAcc(int insert_size_max = 512);
+    // add an engine accumulator block of the given max_cycles
+    void add(const uint64_t* acc, int max_cycles);
+    // raw add of one counter (tests)
+    const std::vector<uint64_t>& head() const { return head_; }
+    int cycles_capacity() const { return cap_; }
+    uint64_t filter(int code) const { return head_[FQ_ACC_FILTER + code]; }
+    uint64_t stat(int k, int field) const { return st_[k][field]; }
+    uint64_t cyc(int k, int c, int slot) const { return (size_t)c < cyc_[k].size() / 16 ? cyc_[k][(size_t)c * 16 + slot] : 0; }
+    int insert_size_max() const { return ism_; }
+
+   private:
+    int ism_;
+    int cap_ = 0;
+    std::vector<uint64_t> head_;   // everything before the stats blocks
+    uint64_t st_[4][4] = {};       // reads, length_sum, q20, q30
+    std::vector<uint64_t> cyc_[4];  // [cycle][16]
+};
+
+// FilterResult's adapter string -> count maps (src/filterresult.cpp:138-177)
+struct AdapterCounts {
+    std::map<std::string, size_t> r1, r2;
+    void add(const Pack& pk, const fq_read_result* res, const fq_params& p);
+};
+
+Json build_report(const Options& o, const HostAcc& acc, const AdapterCounts& ac);
+
+}  // namespace fqhost

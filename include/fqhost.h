@@ -1,0 +1,64 @@
+/* fqhost.h -- C-ABI of the host side (libfqhost.so): the reference's CLI/Processor plumbing
+ * around the engine of fqengine.h.
+ *
+ * fqh_run is the whole tool (the reference's main(), src/main.cpp:11-176, with the per-pack loop
+ * bodies of src/peprocessor.cpp:276-441 / src/seprocessor.cpp:271-352 running on the GPU).
+ *
+ * The session calls expose the same pipeline one pack at a time with the engine call left to the
+ * caller, so a host that keeps its own Processor threads can read packs, hand
+ * them to fq_engine_process / fq_engine_process_device and get the reference's output text and
+ * JSON back.  Tests drive it with the CPU oracle in the engine's place.
+ */
+#ifndef FQHOST_H
+#define FQHOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fqengine.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The tool: same arguments, outputs, messages and exit codes as the reference binary. */
+int fqh_run(int argc, char** argv);
+
+/* nlohmann::json 3.5.0 number formatting of a double (Grisu2, src/json.hpp); returns length. */
+int fqh_json_double(double v, char* buf, size_t n);
+/* OverlapAnalysis::merge read name (src/overlapanalysis.cpp:93-101). */
+int fqh_merged_name(const char* name, int len1, int len2, char* buf, size_t n);
+/* Evaluator::evaluateReadLen / detectAdapter (src/evaluator.cpp:24-86, :88-260). */
+int fqh_evaluate_read_len(const char* path);
+int fqh_detect_adapter(const char* path, int trim_tail1, char* buf, size_t n);
+
+/* JSON report from one accumulator block; argv_blob = argc NUL-terminated strings back to back;
+ * side = lines "D1\tSEQ", "D2\tSEQ" (detected adapters), "1\tSEQ\tN", "2\tSEQ\tN" (adapter counts).
+ * Returns a malloc'd string (free with fqh_free); starts with "ERROR: " on failure. */
+char* fqh_report_json(int argc, const char* argv_blob, const uint64_t* acc, int max_cycles, const char* side);
+void fqh_free(char* p);
+
+typedef struct fqh_session fqh_session;
+/* parses argv like the tool (incl. the Evaluator pre-pass) and opens the inputs; on failure
+ * returns -1 with *out still set so fqh_session_error can be read (then close it) */
+int fqh_session_open(int argc, char** argv, fqh_session** out);
+const char* fqh_session_error(const fqh_session* s);
+/* engine parameters for this command line at a given stats cycle capacity */
+int fqh_session_params(fqh_session* s, int max_cycles, fq_params* out);
+/* next pack (up to max_n records/pairs): 1 = got one, 0 = end of input, -1 = error.
+ * The batch points into session memory valid until the next call. */
+int fqh_session_next(fqh_session* s, int max_n, fq_batch* out);
+/* per-read records of the current pack (fq_engine_process output) -> output files, written with
+ * the tool's rules, and adapter string counts */
+int fqh_session_consume(fqh_session* s, const fq_read_result* res, int max_cycles);
+/* adds an accumulator block (fq_engine_read_acc layout at max_cycles) */
+int fqh_session_add_acc(fqh_session* s, const uint64_t* acc, int max_cycles);
+/* closes the outputs, writes the JSON report file (-J) and returns its text (malloc'd, fqh_free) */
+char* fqh_session_finish(fqh_session* s);
+void fqh_session_close(fqh_session* s);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FQHOST_H */

@@ -1,0 +1,120 @@
+"""End-to-end helpers: the golden manifest written by tests/golden/make_e2e.py (reference binary
+runs), argv construction, and comparison of a run directory against it."""
+import ctypes
+import gzip
+import hashlib
+import json
+import os
+import re
+
+import numpy as np
+
+from fqtool_amd import abi
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+INPUTS = os.path.join(GOLDEN, "inputs")
+E2E = os.path.join(GOLDEN, "e2e")
+
+
+def manifest():
+    with open(os.path.join(E2E, "manifest.json")) as f:
+        return json.load(f)
+
+
+def ok_cases():
+    return sorted(k for k, v in manifest().items() if v["exit"] == 0)
+
+
+def err_cases():
+    return sorted(k for k, v in manifest().items() if v["exit"] != 0)
+
+
+def argv_for(binary, case, outdir):
+    """Same argument order make_e2e.py used for the reference."""
+    args = manifest()[case]["args"]
+    argv = [binary, "-w", "1", "-J", os.path.join(outdir, "report.json"), "-H", os.path.join(outdir, "report.html")]
+    return argv + args.format(**{"in": INPUTS, "out": outdir}).split()
+
+
+def mask_software(text):
+    text = re.sub(r'"CWD": "[^"]*"', '"CWD": ""', text)
+    return re.sub(r'"Command": "[^"]*"', '"Command": ""', text)
+
+
+def golden_json(case):
+    with gzip.open(os.path.join(E2E, manifest()[case]["json"]), "rt") as f:
+        return f.read()
+
+
+def digest(path):
+    data = open(path, "rb").read()
+    if path.endswith(".gz"):
+        data = gzip.decompress(data) if data else b""
+    return {"sha256": hashlib.sha256(data).hexdigest(), "lines": data.count(b"\n")}
+
+
+def check_outputs(case, outdir, report_text=None):
+    """Asserts every output file and the JSON report equal the reference's."""
+    m = manifest()[case]
+    present = {}
+    for name in ["o1.fq", "o2.fq", "o1.fq.gz", "o2.fq.gz", "u1.fq", "u2.fq", "u.fq", "failed.fq", "merged.fq"]:
+        fp = os.path.join(outdir, name)
+        if os.path.exists(fp):
+            present[name] = digest(fp)
+    assert sorted(present) == sorted(m["outputs"]), (sorted(present), sorted(m["outputs"]))
+    for name, d in m["outputs"].items():
+        assert present[name] == d, "%s: %s differs from the reference (%s vs %s lines)" % (
+            case, name, present[name]["lines"], d["lines"])
+    if report_text is None:
+        with open(os.path.join(outdir, "report.json")) as f:
+            report_text = f.read()
+    ref = mask_software(golden_json(case))
+    got = mask_software(report_text)
+    if got != ref:
+        a, b = json.loads(got), json.loads(ref)
+        for k in sorted(set(a) | set(b)):
+            assert a.get(k) == b.get(k), "%s: JSON section %s differs" % (case, k)
+        assert got == ref, "%s: JSON text differs (number formatting / key order)" % case
+
+
+def round16(x):
+    return (x + 15) & ~15
+
+
+def run_session_with_oracle(host, orc, argv, max_n=1500):
+    """The tool's host pipeline (libfqhost session API) with the CPU oracle in the engine's place:
+    checks the host side (parsing, packing, formatting, writers, report) on CPU."""
+    enc = [a.encode() for a in argv]
+    arr = (ctypes.c_char_p * len(enc))(*enc)
+    s = ctypes.c_void_p()
+    rc = host.fqh_session_open(len(enc), arr, ctypes.byref(s))
+    try:
+        assert rc == 0, host.fqh_session_error(s)
+        p0 = abi.FqParams()
+        host.fqh_session_params(s, 16, ctypes.byref(p0))
+        while True:
+            b = abi.FqBatch()
+            r = host.fqh_session_next(s, max_n, ctypes.byref(b))
+            assert r >= 0, host.fqh_session_error(s)
+            if r == 0:
+                break
+            n = b.n
+            paired = bool(b.seq2)
+            l1 = np.ctypeslib.as_array(ctypes.cast(b.len1, ctypes.POINTER(ctypes.c_uint16)), (n,))
+            m1 = int(l1.max()) if n else 0
+            m2 = 0
+            if paired:
+                l2 = np.ctypeslib.as_array(ctypes.cast(b.len2, ctypes.POINTER(ctypes.c_uint16)), (n,))
+                m2 = int(l2.max()) if n else 0
+            need = m1 + m2 if p0.merge_enabled else max(m1, m2)
+            mc = max(16, round16(need))
+            p = abi.FqParams()
+            host.fqh_session_params(s, mc, ctypes.byref(p))
+            res = np.zeros(n * (2 if paired else 1), dtype=np.dtype(abi.RESULT_DTYPE_FIELDS))
+            acc = np.zeros(abi.acc_words(p.insert_size_max, mc), np.uint64)
+            assert orc.orc_process_batch(ctypes.byref(p), ctypes.byref(b), res.ctypes.data, acc.ctypes.data) == 0
+            assert host.fqh_session_consume(s, res.ctypes.data, mc) == 0, host.fqh_session_error(s)
+            host.fqh_session_add_acc(s, acc.ctypes.data, mc)
+        return abi.take_string(host, host.fqh_session_finish(s))
+    finally:
+        host.fqh_session_close(s)

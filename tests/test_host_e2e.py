@@ -1,0 +1,54 @@
+"""End-to-end parity of the tool against the reference binary's outputs (tests/golden/e2e, made
+by tests/golden/make_e2e.py from oracle/_ref/fqtool_ref runs with -w 1).
+
+CPU: the host pipeline (CLI, FASTQ packing, output formatting/writers, JSON report) driven through
+the libfqhost session API with the CPU oracle standing in for the engine, and the CLI's error
+behaviour (exit status + message) of the real binary, which fails before touching a device.
+GPU: the real `fqtool` binary, engine on MI355X, byte-identical outputs and JSON.
+"""
+import os
+import subprocess
+
+import pytest
+
+import e2e_util as E
+from fqtool_amd import abi
+
+
+@pytest.fixture(scope="module")
+def host():
+    if not (os.path.exists(abi.HOST_LIB) and os.path.exists(abi.FQTOOL_BIN)):
+        subprocess.run(["make", "-s", "-C", abi.REPO_DIR, "host"], check=True)
+    return abi.load_host()
+
+
+@pytest.mark.parametrize("case", E.ok_cases())
+def test_host_pipeline_with_oracle_engine(case, host, oracle, tmp_path):
+    argv = E.argv_for("fqtool", case, str(tmp_path))
+    report = E.run_session_with_oracle(host, oracle, argv)
+    E.check_outputs(case, str(tmp_path), report)
+
+
+@pytest.mark.parametrize("case", E.err_cases())
+def test_cli_errors_match_reference(case, tmp_path):
+    if not os.path.exists(abi.FQTOOL_BIN):
+        subprocess.run(["make", "-s", "-C", abi.REPO_DIR, "host"], check=True)
+    m = E.manifest()[case]
+    p = subprocess.run(E.argv_for(abi.FQTOOL_BIN, case, str(tmp_path)), capture_output=True, cwd=tmp_path,
+                       timeout=120)
+    assert p.returncode == m["exit"], p.stderr
+    err = p.stderr.decode().replace(E.INPUTS, "{in}").replace(str(tmp_path), "{out}")
+    if m["exit"] == 255:
+        assert [l for l in err.splitlines() if l.startswith("ERROR:")] == \
+            [l for l in m["stderr"].splitlines() if l.startswith("ERROR:")]
+    else:
+        assert err == m["stderr"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", E.ok_cases())
+def test_fqtool_binary_matches_reference(case, tmp_path):
+    p = subprocess.run(E.argv_for(abi.FQTOOL_BIN, case, str(tmp_path)), capture_output=True, cwd=tmp_path,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    E.check_outputs(case, str(tmp_path))
