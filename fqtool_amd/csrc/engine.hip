@@ -116,7 +116,7 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     if ((he = hipEventCreate(&e->ev0)) != hipSuccess) return bail(hip_fail(e, he, "hipEventCreate"));
     if ((he = hipEventCreate(&e->ev1)) != hipSuccess) return bail(hip_fail(e, he, "hipEventCreate"));
     if (fq_pack_kernel_lds_bytes(e->p) > 160 * 1024)
-        return bail(fail(e, FQ_E_INVALID, "max_cycles too large for the LDS-privatised accumulators"));
+        return bail(fail(e, FQ_E_INVALID, "insert_size_max too large for the LDS-privatised accumulators"));
     if ((he = fq_pack_kernel_set_lds(e->p)) != hipSuccess) return bail(hip_fail(e, he, "hipFuncSetAttribute"));
     const char* force_general = std::getenv("FQ_ENGINE_GENERAL_ONLY");
     e->fast = fq_pe_fast_supported(e->p) && !(force_general && force_general[0] == '1');

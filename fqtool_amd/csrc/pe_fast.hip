@@ -261,7 +261,10 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         // ---------------- trimAndCut (src/peprocessor.cpp:292-293) ----------------
         int st = 0, n = 0;
         bool nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n);
-        const bool both = nn && __shfl_xor(nn ? 1 : 0, 32) != 0;
+        // the shuffle must run in every lane: ds_bpermute from a lane that is switched off returns
+        // whatever its register held before (e.g. the previous tile's value)
+        const int nn_o = __shfl_xor(nn ? 1 : 0, 32);
+        const bool both = nn && nn_o != 0;
         fq_read_result rr;
         rr.flags = nn ? 0 : FQ_RF_NULL;
         rr.code = 0;

@@ -23,16 +23,29 @@ namespace {
 constexpr int kRec = 17;  // LDS words per (stats, cycle) record
 
 struct Smem {
-    uint32_t* hist;         // [4][C][17]
+    uint32_t* hist;         // [4][clds][17]
     unsigned long long* c;  // small u64 counters, indexed like the global accumulator head
     unsigned long long* scal;  // [4][4] reads, length_sum, q20, q30
+    int clds;                  // cycles privatised in LDS; later cycles go to global atomics
+    unsigned long long* gcyc;  // global per-cycle block of stats 0 (+ k * stats words)
+    size_t gstride;            // u64 words between the stats blocks
 };
+
+// cycles the LDS histograms can hold next to the small counters
+__host__ __device__ inline int lds_cycles(const fq_params& p) {
+    const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
+    const int small_words = 2 * (((nsmall + 1) & ~1) + 16);
+    const int cap = (160 * 1024 / 4 - small_words) / (4 * kRec);
+    return p.max_cycles < cap ? p.max_cycles : cap;
+}
 
 __device__ __forceinline__ void lds_add64(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
 
 // Stats::statRead, reference src/stats.cpp:237-295, on a window of a row (cycle i = data[i]).
 template <typename Fetch>
-__device__ inline void stat_read(uint32_t* hist, unsigned long long* scal, int len, int skew, Fetch fetch) {
+__device__ inline void stat_read(const Smem& sm, int k, int len, int skew, Fetch fetch) {
+    uint32_t* hist = sm.hist + (size_t)k * sm.clds * kRec;
+    unsigned long long* scal = sm.scal + 4 * k;
     if (len <= 0) {
         lds_add64(&scal[0], 1ull);
         return;
@@ -48,9 +61,15 @@ __device__ inline void stat_read(uint32_t* hist, unsigned long long* scal, int l
         const int cls = b & 7;
         q20 += q > '5';
         q30 += q > '?';
-        uint32_t* rec = hist + c * kRec;
-        atomicAdd(&rec[cls], 1u);
-        atomicAdd(&rec[8 + cls], (uint32_t)(q + 128));
+        if (c < sm.clds) {
+            uint32_t* rec = hist + c * kRec;
+            atomicAdd(&rec[cls], 1u);
+            atomicAdd(&rec[8 + cls], (uint32_t)(q + 128));
+        } else {  // reads longer than the LDS histograms (merged long reads): straight to HBM
+            unsigned long long* g = sm.gcyc + k * sm.gstride + (size_t)c * FQ_ST_PER_CYCLE;
+            atomicAdd(&g[cls], 1ull);
+            atomicAdd(&g[8 + cls], (unsigned long long)(long long)(q - 33));
+        }
     }
     lds_add64(&scal[0], 1ull);
     lds_add64(&scal[1], (unsigned long long)len);
@@ -60,7 +79,8 @@ __device__ inline void stat_read(uint32_t* hist, unsigned long long* scal, int l
 
 __device__ __forceinline__ void row_stat(const Smem& sm, int k, int C, const uint8_t* s, const uint8_t* q,
                                          int len, int skew) {
-    stat_read(sm.hist + (size_t)k * C * kRec, sm.scal + 4 * k, len, skew, [&](int i, uint8_t& b, int& qq) {
+    (void)C;
+    stat_read(sm, k, len, skew, [&](int i, uint8_t& b, int& qq) {
         b = s[i];
         qq = qv(q, i);
     });
@@ -133,7 +153,10 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
     sm.c = reinterpret_cast<unsigned long long*>(lds);
     sm.scal = sm.c + ((nsmall + 1) & ~1);
     sm.hist = reinterpret_cast<uint32_t*>(sm.scal + 16);
-    const int total_words = 2 * (((nsmall + 1) & ~1) + 16) + 4 * C * kRec;
+    sm.clds = lds_cycles(p);
+    sm.gstride = acc_stats_words(C);
+    sm.gcyc = acc + acc_stats_offset(p.insert_size_max, C, 0) + FQ_ST_CYCLES;
+    const int total_words = 2 * (((nsmall + 1) & ~1) + 16) + 4 * sm.clds * kRec;
     for (int i = threadIdx.x; i < total_words; i += blockDim.x) lds[i] = 0;
     __syncthreads();
 
@@ -292,7 +315,7 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
                         if (mlen > C) {
                             atomicOr(err, 1);
                         } else {
-                            stat_read(sm.hist + (size_t)2 * C * kRec, sm.scal + 8, mlen, skew, fetch);
+                            stat_read(sm, 2, mlen, skew, fetch);
                             lds_add64(&sm.c[FQ_ACC_MERGED_PAIRS], 1ull);
                         }
                     }
@@ -346,8 +369,8 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
         unsigned long long v = sm.scal[threadIdx.x];
         if (v) atomicAdd(&acc[st_base + k * st_words + f], v);
     }
-    for (int i = threadIdx.x; i < 4 * C; i += blockDim.x) {
-        const int k = i / C, c = i - k * C;
+    for (int i = threadIdx.x; i < 4 * sm.clds; i += blockDim.x) {
+        const int k = i / sm.clds, c = i - k * sm.clds;
         const uint32_t* rec = sm.hist + (size_t)i * kRec;
         unsigned long long* dst = acc + st_base + k * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
 #pragma unroll
@@ -366,7 +389,7 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
 
 size_t fq_pack_kernel_lds_bytes(const fq_params& p) {
     const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
-    return (size_t)(2 * (((nsmall + 1) & ~1) + 16) + 4 * p.max_cycles * kRec) * sizeof(uint32_t);
+    return (size_t)(2 * (((nsmall + 1) & ~1) + 16) + 4 * lds_cycles(p) * kRec) * sizeof(uint32_t);
 }
 
 hipError_t fq_launch_pack_kernel(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,

@@ -81,9 +81,18 @@ def round16(x):
     return (x + 15) & ~15
 
 
-def run_session_with_oracle(host, orc, argv, max_n=1500):
-    """The tool's host pipeline (libfqhost session API) with the CPU oracle in the engine's place:
-    checks the host side (parsing, packing, formatting, writers, report) on CPU."""
+def oracle_process(orc):
+    def process(p, b, nres, mc):
+        res = np.zeros(nres, dtype=np.dtype(abi.RESULT_DTYPE_FIELDS))
+        acc = np.zeros(abi.acc_words(p.insert_size_max, mc), np.uint64)
+        assert orc.orc_process_batch(ctypes.byref(p), ctypes.byref(b), res.ctypes.data, acc.ctypes.data) == 0
+        return res, acc
+    return process
+
+
+def run_session(host, argv, process, max_n=1500):
+    """The tool's host pipeline (libfqhost session API) with `process(params, batch, n_results,
+    max_cycles) -> (results, accumulator)` standing in for the engine call."""
     enc = [a.encode() for a in argv]
     arr = (ctypes.c_char_p * len(enc))(*enc)
     s = ctypes.c_void_p()
@@ -110,11 +119,21 @@ def run_session_with_oracle(host, orc, argv, max_n=1500):
             mc = max(16, round16(need))
             p = abi.FqParams()
             host.fqh_session_params(s, mc, ctypes.byref(p))
-            res = np.zeros(n * (2 if paired else 1), dtype=np.dtype(abi.RESULT_DTYPE_FIELDS))
-            acc = np.zeros(abi.acc_words(p.insert_size_max, mc), np.uint64)
-            assert orc.orc_process_batch(ctypes.byref(p), ctypes.byref(b), res.ctypes.data, acc.ctypes.data) == 0
+            res, acc = process(p, b, n * (2 if paired else 1), mc)
             assert host.fqh_session_consume(s, res.ctypes.data, mc) == 0, host.fqh_session_error(s)
             host.fqh_session_add_acc(s, acc.ctypes.data, mc)
         return abi.take_string(host, host.fqh_session_finish(s))
     finally:
         host.fqh_session_close(s)
+
+
+def run_session_with_oracle(host, orc, argv, max_n=1500):
+    """Host pipeline with the CPU oracle in the engine's place: checks the host side (parsing,
+    packing, formatting, writers, report) on CPU."""
+    return run_session(host, argv, oracle_process(orc), max_n)
+
+
+def read_row(b, mate, i, length):
+    seq = ctypes.string_at((b.seq1 if mate == 0 else b.seq2) + i * b.stride, length)
+    qual = ctypes.string_at((b.qual1 if mate == 0 else b.qual2) + i * b.stride, length)
+    return seq, qual

@@ -176,3 +176,21 @@ def test_too_long_read_is_rejected(eng_lib, oracle):
         assert rc == -4
     finally:
         eng_lib.fq_engine_destroy(h)
+
+
+def test_null_mate_after_full_pairs(eng_lib, oracle, mode):
+    """Regression: a pair whose read 2 is NULL must not see read 2 as present because the lane
+    processed a full pair in its previous tile (the mate-presence shuffle once ran only in the
+    lanes whose own read survived).  The first 2 tiles of every wave have both mates good, the
+    rest have an all-N read 2 that cut_front trims to NULL."""
+    p = config("PE_all", max_cycles=512)
+    p.cut_front = 1
+    n = 32 * 4096 * 3
+    pk = synth_pack(oracle, n, True, first=777)
+    bad = slice(32 * 4096, None)
+    pk.seq2[bad, :150] = ord("N")
+    pk.qual2[bad, :150] = ord("#")
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    assert (res_o["flags"][1::2][32 * 4096:] & abi.FQ_RF_NULL).all()
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
