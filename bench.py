@@ -132,6 +132,7 @@ def main():
     import torch.distributed as dist
 
     from fqtool_amd import abi
+    from fqtool_amd.dist import reduce_accumulator, shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -150,7 +151,7 @@ def main():
     if lib.fq_engine_create(ctypes.byref(p), local, 0, 0, ctypes.byref(h)) != 0:
         raise SystemExit("fq_engine_create: " + lib.fq_engine_last_error(None).decode())
 
-    n = args.pairs
+    first, n = shard(rank, world, args.pairs)
     log(f"rank {rank}/{world}: allocating {4 * n * STRIDE / 1e9:.1f} GB of reads for {n} pairs")
     bufs = [torch.empty(n * STRIDE, dtype=torch.uint8, device=dev) for _ in range(4)]
     lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
@@ -163,7 +164,7 @@ def main():
     b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
     stream = torch.cuda.current_stream(dev)
     t0 = time.time()
-    assert lib.fq_synth_fill_device(ctypes.byref(b), SEED, rank * n, READ_LEN, ctypes.c_void_p(stream.cuda_stream)) == 0
+    assert lib.fq_synth_fill_device(ctypes.byref(b), SEED, first, READ_LEN, ctypes.c_void_p(stream.cuda_stream)) == 0
     torch.cuda.synchronize(dev)
     log(f"synthetic data generated in {time.time() - t0:.2f}s")
 
@@ -176,8 +177,7 @@ def main():
             raise RuntimeError(lib.fq_engine_last_error(h).decode())
         if ev:
             ev[1].record(stream)
-        if world > 1:
-            dist.all_reduce(acc)  # Stats/FilterResult/insert-size reduce over RCCL (xGMI)
+        reduce_accumulator(acc)  # Stats/FilterResult/insert-size sum over RCCL (xGMI) when world > 1
 
     for i in range(args.warmup):
         step()
