@@ -1,32 +1,29 @@
-// pe_fast.hip -- v2 hot path for paired-end packs on gfx950 (everything except -m merge).
+// pe_fast.hip -- hot path for paired-end packs on gfx950 (everything except -m merge).
 //
 // Mapping: one workgroup = 8 waves, one wave = a tile of 32 pairs, one LANE = one READ
 // (lanes 0-31 read 1, lanes 32-63 read 2 of the same pairs), so every per-read operation of
 // PairEndProcessor::processPairEnd (reference src/peprocessor.cpp:261-508) keeps all 64 lanes
 // busy and the two mates of a pair are lanes l and l^32 of the same wave.
 //
-// Staging: each lane streams its seq row from HBM with 16-byte loads into its own LDS column
-// (word (field*64 + lane): conflict-free for any per-lane position) and derives, in registers,
-//   * a 2-bit base code per position (A=0 C=1 T=2 G=3, N=3, i.e. (byte>>1)&3) and
-//   * an N mask (one bit per position, spaced to line up with the 2-bit codes),
-// read 1 forward, read 2 already reverse-complemented (the orientation OverlapAnalysis::analyze
-// compares, src/overlapanalysis.cpp:7-72).  Qualities stay in HBM/L2 and are re-read per pass.
-// A tile whose bases are not all in {A,C,G,T,N}, whose quality bytes are >= 128, or whose
-// reads are longer than 160 is handed to the general kernel (pe_kernel.hip) through a
-// device-side tile list, so the fast path may assume that alphabet.
+// Staging: each lane streams its seq and qual rows from HBM with 16-byte loads.  Sequence bytes
+// are reduced in registers to 2-bit base codes (A=0 C=1 T=2 G=3, N=3, i.e. (byte>>1)&3) plus a
+// spaced N mask; quality bytes are kept verbatim.  Both go to the lane's own LDS column (word
+// field*64 + lane: conflict-free for any per-lane position).  Read 1 codes are stored forward,
+// read 2 codes reverse-complemented (the orientation OverlapAnalysis::analyze compares,
+// src/overlapanalysis.cpp:7-72); qualities are forward for both.  A tile with a byte outside
+// {A,C,G,T,N}, a quality >= 128 or a read longer than 160 is handed to the general kernel
+// (pe_kernel.hip) through a device-side tile list, so everything here may assume that alphabet
+// and rebuild bases from codes.
 //
-// Overlap analysis: for every candidate offset a lane compares 16 positions at once on the
-// 2-bit codes (equal bytes => equal codes, so the code mismatch count is a lower bound of the
-// byte mismatch count and rejecting at >= max(limit,1) is exact); the first surviving offset
-// is verified exactly with codes + N masks (equal bases <=> equal code and equal N bit on this
-// alphabet) applying the reference's break/accept rule.  Read 1's lane scans phase 1
-// (offset >= 0), read 2's lane phase 2 (offset <= 0); the pair's answer is phase 1's if any.
-//
-// Statistics: Stats::statRead (src/stats.cpp:237-295) per cycle and base class into
-// workgroup-private LDS histograms of u64 cells (count << 40 | sum(q+128)); each lane walks its
-// read's dwords from a lane-dependent rotation so the wave's 64 atomics spread over cycles.
-// Post-filter stats are accumulated as "removed" (pre minus what survives) when the surviving
-// window always starts at 0, which touches only trimmed tails and failed reads.
+// Per read, in the reference's order: trimAndCut (integer windows over LDS qualities), polyG
+// (bit-parallel: the 3'-end scan only changes state at non-G bases, visited with find-last-set),
+// overlap analysis (read 1 lanes scan phase 1, read 2 lanes phase 2 through one code path: a
+// 16-position code-mismatch lower bound rejects offsets, survivors are verified exactly with
+// codes + N masks under the reference's break/accept rule), adapter trimming, polyX, maxLen,
+// passFilter (SWAR over the window's quality words), then Stats::statRead for the pre and post
+// blocks into workgroup-private LDS histograms of u64 cells (count << 40 | sum(q+128)); lanes
+// walk each 16-position chunk from a lane-dependent rotation so a wave's atomics spread over
+// cycles.
 #include <hip/hip_runtime.h>
 
 #include "device_ops.h"
@@ -39,24 +36,26 @@ namespace {
 constexpr int kWaves = 8;
 constexpr int kBlock = 64 * kWaves;
 constexpr int kMaxLen = 160;
-constexpr int kRawW = kMaxLen / 4;          // raw seq dwords per lane column
-constexpr int kCodeW = kMaxLen / 16;        // 2-bit code dwords (16 positions each)
-constexpr int kColW = kRawW + 2 * kCodeW;   // words per lane column: raw | codes | N mask
-constexpr int kCellW = 12;                  // u32 words per cycle: 6 slots x u64
-constexpr int kGroupW = 4 * kCellW + 2;     // words per 4 cycles (+2 pad spreads LDS banks)
-constexpr int kHistW = (kMaxLen / 4) * kGroupW;
+constexpr int kChunks = kMaxLen / 16;             // 16-position chunks per read
+constexpr int kFC = 0;                            // column fields (words): 2-bit codes,
+constexpr int kFN = kChunks;                      //   spaced N mask,
+constexpr int kFQ = 2 * kChunks;                  //   quality bytes
+constexpr int kColW = 2 * kChunks + kMaxLen / 4;  // words per lane column
+constexpr int kCycW = 10;                         // words per cycle: 5 base classes x u64
+constexpr int kHistW = (kMaxLen + 1) * kCycW;     // + one dummy cycle for masked-off positions
+constexpr int kDummy = kMaxLen * kCycW;
 constexpr int kSmallU64 = FQ_ACC_INSERT + 512 + 1;
 constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
 constexpr int kScalW = 2 * 16;  // [4 stats][reads, length_sum, q20, q30] u64
 constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
+constexpr int kLutW = kMaxLen / 2;  // polyG allowed-mismatch table, int16 per scan index
 constexpr int kColsW = kWaves * kColW * 64;
-constexpr int kLdsWords = kColsW + 4 * kHistW + kSmallW + kScalW + kAdW;
+constexpr int kLdsWords = kColsW + 4 * kHistW + kSmallW + kScalW + kAdW + kLutW;
 static_assert(kLdsWords * 4 <= 160 * 1024, "LDS budget");
+static_assert((kColsW & 1) == 0 && (kHistW & 1) == 0, "u64 cells must stay 8-byte aligned");
 
 constexpr unsigned long long kCount1 = 1ull << 40;
 constexpr unsigned long long kQMask = kCount1 - 1;
-
-__device__ __forceinline__ uint32_t pack4(uint32_t x) { return (x | (x >> 6) | (x >> 12) | (x >> 18)) & 0xFFu; }
 
 // reverse the order of the 16 two-bit fields of a word
 __device__ __forceinline__ uint32_t pairrev(uint32_t x) {
@@ -76,21 +75,63 @@ __device__ __forceinline__ uint32_t bytemask(int n) {
     return n >= 4 ? 0xFFFFFFFFu : n <= 0 ? 0u : ((1u << (8 * n)) - 1u);
 }
 
-struct LdsSeq {  // raw byte i of a lane column
+// 4x4 transpose of two-bit elements, row = byte: element (r, c) at bit 8r+2c moves to 8c+2r
+__device__ __forceinline__ uint32_t tr4x4(uint32_t y) {
+    uint32_t t = (y ^ (y >> 6)) & 0x00CC00CCu;
+    y ^= t ^ (t << 6);
+    t = (y ^ (y >> 12)) & 0x0000F0F0u;
+    return y ^ t ^ (t << 12);
+}
+
+// 16 consecutive two-bit positions [pos, pos+16) of field f (codes or N mask) of column c;
+// positions outside the column read as 0
+__device__ __forceinline__ uint32_t field_window(const uint32_t* col, int f, int c, int pos) {
+    const int w = pos >> 4, sh = 2 * (pos & 15);
+    const int wl = min(max(w, 0), kChunks - 1), wh = min(max(w + 1, 0), kChunks - 1);
+    const uint32_t lo = col[(f + wl) * 64 + c] & ((unsigned)w < (unsigned)kChunks ? ~0u : 0u);
+    const uint32_t hi = col[(f + wh) * 64 + c] & ((unsigned)(w + 1) < (unsigned)kChunks ? ~0u : 0u);
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+}
+
+struct Fwd {
+    uint32_t c, n;
+};
+
+// forward codes / N mask of positions [16F, 16F+16) of lane c's read of length L (read 2
+// columns are stored reverse-complemented); positions >= L are garbage for the caller to mask
+__device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool rc, int L) {
+    const int s0 = rc ? L - 16 - 16 * F : 16 * F;
+    uint32_t cw = field_window(col, kFC, c, s0);
+    uint32_t nw = field_window(col, kFN, c, s0);
+    if (rc) {
+        cw = pairrev(cw);
+        nw = pairrev(nw);
+        cw ^= 0xAAAAAAAAu & ~(nw << 1);  // complement back, N stays code 3
+    }
+    return Fwd{cw, nw};
+}
+
+struct LdsQual {  // forward quality byte i of a lane column
     const uint32_t* col;
     int c;
-    __device__ __forceinline__ uint8_t operator()(int i) const {
-        return (uint8_t)(col[(i >> 2) * 64 + c] >> ((i & 3) * 8));
+    __device__ __forceinline__ int operator()(int i) const {
+        return (int)((col[(kFQ + (i >> 2)) * 64 + c] >> ((i & 3) * 8)) & 0xFFu);
     }
 };
 
-// 16 two-bit code positions [pos, pos+16) of field `f` (codes or N mask) of column c
-__device__ __forceinline__ uint32_t code_window(const uint32_t* col, int f, int c, int pos) {
-    const int w = pos >> 4, sh = 2 * (pos & 15);
-    const uint32_t lo = w < kCodeW ? col[(f + w) * 64 + c] : 0u;
-    const uint32_t hi = w + 1 < kCodeW ? col[(f + w + 1) * 64 + c] : 0u;
-    return __builtin_amdgcn_alignbit(hi, lo, sh);
-}
+struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N)
+    const uint32_t* col;
+    int c, L;
+    bool rc;
+    __device__ __forceinline__ uint8_t operator()(int i) const {
+        const int q = rc ? L - 1 - i : i;
+        const int w = q >> 4, sh = 2 * (q & 15);
+        uint32_t code = (col[(kFC + w) * 64 + c] >> sh) & 3u;
+        const uint32_t nb = (col[(kFN + w) * 64 + c] >> sh) & 1u;
+        code ^= rc ? 2u : 0u;
+        return nb ? (uint8_t)'N' : (uint8_t)(0x47544341u >> (8 * code));  // "ACTG"
+    }
+};
 
 struct OvOut {
     bool found;
@@ -104,10 +145,10 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
     int d50 = 0, D = 0;
     const int nw = (ol + 15) >> 4;
     for (int j = 0; j < nw; ++j) {
-        const uint32_t a = code_window(col, kRawW, c1, p1 + 16 * j);
-        const uint32_t b = code_window(col, kRawW, c2, p2 + 16 * j);
-        const uint32_t wa = code_window(col, kRawW + kCodeW, c1, p1 + 16 * j);
-        const uint32_t wb = code_window(col, kRawW + kCodeW, c2, p2 + 16 * j);
+        const uint32_t a = field_window(col, kFC, c1, p1 + 16 * j);
+        const uint32_t b = field_window(col, kFC, c2, p2 + 16 * j);
+        const uint32_t wa = field_window(col, kFN, c1, p1 + 16 * j);
+        const uint32_t wb = field_window(col, kFN, c2, p2 + 16 * j);
         const uint32_t mism = (fold2(a ^ b) & ~(wa | wb)) | (wa ^ wb);
         D += __popc(mism & posmask(ol - 16 * j));
         d50 += __popc(mism & posmask(min(ol, 50) - 16 * j));
@@ -120,22 +161,28 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
 
 // Scan one phase: offsets k = k0 .. cnt-1 move a 16-position window of column `cm` starting at
 // code position mpos0 + k against the fixed 16-position word `fixed`; returns the first offset
-// whose code-level lower bound is < K (or -1).  ol(k) = min(olA - k, olB).
+// whose code-level lower bound is < K (or -1).  ol(k) = min(olA - k, olB).  With FIXED_MASK the
+// caller guarantees ol(k) >= min(olB, 16) for every scanned k (overlap_require >= 16), so the
+// mask of compared positions is the constant `pm`.
+template <bool FIXED_MASK>
 __device__ inline int ov_scan(const uint32_t* col, int cm, int mpos0, int k0, int cnt, uint32_t fixed, int olA,
-                              int olB, int K) {
+                              int olB, int K, uint32_t pm) {
     for (int k = k0; k < cnt;) {
         const int P = mpos0 + k;
         const int w = P >> 4;
-        const uint32_t lo = w < kCodeW ? col[(kRawW + w) * 64 + cm] : 0u;
-        const uint32_t hi = w + 1 < kCodeW ? col[(kRawW + w + 1) * 64 + cm] : 0u;
+        const uint32_t lo = w < kChunks ? col[(kFC + w) * 64 + cm] : 0u;
+        const uint32_t hi = w + 1 < kChunks ? col[(kFC + w + 1) * 64 + cm] : 0u;
         uint32_t bits = 0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             // window starting at absolute position 16w + r
             const uint32_t win = r == 0 ? lo : __builtin_amdgcn_alignbit(hi, lo, 2 * r);
-            const int kk = 16 * w + r - mpos0;
-            const int ol = min(olA - kk, olB);
-            const int lb = __popc(fold2(win ^ fixed) & posmask(ol));
+            uint32_t m = pm;
+            if (!FIXED_MASK) {
+                const int kk = 16 * w + r - mpos0;
+                m = posmask(min(olA - kk, olB));
+            }
+            const int lb = __popc(fold2(win ^ fixed) & m);
             bits |= (uint32_t)(lb < K) << r;
         }
         // keep offsets within [k, cnt)
@@ -149,7 +196,56 @@ __device__ inline int ov_scan(const uint32_t* col, int cm, int mpos0, int k0, in
     return -1;
 }
 
+// PolyX::trimPolyG (src/polyx.cpp:14-38) on the code columns.  The scan from the 3' end changes
+// its state only at non-G bases (a G never breaks it: the allowance never shrinks), so it visits
+// just those, with find-last-set over 16-position chunks; allowed[j] = min(maxMM, max(1,
+// (j+1)/per)) comes from an LDS table.  Returns the new window length; bases < 0: not recorded.
+__device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int st, int n,
+                                 const int16_t* allowed, int compareReq, int& bases) {
+    const int e = st + n - 1;  // last forward position of the window
+    int mism = 0, iend = n;    // iend: scan index of the break, or rlen when the scan ran through
+    for (int F = e >> 4; F >= (st >> 4) && iend == n; --F) {
+        const Fwd f = fwd_chunk(col, c, F, rc, L);
+        const uint32_t g = ~fold2(~f.c) & ~f.n & 0x55555555u;
+        uint32_t m = ~g & 0x55555555u & posmask(e - 16 * F + 1) & ~posmask(st - 16 * F);
+        while (m) {
+            const int b = 31 - __clz(m);
+            const int j = e - (16 * F + (b >> 1));
+            ++mism;
+            if (mism > allowed[j]) {
+                iend = j;
+                break;
+            }
+            m ^= 1u << b;
+        }
+    }
+    bases = -1;
+    if (iend + 1 < compareReq) return n;
+    // firstG: the lowest scanned position holding a G, i.e. the lowest G in [e-iend+1, e]
+    // (the reference's default is rlen-1)
+    int firstG = n - 1;
+    const int lo = e - iend + 1;
+    for (int F = lo >> 4; F <= (e >> 4); ++F) {
+        const Fwd f = fwd_chunk(col, c, F, rc, L);
+        uint32_t g = ~fold2(~f.c) & ~f.n & 0x55555555u;
+        g &= posmask(e - 16 * F + 1) & ~posmask(lo - 16 * F);
+        if (g) {
+            firstG = 16 * F + ((__ffs(g) - 1) >> 1) - st;
+            break;
+        }
+    }
+    bases = n - firstG;
+    return firstG;  // n >= 1 here, so 0 <= firstG <= n-1 (Read::resize keeps it)
+}
+
 __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
+
+__device__ __forceinline__ void hadd(uint32_t* base, int word, unsigned long long v) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(base + word), v);
+}
+
+// histogram slot (A C T G N) -> Stats base class (byte & 7), src/stats.cpp:249
+__device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) & 0xF; }
 
 __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
@@ -157,33 +253,41 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* col = lds + wave * kColW * 64;
-    uint32_t* hist = lds + kColsW;  // [pre1, pre2, aux1, aux2] x kHistW
+    uint32_t* hist = lds + kColsW;  // [pre1, pre2, post1, post2] x kHistW
     unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + 4 * kHistW);
     unsigned long long* scal = small + kSmallW / 2;
     uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16);
+    int16_t* allowed = reinterpret_cast<int16_t*>(adp + 2 * FQ_MAX_ADAPTER);
     for (int i = threadIdx.x; i < 4 * kHistW + kSmallW + kScalW; i += kBlock) hist[i] = 0;
     for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kBlock)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
+    for (int j = threadIdx.x; j < kMaxLen; j += kBlock) {
+        const int per = max(p.polyg_one_mismatch_per, 1);
+        allowed[j] = (int16_t)min(p.polyg_max_mismatch, max(1, (j + 1) / per));
+    }
     __syncthreads();
 
     const int mate = lane >> 5, pl = lane & 31;
     const int mlane = lane ^ 32;
+    const bool rc = mate == 1;
     // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
     // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics
     const int abl = p.reserved[0];
-    const bool removed_mode = p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front;
     const int ntiles = (b.n + 31) >> 5;
-    const int nchunks = min(kCodeW, b.stride >> 4);
+    const int nchunks = min(kChunks, b.stride >> 4);
     const int limit = p.overlap_diff_limit;
     const int K = max(limit, 1);
+    const int req = p.overlap_require;
     const int front = mate ? p.trim_front2 : p.trim_front1;
     const int tail = mate ? p.trim_tail2 : p.trim_tail1;
     const uint8_t* my_ad = adp + (mate ? FQ_MAX_ADAPTER : 0);
     const int my_alen = mate ? p.adapter2_len : p.adapter1_len;
     const int my_maxlen = mate ? p.max_len2 : p.max_len1;
+    const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
     uint32_t* my_pre = hist + mate * kHistW;
-    uint32_t* my_aux = hist + (2 + mate) * kHistW;
-    unsigned long long s_pre[4] = {0, 0, 0, 0}, s_aux[4] = {0, 0, 0, 0};
+    uint32_t* my_post = hist + (2 + mate) * kHistW;
+    const int r = lane & 15;  // stats rotation within a chunk
+    unsigned long long s_pre[4] = {0, 0, 0, 0}, s_post[4] = {0, 0, 0, 0};
 
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
         const int idx = t * 32 + pl;
@@ -194,30 +298,41 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         const int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
 
         // ---------------- staging ----------------
-        bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4);
-        uint32_t exo = 0, qhi = 0;
-        uint32_t fc[kCodeW], fw[kCodeW];
+        const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4);
+        uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0;
+        uint32_t fc[kChunks], fw[kChunks];
+        // Loads are unconditional (every row of the batch is readable up to its stride) so the
+        // whole chunk sequence is one basic block and the loads can be issued early; only the
+        // chunks that some lane's read does not fill (wave-uniform test) pay for byte masks.
 #pragma unroll
-        for (int k = 0; k < kCodeW; ++k) {
+        for (int k = 0; k < kChunks; ++k) {
             fc[k] = 0;
             fw[k] = 0;
-            if (k < nchunks && valid && !odd) {
+            if (k < nchunks) {
                 const uint4 s4 = *reinterpret_cast<const uint4*>(S + 16 * k);
                 const uint4 q4 = *reinterpret_cast<const uint4*>(Q + 16 * k);
                 const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
                 const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+                uint32_t cc = 0, nn4 = 0;
+                const bool full = __all(L >= 16 * k + 16);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    col[(4 * k + j) * 64 + lane] = sw[j];
-                    const uint32_t bm = bytemask(L - (16 * k + 4 * j));
+                    col[(kFQ + 4 * k + j) * 64 + lane] = qw[j];
+                    const uint32_t bm = full ? 0xFFFFFFFFu : bytemask(L - (16 * k + 4 * j));
                     const uint32_t kk = (sw[j] >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
                     const uint32_t canon = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, kk);
                     exo |= (canon ^ sw[j]) & bm;
-                    qhi |= qw[j] & bm;
-                    fc[k] |= pack4(kk & 0x03030303u) << (8 * j);
-                    fw[k] |= pack4((kk >> 2) & 0x01010101u) << (8 * j);
+                    const uint32_t qm = qw[j] & bm;
+                    qhi |= qm;
+                    const uint32_t q7 = qm & 0x7F7F7F7Fu;
+                    q20 += __popc(((q7 + 0x4A4A4A4Au) & 0x80808080u) & bm);  // q > '5'
+                    q30 += __popc(((q7 + 0x40404040u) & 0x80808080u) & bm);  // q > '?'
+                    cc |= (kk & 0x03030303u) << (2 * j);
+                    nn4 |= ((kk >> 2) & 0x01010101u) << (2 * j);
                 }
+                fc[k] = tr4x4(cc);
+                fw[k] = tr4x4(nn4);
             }
         }
         const bool bad = odd || exo != 0 || (qhi & 0x80808080u) != 0;
@@ -227,36 +342,36 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         }
         if (mate == 0) {
 #pragma unroll
-            for (int k = 0; k < kCodeW; ++k) {
-                col[(kRawW + k) * 64 + lane] = fc[k];
-                col[(kRawW + kCodeW + k) * 64 + lane] = fw[k];
+            for (int k = 0; k < kChunks; ++k) {
+                col[(kFC + k) * 64 + lane] = fc[k];
+                col[(kFN + k) * 64 + lane] = fw[k];
             }
         } else {
             // reverse-complement read 2's codes: rc[j] = comp(code[L-1-j]); N stays N (3)
 #pragma unroll
-            for (int m = 0; m < kCodeW; ++m) {
-                col[(kRawW + m) * 64 + lane] = pairrev(fc[kCodeW - 1 - m]);
-                col[(kRawW + kCodeW + m) * 64 + lane] = pairrev(fw[kCodeW - 1 - m]);
+            for (int m = 0; m < kChunks; ++m) {
+                col[(kFC + m) * 64 + lane] = pairrev(fc[kChunks - 1 - m]);
+                col[(kFN + m) * 64 + lane] = pairrev(fw[kChunks - 1 - m]);
             }
             const int sh = kMaxLen - L, q = sh >> 4, r2 = 2 * (sh & 15);
-            for (int m = 0; m < kCodeW; ++m) {
+            for (int m = 0; m < kChunks; ++m) {
                 const int a = m + q;
-                const uint32_t clo = a < kCodeW ? col[(kRawW + a) * 64 + lane] : 0u;
-                const uint32_t chi = a + 1 < kCodeW ? col[(kRawW + a + 1) * 64 + lane] : 0u;
-                const uint32_t wlo = a < kCodeW ? col[(kRawW + kCodeW + a) * 64 + lane] : 0u;
-                const uint32_t whi = a + 1 < kCodeW ? col[(kRawW + kCodeW + a + 1) * 64 + lane] : 0u;
+                const uint32_t clo = a < kChunks ? col[(kFC + a) * 64 + lane] : 0u;
+                const uint32_t chi = a + 1 < kChunks ? col[(kFC + a + 1) * 64 + lane] : 0u;
+                const uint32_t wlo = a < kChunks ? col[(kFN + a) * 64 + lane] : 0u;
+                const uint32_t whi = a + 1 < kChunks ? col[(kFN + a + 1) * 64 + lane] : 0u;
                 const uint32_t w = __builtin_amdgcn_alignbit(whi, wlo, r2);
                 const uint32_t c = __builtin_amdgcn_alignbit(chi, clo, r2) ^ (0xAAAAAAAAu & ~(w << 1));
-                col[(kRawW + m) * 64 + lane] = c;
-                col[(kRawW + kCodeW + m) * 64 + lane] = w;
+                col[(kFC + m) * 64 + lane] = c;
+                col[(kFN + m) * 64 + lane] = w;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        const LdsSeq seq{col, lane};
-        const PtrQual qual{Q};
+        const CodeSeq seq{col, lane, L, rc};
+        const LdsQual qual{col, lane};
 
         // ---------------- trimAndCut (src/peprocessor.cpp:292-293) ----------------
         int st = 0, n = 0;
@@ -273,7 +388,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         // ---------------- polyG (src/peprocessor.cpp:295-299) ----------------
         if (both && p.polyg_enabled && !(abl & 8)) {
             int bases;
-            n = trim_polyg_t(at(seq, st), n, p.polyg_compare_req, p.polyg_max_mismatch, p.polyg_one_mismatch_per, bases);
+            n = polyg_bits(col, lane, rc, L, st, n, allowed, p.polyg_compare_req, bases);
             if (bases >= 0) {
                 sadd(&small[FQ_ACC_POLYX_READS + 3], 1ull);
                 sadd(&small[FQ_ACC_POLYX_BASES + 3], (unsigned long long)(long long)bases);
@@ -287,36 +402,25 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
             const int st2 = mate ? st : st_o, n2 = mate ? n : n_o, L2 = mate ? L : L_o;
             const int c1 = mate ? mlane : lane, c2 = mate ? lane : mlane;
             const int off2 = L2 - st2 - n2;  // rc2 of the trimmed read starts here in rc coordinates
-            const int req = p.overlap_require;
+            // read 1 lanes: phase 1 (offset o >= 0: r1 window moves, rc2 fixed);
+            // read 2 lanes: phase 2 (offset -m <= 0: rc2 window moves, r1 fixed)
+            const int cm = mate ? c2 : c1, mpos = mate ? off2 : st1;
+            const int olA = mate ? n2 : n1, olB = mate ? n1 : n2;
+            const uint32_t fixed = field_window(col, kFC, mate ? c1 : c2, mate ? st1 : off2);
+            const int cnt = max(0, olA - req);
+            const uint32_t pm = posmask(olB);
             OvOut mine{false, 0, 0, 0};
-            if (mate == 0) {  // phase 1: offset o >= 0, r1 window moves, rc2 fixed
-                const int cnt = max(0, n1 - req);
-                const uint32_t fixed = code_window(col, kRawW, c2, off2);
-                for (int k0 = 0;;) {
-                    const int o = ov_scan(col, c1, st1, k0, cnt, fixed, n1, n2, K);
-                    if (o < 0) break;
-                    const int ol = min(n1 - o, n2);
-                    int diff;
-                    if (ov_exact(col, c1, st1 + o, c2, off2, ol, limit, K, diff)) {
-                        mine = OvOut{true, o, ol, diff};
-                        break;
-                    }
-                    k0 = o + 1;
+            for (int k0 = 0;;) {
+                const int o = req >= 16 ? ov_scan<true>(col, cm, mpos, k0, cnt, fixed, olA, olB, K, pm)
+                                        : ov_scan<false>(col, cm, mpos, k0, cnt, fixed, olA, olB, K, pm);
+                if (o < 0) break;
+                const int ol = min(olA - o, olB);
+                int diff;
+                if (ov_exact(col, c1, mate ? st1 : st1 + o, c2, mate ? off2 + o : off2, ol, limit, K, diff)) {
+                    mine = OvOut{true, mate ? -o : o, ol, diff};
+                    break;
                 }
-            } else {  // phase 2: offset -m <= 0, rc2 window moves, r1 fixed
-                const int cnt = max(0, n2 - req);
-                const uint32_t fixed = code_window(col, kRawW, c1, st1);
-                for (int k0 = 0;;) {
-                    const int m = ov_scan(col, c2, off2, k0, cnt, fixed, n2, n1, K);
-                    if (m < 0) break;
-                    const int ol = min(n1, n2 - m);
-                    int diff;
-                    if (ov_exact(col, c1, st1, c2, off2 + m, ol, limit, K, diff)) {
-                        mine = OvOut{true, -m, ol, diff};
-                        break;
-                    }
-                    k0 = m + 1;
-                }
+                k0 = o + 1;
             }
             const int f_o = __shfl_xor(mine.found ? 1 : 0, 32);
             const int off_o = __shfl_xor(mine.off, 32), ol_o = __shfl_xor(mine.ol, 32), d_o = __shfl_xor(mine.diff, 32);
@@ -379,22 +483,23 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         }
         if (both && my_maxlen > 0 && my_maxlen < n) n = my_maxlen;
 
-        // ---------------- passFilter (pass A, src/filter.cpp:3-52) ----------------
+        // ---------------- passFilter (src/filter.cpp:3-52) ----------------
         int code = FQ_FAIL_LENGTH;
+        uint32_t w20 = 0, w30 = 0;  // Q20/Q30 of the window, for the post stats
         if (nn && n > 0) {
             int low = 0, tq = 0, nb = 0;
-            if ((p.qual_filter_enabled || p.length_filter_enabled) && !(abl & 2)) {
-                const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
+            if (!(abl & 2)) {
                 const int end = st + n;
-                for (int c = st >> 4; c < ((end + 15) >> 4); ++c) {
-                    const uint4 q4 = *reinterpret_cast<const uint4*>(Q + 16 * c);
-                    const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+                for (int F = st >> 4; F < ((end + 15) >> 4); ++F) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const int b0 = 16 * c + 4 * j;
+                        const int b0 = 16 * F + 4 * j;
                         const uint32_t bm = bytemask(end - b0) & ~bytemask(st - b0);
-                        const uint32_t w = qw[j] & bm;
-                        low += __popc(~((w & 0x7F7F7F7Fu) + limq) & 0x80808080u & bm);
+                        const uint32_t w = col[(kFQ + 4 * F + j) * 64 + lane] & bm;
+                        const uint32_t w7 = w & 0x7F7F7F7Fu;
+                        low += __popc(~(w7 + limq) & 0x80808080u & bm);
+                        w20 += __popc(((w7 + 0x4A4A4A4Au) & 0x80808080u) & bm);
+                        w30 += __popc(((w7 + 0x40404040u) & 0x80808080u) & bm);
                         tq = (int)__builtin_amdgcn_sad_u8(w, 0u, (uint32_t)tq);
                     }
                 }
@@ -402,7 +507,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
                 // N count from the N mask (read 2's column is reverse-complemented)
                 const int lo = mate ? L - st - n : st;
                 for (int c = lo >> 4; c < ((lo + n + 15) >> 4); ++c) {
-                    const uint32_t w = col[(kRawW + kCodeW + c) * 64 + lane];
+                    const uint32_t w = col[(kFN + c) * 64 + lane];
                     nb += __popc(w & posmask(lo + n - 16 * c) & ~posmask(lo - 16 * c));
                 }
             }
@@ -416,39 +521,34 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         const bool pair_pass = both && code == FQ_PASS_FILTER && code_o == FQ_PASS_FILTER;
         if (mate == 0 && valid) sadd(&small[FQ_ACC_FILTER + max(code, code_o)], 2ull);  // addFilterResult: +2
 
-        // ---------------- Stats (pass B): pre, and removed/post ----------------
+        // ---------------- Stats::statRead, pre and post (src/peprocessor.cpp:276-277,400-401) ----
         if (valid && !(abl & 4)) {
-            const int nd = (L + 3) >> 2;
-            const int rot = nd ? lane % nd : 0;
-            uint32_t q20 = 0, q30 = 0, a20 = 0, a30 = 0;
-            for (int it = 0; it < nd; ++it) {
-                int d = it + rot;
-                if (d >= nd) d -= nd;
-                const uint32_t sw = col[d * 64 + lane];
-                const uint32_t qw = *reinterpret_cast<const uint32_t*>(Q + 4 * d);
-                const uint32_t vm = bytemask(L - 4 * d);
-                const uint32_t t20 = ((qw & 0x7F7F7F7Fu) + 0x4A4A4A4Au) & 0x80808080u;  // byte > '5'
-                const uint32_t t30 = ((qw & 0x7F7F7F7Fu) + 0x40404040u) & 0x80808080u;  // byte > '?'
-                q20 += __popc(t20 & vm);
-                q30 += __popc(t30 & vm);
-                uint32_t am;  // bytes that go to the aux histogram
-                if (removed_mode) am = pair_pass ? (vm & ~bytemask(n - 4 * d)) : vm;
-                else am = pair_pass ? (bytemask(st + n - 4 * d) & ~bytemask(st - 4 * d)) : 0u;
-                a20 += __popc(t20 & am);
-                a30 += __popc(t30 & am);
+            const int wlen = pair_pass ? n : 0;  // post window [st, st + wlen)
+            const int nchl = (L + 15) >> 4;
+            const int dsel = r >> 2;
+            for (int F = 0; F < nchl; ++F) {
+                const Fwd f = fwd_chunk(col, lane, F, rc, L);
+                const uint32_t q0 = col[(kFQ + 4 * F) * 64 + lane], q1 = col[(kFQ + 4 * F + 1) * 64 + lane];
+                const uint32_t q2 = col[(kFQ + 4 * F + 2) * 64 + lane], q3 = col[(kFQ + 4 * F + 3) * 64 + lane];
+                // rotate the chunk by r positions: position t of the rotated view is 16F + (t+r)%16
+                const uint32_t cr = __builtin_amdgcn_alignbit(f.c, f.c, 2 * r);
+                const uint32_t nr = __builtin_amdgcn_alignbit(f.n, f.n, 2 * r);
+                const uint32_t t0 = (dsel & 1) ? q1 : q0, t1 = (dsel & 1) ? q2 : q1;
+                const uint32_t t2 = (dsel & 1) ? q3 : q2, t3 = (dsel & 1) ? q0 : q3;
+                const uint32_t a0 = (dsel & 2) ? t2 : t0, a1 = (dsel & 2) ? t3 : t1;
+                const uint32_t a2 = (dsel & 2) ? t0 : t2, a3 = (dsel & 2) ? t1 : t3;
+                const uint32_t qr[4] = {__builtin_amdgcn_alignbyte(a1, a0, r & 3), __builtin_amdgcn_alignbyte(a2, a1, r & 3),
+                                        __builtin_amdgcn_alignbyte(a3, a2, r & 3), __builtin_amdgcn_alignbyte(a0, a3, r & 3)};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (((vm >> (8 * j)) & 1u) && !(abl & 16)) {
-                        const uint32_t cls = (sw >> (8 * j)) & 7u;
-                        const uint32_t slot = (cls * 3u) & 7u;
-                        const unsigned long long v = kCount1 | (unsigned long long)(((qw >> (8 * j)) & 0xFFu) ^ 0x80u);
-                        const int cell = d * kGroupW + j * kCellW + 2 * (int)slot;
-                        atomicAdd(reinterpret_cast<unsigned long long*>(my_pre + cell), v);
-                        if ((am >> (8 * j)) & 1u) {
-                            const int c = removed_mode ? 4 * d + j : 4 * d + j - st;
-                            const int acell = (c >> 2) * kGroupW + (c & 3) * kCellW + 2 * (int)slot;
-                            atomicAdd(reinterpret_cast<unsigned long long*>(my_aux + acell), v);
-                        }
+                for (int tt = 0; tt < 16; ++tt) {
+                    const int pos = 16 * F + ((tt + r) & 15);
+                    const uint32_t qv = (qr[tt >> 2] >> (8 * (tt & 3))) & 0xFFu;
+                    const int slot = (int)(((cr >> (2 * tt)) & 3u) + ((nr >> (2 * tt)) & 1u));
+                    const unsigned long long v = kCount1 | (unsigned long long)(qv | 0x80u);
+                    const int a = pos * kCycW + 2 * slot;
+                    if (!(abl & 16)) {
+                        hadd(my_pre, pos < L ? a : kDummy, v);
+                        hadd(my_post, (unsigned)(pos - st) < (unsigned)wlen ? a - st * kCycW : kDummy, v);
                     }
                 }
             }
@@ -456,18 +556,14 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
             s_pre[1] += (unsigned long long)L;
             s_pre[2] += q20;
             s_pre[3] += q30;
-            if (removed_mode) {
-                s_aux[0] += pair_pass ? 0 : 1;
-                s_aux[1] += (unsigned long long)(pair_pass ? L - n : L);
-            } else {
-                s_aux[0] += pair_pass ? 1 : 0;
-                s_aux[1] += (unsigned long long)(pair_pass ? n : 0);
+            if (pair_pass) {
+                s_post[0] += 1;
+                s_post[1] += (unsigned long long)n;
+                s_post[2] += w20;
+                s_post[3] += w30;
             }
-            s_aux[2] += a20;
-            s_aux[3] += a30;
         }
         if (valid) {
-
             rr.start = nn ? (uint16_t)st : 0;
             rr.len = nn ? (uint16_t)n : 0;
             rr.code = (uint8_t)code;
@@ -479,7 +575,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
         if (s_pre[f]) sadd(&scal[4 * mate + f], s_pre[f]);
-        if (s_aux[f]) sadd(&scal[4 * (2 + mate) + f], s_aux[f]);
+        if (s_post[f]) sadd(&scal[4 * (2 + mate) + f], s_post[f]);
     }
     __syncthreads();
 
@@ -491,29 +587,19 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
     const size_t st_words = acc_stats_words(p.max_cycles);
     if (threadIdx.x < 16) {
         const int k = threadIdx.x >> 2, f = threadIdx.x & 3;
-        unsigned long long v = scal[threadIdx.x];
-        if (k >= 2 && removed_mode) v = scal[threadIdx.x - 8] - v;  // post = pre - removed
+        const unsigned long long v = scal[threadIdx.x];
         if (v) atomicAdd(&acc[st_base + k * st_words + f], v);
     }
     const int ncyc = min(kMaxLen, p.max_cycles);
-    for (int i = threadIdx.x; i < 4 * ncyc * 6; i += kBlock) {
-        const int k = i / (ncyc * 6);
-        const int rem = i - k * ncyc * 6;
-        const int c = rem / 6, slot = rem - c * 6;
-        if (slot == 0) continue;
-        const int cell = (c >> 2) * kGroupW + (c & 3) * kCellW + 2 * slot;
-        const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hist + k * kHistW + cell);
-        long long cnt = (long long)(v >> 40);
-        long long qs = (long long)(v & kQMask) - 161ll * cnt;
-        if (k >= 2 && removed_mode) {
-            const unsigned long long pv = *reinterpret_cast<const unsigned long long*>(hist + (k - 2) * kHistW + cell);
-            const long long pc = (long long)(pv >> 40);
-            const long long pq = (long long)(pv & kQMask) - 161ll * pc;
-            cnt = pc - cnt;
-            qs = pq - qs;
-        }
-        if (cnt == 0 && qs == 0) continue;
-        const int cls = (3 * slot) & 7;
+    for (int i = threadIdx.x; i < 4 * ncyc * 5; i += kBlock) {
+        const int k = i / (ncyc * 5);
+        const int rem = i - k * ncyc * 5;
+        const int c = rem / 5, slot = rem - c * 5;
+        const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hist + k * kHistW + c * kCycW + 2 * slot);
+        const long long cnt = (long long)(v >> 40);
+        const long long qs = (long long)(v & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
+        if (cnt == 0) continue;
+        const int cls = slot_class(slot);
         unsigned long long* dst = acc + st_base + k * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
         atomicAdd(&dst[cls], (unsigned long long)cnt);
         atomicAdd(&dst[8 + cls], (unsigned long long)qs);
