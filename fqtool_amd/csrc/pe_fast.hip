@@ -39,19 +39,23 @@ constexpr int kMaxLen = 160;
 constexpr int kChunks = kMaxLen / 16;             // 16-position chunks per read
 constexpr int kFC = 0;                            // column fields (words): 2-bit codes,
 constexpr int kFN = kChunks;                      //   spaced N mask,
-constexpr int kFQ = 2 * kChunks;                  //   quality bytes
-constexpr int kColW = 2 * kChunks + kMaxLen / 4;  // words per lane column
-constexpr int kCycW = 10;                         // words per cycle: 5 base classes x u64
-constexpr int kHistW = (kMaxLen + 1) * kCycW;     // + one dummy cycle for masked-off positions
-constexpr int kDummy = kMaxLen * kCycW;
+constexpr int kWaveW = 2 * kChunks * 64;          // code + N columns of a wave
+constexpr int kBlocksPerCU = 2;                   // 16 waves per CU: LDS and VGPRs sized for it
+// Stats histograms: u64 cells [cycle / 16][slot][cycle % 16], slots A C T G N + one dummy slot
+// that absorbs masked-off positions.  A cell's LDS bank pair depends only on cycle % 16, so the
+// 16 lanes of an atomic's lane group (distinct cycle % 16 by the per-lane rotation) never
+// collide, whatever their base classes.
+constexpr int kSlots = 6;
+constexpr int kDummySlot = 5;
+constexpr int kHistW = kChunks * kSlots * 32;
+__host__ __device__ constexpr int cell(int c, int slot) { return ((c >> 4) * kSlots + slot) * 32 + 2 * (c & 15); }
 constexpr int kSmallU64 = FQ_ACC_INSERT + 512 + 1;
 constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
 constexpr int kScalW = 2 * 16;  // [4 stats][reads, length_sum, q20, q30] u64
 constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
-constexpr int kLutW = kMaxLen / 2;  // polyG allowed-mismatch table, int16 per scan index
-constexpr int kColsW = kWaves * kColW * 64;
-constexpr int kLdsWords = kColsW + 4 * kHistW + kSmallW + kScalW + kAdW + kLutW;
-static_assert(kLdsWords * 4 <= 160 * 1024, "LDS budget");
+constexpr int kColsW = kWaves * kWaveW;
+constexpr int kLdsWords = kColsW + 4 * kHistW + kSmallW + kScalW + kAdW;
+static_assert(kLdsWords * 4 * kBlocksPerCU <= 160 * 1024, "LDS budget");
 static_assert((kColsW & 1) == 0 && (kHistW & 1) == 0, "u64 cells must stay 8-byte aligned");
 
 constexpr unsigned long long kCount1 = 1ull << 40;
@@ -111,13 +115,6 @@ __device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool
     return Fwd{cw, nw};
 }
 
-struct LdsQual {  // forward quality byte i of a lane column
-    const uint32_t* col;
-    int c;
-    __device__ __forceinline__ int operator()(int i) const {
-        return (int)((col[(kFQ + (i >> 2)) * 64 + c] >> ((i & 3) * 8)) & 0xFFu);
-    }
-};
 
 struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N)
     const uint32_t* col;
@@ -167,11 +164,13 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
 template <bool FIXED_MASK>
 __device__ inline int ov_scan(const uint32_t* col, int cm, int mpos0, int k0, int cnt, uint32_t fixed, int olA,
                               int olB, int K, uint32_t pm) {
+    int w = (mpos0 + k0) >> 4;
+    uint32_t lo = w < kChunks ? col[(kFC + min(w, kChunks - 1)) * 64 + cm] : 0u;
+    uint32_t hi = w + 1 < kChunks ? col[(kFC + min(w + 1, kChunks - 1)) * 64 + cm] : 0u;
     for (int k = k0; k < cnt;) {
         const int P = mpos0 + k;
-        const int w = P >> 4;
-        const uint32_t lo = w < kChunks ? col[(kFC + w) * 64 + cm] : 0u;
-        const uint32_t hi = w + 1 < kChunks ? col[(kFC + w + 1) * 64 + cm] : 0u;
+        // the next window's high word is fetched while this one is scanned
+        const uint32_t nx = w + 2 < kChunks ? col[(kFC + min(w + 2, kChunks - 1)) * 64 + cm] : 0u;
         uint32_t bits = 0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -192,27 +191,38 @@ __device__ inline int ov_scan(const uint32_t* col, int cm, int mpos0, int k0, in
         if (last < 15) bits &= (last < 0) ? 0u : ((2u << last) - 1u);
         if (bits) return 16 * w + (__ffs(bits) - 1) - mpos0;
         k = 16 * (w + 1) - mpos0;
+        ++w;
+        lo = hi;
+        hi = nx;
     }
     return -1;
 }
 
+__device__ __forceinline__ uint32_t gmask(const Fwd& f) { return ~fold2(~f.c) & ~f.n & 0x55555555u; }
+
 // PolyX::trimPolyG (src/polyx.cpp:14-38) on the code columns.  The scan from the 3' end changes
-// its state only at non-G bases (a G never breaks it: the allowance never shrinks), so it visits
-// just those, with find-last-set over 16-position chunks; allowed[j] = min(maxMM, max(1,
-// (j+1)/per)) comes from an LDS table.  Returns the new window length; bases < 0: not recorded.
-__device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int st, int n,
-                                 const int16_t* allowed, int compareReq, int& bases) {
+// its state only at non-G bases (with maxMM >= 0 the allowance never shrinks, so a G never
+// breaks it), so it visits just those, with find-last-set over 16-position chunks.
+// allowed(j) = min(maxMM, max(1, (j+1)/per)); (j+1)/per = ((j+1)*inv) >> 16 with
+// inv = ceil(65536/per) is exact for j+1 <= 161 and per <= 256 (inv = 0 for per > 256, where the
+// quotient is 0 anyway).  The two chunks at the 3' end are fetched up front; they hold the whole
+// scan for almost every read.  Returns the new window length; bases < 0: not recorded.
+__device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int st, int n, int maxMM, int inv,
+                                 int compareReq, int& bases) {
     const int e = st + n - 1;  // last forward position of the window
-    int mism = 0, iend = n;    // iend: scan index of the break, or rlen when the scan ran through
-    for (int F = e >> 4; F >= (st >> 4) && iend == n; --F) {
-        const Fwd f = fwd_chunk(col, c, F, rc, L);
-        const uint32_t g = ~fold2(~f.c) & ~f.n & 0x55555555u;
+    const int Fe = e >> 4, Fs = st >> 4;
+    const uint32_t g0 = gmask(fwd_chunk(col, c, Fe, rc, L));
+    const uint32_t g1 = gmask(fwd_chunk(col, c, Fe - 1, rc, L));
+    int mism = 0, iend = n;  // iend: scan index of the break, or rlen when the scan ran through
+    if (maxMM < 0) iend = 0;  // mismatch 0 > allowed at the very first base
+    for (int F = Fe; F >= Fs && iend == n; --F) {
+        const uint32_t g = F == Fe ? g0 : F == Fe - 1 ? g1 : gmask(fwd_chunk(col, c, F, rc, L));
         uint32_t m = ~g & 0x55555555u & posmask(e - 16 * F + 1) & ~posmask(st - 16 * F);
         while (m) {
             const int b = 31 - __clz(m);
             const int j = e - (16 * F + (b >> 1));
             ++mism;
-            if (mism > allowed[j]) {
+            if (mism > min(maxMM, max(1, ((j + 1) * inv) >> 16))) {
                 iend = j;
                 break;
             }
@@ -225,9 +235,8 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int
     // (the reference's default is rlen-1)
     int firstG = n - 1;
     const int lo = e - iend + 1;
-    for (int F = lo >> 4; F <= (e >> 4); ++F) {
-        const Fwd f = fwd_chunk(col, c, F, rc, L);
-        uint32_t g = ~fold2(~f.c) & ~f.n & 0x55555555u;
+    for (int F = lo >> 4; F <= Fe; ++F) {
+        uint32_t g = F == Fe ? g0 : F == Fe - 1 ? g1 : gmask(fwd_chunk(col, c, F, rc, L));
         g &= posmask(e - 16 * F + 1) & ~posmask(lo - 16 * F);
         if (g) {
             firstG = 16 * F + ((__ffs(g) - 1) >> 1) - st;
@@ -240,6 +249,12 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int
 
 __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
 
+// Profiling aid: per-phase wave cycles (s_memtime deltas summed over waves), compiled in with
+// -DFQ_PHASE_STAMPS (make STAMPS=1), collected when fq_params.reserved[1] != 0 and read back with
+// fq_debug_phase_cycles().
+constexpr int kPhases = 8;  // staging, trim, polyG, overlap, polyX/maxlen, filter, stats, store
+__device__ unsigned long long g_phase_cycles[kPhases];
+
 __device__ __forceinline__ void hadd(uint32_t* base, int word, unsigned long long v) {
     atomicAdd(reinterpret_cast<unsigned long long*>(base + word), v);
 }
@@ -247,24 +262,23 @@ __device__ __forceinline__ void hadd(uint32_t* base, int word, unsigned long lon
 // histogram slot (A C T G N) -> Stats base class (byte & 7), src/stats.cpp:249
 __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) & 0xF; }
 
-__global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
+// LEAN: the option set of the headline workloads (no trimming/cutting windows, polyX, adapter
+// sequences, maxLen or low-complexity filter), instantiated separately so the hot loop carries
+// neither their code nor their parameters.
+template <bool LEAN>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 * kBlocksPerCU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t* col = lds + wave * kColW * 64;
+    uint32_t* col = lds + wave * kWaveW;  // code / N columns: word field*64 + lane
     uint32_t* hist = lds + kColsW;  // [pre1, pre2, post1, post2] x kHistW
     unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + 4 * kHistW);
     unsigned long long* scal = small + kSmallW / 2;
     uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16);
-    int16_t* allowed = reinterpret_cast<int16_t*>(adp + 2 * FQ_MAX_ADAPTER);
     for (int i = threadIdx.x; i < 4 * kHistW + kSmallW + kScalW; i += kBlock) hist[i] = 0;
     for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kBlock)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
-    for (int j = threadIdx.x; j < kMaxLen; j += kBlock) {
-        const int per = max(p.polyg_one_mismatch_per, 1);
-        allowed[j] = (int16_t)min(p.polyg_max_mismatch, max(1, (j + 1) / per));
-    }
     __syncthreads();
 
     const int mate = lane >> 5, pl = lane & 31;
@@ -284,30 +298,43 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
     const int my_alen = mate ? p.adapter2_len : p.adapter1_len;
     const int my_maxlen = mate ? p.max_len2 : p.max_len1;
     const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
+    const int g_per = max(p.polyg_one_mismatch_per, 1);
+    const int g_inv = g_per > 256 ? 0 : (65536 + g_per - 1) / g_per;
     uint32_t* my_pre = hist + mate * kHistW;
     uint32_t* my_post = hist + (2 + mate) * kHistW;
     const int r = lane & 15;  // stats rotation within a chunk
-    unsigned long long s_pre[4] = {0, 0, 0, 0}, s_post[4] = {0, 0, 0, 0};
+    // per-lane stats scalars: a lane sees at most a few hundred reads of <= 160 bases, so u32 holds them
+    uint32_t s_pre[4] = {0, 0, 0, 0}, s_post[4] = {0, 0, 0, 0};
+#ifdef FQ_PHASE_STAMPS
+    const bool stamps = p.reserved[1] != 0;
+    unsigned long long ph[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t_last = stamps ? clock64() : 0;
+#define FQ_STAMP(i)                                \
+    if (stamps) {                                  \
+        const unsigned long long now_ = clock64(); \
+        ph[i] += now_ - t_last;                    \
+        t_last = now_;                             \
+    }
+#else
+#define FQ_STAMP(i)
+#endif
 
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
         const int idx = t * 32 + pl;
         const bool valid = idx < b.n;
-        const size_t roff = (size_t)(valid ? idx : 0) * b.stride;
-        const uint8_t* S = (mate ? b.seq2 : b.seq1) + roff;
-        const uint8_t* Q = (mate ? b.qual2 : b.qual1) + roff;
         const int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
 
         // ---------------- staging ----------------
+        const size_t roff = (size_t)(valid ? idx : 0) * b.stride;
+        const uint8_t* S = (mate ? b.seq2 : b.seq1) + roff;
+        const uint8_t* Q = (mate ? b.qual2 : b.qual1) + roff;
         const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4);
-        uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0;
-        uint32_t fc[kChunks], fw[kChunks];
+        uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0, lowf = 0, tqf = 0, nbf = 0;  // whole-read sums
         // Loads are unconditional (every row of the batch is readable up to its stride) so the
         // whole chunk sequence is one basic block and the loads can be issued early; only the
         // chunks that some lane's read does not fill (wave-uniform test) pay for byte masks.
 #pragma unroll
         for (int k = 0; k < kChunks; ++k) {
-            fc[k] = 0;
-            fw[k] = 0;
             if (k < nchunks) {
                 const uint4 s4 = *reinterpret_cast<const uint4*>(S + 16 * k);
                 const uint4 q4 = *reinterpret_cast<const uint4*>(Q + 16 * k);
@@ -317,7 +344,6 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
                 const bool full = __all(L >= 16 * k + 16);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    col[(kFQ + 4 * k + j) * 64 + lane] = qw[j];
                     const uint32_t bm = full ? 0xFFFFFFFFu : bytemask(L - (16 * k + 4 * j));
                     const uint32_t kk = (sw[j] >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
@@ -328,11 +354,16 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
                     const uint32_t q7 = qm & 0x7F7F7F7Fu;
                     q20 += __popc(((q7 + 0x4A4A4A4Au) & 0x80808080u) & bm);  // q > '5'
                     q30 += __popc(((q7 + 0x40404040u) & 0x80808080u) & bm);  // q > '?'
+                    lowf += __popc(~(q7 + limq) & 0x80808080u & bm);          // q < limit
+                    tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);
                     cc |= (kk & 0x03030303u) << (2 * j);
                     nn4 |= ((kk >> 2) & 0x01010101u) << (2 * j);
                 }
-                fc[k] = tr4x4(cc);
-                fw[k] = tr4x4(nn4);
+                const uint32_t fck = tr4x4(cc), fwk = tr4x4(nn4);
+                nbf += __popc(fwk & (full ? 0x55555555u : posmask(L - 16 * k)));
+                // forward codes for now; read 2 lanes reverse-complement their column below
+                col[(kFC + k) * 64 + lane] = fck;
+                col[(kFN + k) * 64 + lane] = fwk;
             }
         }
         const bool bad = odd || exo != 0 || (qhi & 0x80808080u) != 0;
@@ -340,18 +371,22 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
             if (lane == 0) slow_tiles[atomicAdd(slow_count, 1)] = t;
             continue;
         }
-        if (mate == 0) {
+        for (int k = nchunks; k < kChunks; ++k) {  // unused tail of the column
+            col[(kFC + k) * 64 + lane] = 0u;
+            col[(kFN + k) * 64 + lane] = 0u;
+        }
+        if (mate == 1) {
+            // reverse-complement read 2's column in place: rc[j] = comp(code[L-1-j]); N stays N (3).
+            // Word m of the reversed 160-position column is pairrev(word 9-m); shifting by
+            // kMaxLen - L positions then aligns position L-1 to 0.
 #pragma unroll
-            for (int k = 0; k < kChunks; ++k) {
-                col[(kFC + k) * 64 + lane] = fc[k];
-                col[(kFN + k) * 64 + lane] = fw[k];
-            }
-        } else {
-            // reverse-complement read 2's codes: rc[j] = comp(code[L-1-j]); N stays N (3)
-#pragma unroll
-            for (int m = 0; m < kChunks; ++m) {
-                col[(kFC + m) * 64 + lane] = pairrev(fc[kChunks - 1 - m]);
-                col[(kFN + m) * 64 + lane] = pairrev(fw[kChunks - 1 - m]);
+            for (int m = 0; m < kChunks / 2; ++m) {
+                const uint32_t c0 = col[(kFC + m) * 64 + lane], c1 = col[(kFC + kChunks - 1 - m) * 64 + lane];
+                const uint32_t w0 = col[(kFN + m) * 64 + lane], w1 = col[(kFN + kChunks - 1 - m) * 64 + lane];
+                col[(kFC + m) * 64 + lane] = pairrev(c1);
+                col[(kFC + kChunks - 1 - m) * 64 + lane] = pairrev(c0);
+                col[(kFN + m) * 64 + lane] = pairrev(w1);
+                col[(kFN + kChunks - 1 - m) * 64 + lane] = pairrev(w0);
             }
             const int sh = kMaxLen - L, q = sh >> 4, r2 = 2 * (sh & 15);
             for (int m = 0; m < kChunks; ++m) {
@@ -370,12 +405,19 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+        FQ_STAMP(0)
         const CodeSeq seq{col, lane, L, rc};
-        const LdsQual qual{col, lane};
+        const PtrQual qual{Q};  // trimAndCut windows read the row in HBM/L2 (only with cut options)
 
         // ---------------- trimAndCut (src/peprocessor.cpp:292-293) ----------------
         int st = 0, n = 0;
-        bool nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n);
+        bool nn;
+        if (LEAN) {  // Filter::trimAndCut with nothing to trim returns the read as is (src/filter.cpp:71-75)
+            nn = valid;
+            n = L;
+        } else {
+            nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n);
+        }
         // the shuffle must run in every lane: ds_bpermute from a lane that is switched off returns
         // whatever its register held before (e.g. the previous tile's value)
         const int nn_o = __shfl_xor(nn ? 1 : 0, 32);
@@ -385,16 +427,18 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         rr.code = 0;
         rr.ad_pos = rr.ad_len = rr.m_len1 = rr.m_len2 = rr.reserved = 0;
 
+        FQ_STAMP(1)
         // ---------------- polyG (src/peprocessor.cpp:295-299) ----------------
         if (both && p.polyg_enabled && !(abl & 8)) {
             int bases;
-            n = polyg_bits(col, lane, rc, L, st, n, allowed, p.polyg_compare_req, bases);
+            n = polyg_bits(col, lane, rc, L, st, n, p.polyg_max_mismatch, g_inv, p.polyg_compare_req, bases);
             if (bases >= 0) {
                 sadd(&small[FQ_ACC_POLYX_READS + 3], 1ull);
                 sadd(&small[FQ_ACC_POLYX_BASES + 3], (unsigned long long)(long long)bases);
             }
         }
 
+        FQ_STAMP(2)
         // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
         if (both && !(abl & 1)) {
             const int st_o = __shfl_xor(st, 32), n_o = __shfl_xor(n, 32), L_o = __shfl_xor(L, 32);
@@ -446,7 +490,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
                         sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)((n1 - ol) + (n2 - ol)));
                     }
                     n = ol;
-                } else if (my_alen > 0) {  // AdapterTrimmer::trimBySequence, src/adaptertrimmer.cpp:29-90
+                } else if (!LEAN && my_alen > 0) {  // AdapterTrimmer::trimBySequence, src/adaptertrimmer.cpp:29-90
                     int pos;
                     if (trim_by_sequence_t(at(seq, st), n, my_ad, my_alen, pos)) {
                         int ad_len;
@@ -471,8 +515,9 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
             }
         }
 
+        FQ_STAMP(3)
         // ---------------- polyX, maxLen (src/peprocessor.cpp:335-349) ----------------
-        if (both && p.polyx_enabled) {
+        if (!LEAN && both && p.polyx_enabled) {
             int poly, bases;
             n = trim_polyx_t(at(seq, st), n, p.polyx_mask, p.polyx_compare_req, p.polyx_max_mismatch,
                              p.polyx_one_mismatch_per, poly, bases);
@@ -481,37 +526,47 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
                 sadd(&small[FQ_ACC_POLYX_BASES + poly], (unsigned long long)(long long)bases);
             }
         }
-        if (both && my_maxlen > 0 && my_maxlen < n) n = my_maxlen;
+        if (!LEAN && both && my_maxlen > 0 && my_maxlen < n) n = my_maxlen;
 
+        FQ_STAMP(4)
         // ---------------- passFilter (src/filter.cpp:3-52) ----------------
         int code = FQ_FAIL_LENGTH;
         uint32_t w20 = 0, w30 = 0;  // Q20/Q30 of the window, for the post stats
         if (nn && n > 0) {
-            int low = 0, tq = 0, nb = 0;
+            // window sums = whole-read sums (from staging) minus the trimmed head [0, st) and
+            // tail [st+n, L): the trimmed parts are usually a few bases
+            int low = (int)lowf, tq = (int)tqf, nb = (int)nbf;
+            w20 = q20;
+            w30 = q30;
             if (!(abl & 2)) {
                 const int end = st + n;
-                for (int F = st >> 4; F < ((end + 15) >> 4); ++F) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int b0 = 16 * F + 4 * j;
-                        const uint32_t bm = bytemask(end - b0) & ~bytemask(st - b0);
-                        const uint32_t w = col[(kFQ + 4 * F + j) * 64 + lane] & bm;
-                        const uint32_t w7 = w & 0x7F7F7F7Fu;
-                        low += __popc(~(w7 + limq) & 0x80808080u & bm);
-                        w20 += __popc(((w7 + 0x4A4A4A4Au) & 0x80808080u) & bm);
-                        w30 += __popc(((w7 + 0x40404040u) & 0x80808080u) & bm);
-                        tq = (int)__builtin_amdgcn_sad_u8(w, 0u, (uint32_t)tq);
+                for (int part = 0; part < 2; ++part) {
+                    const int a0 = part ? end : 0, a1 = part ? L : st;  // forward range [a0, a1)
+                    for (int F = a0 >> 4; F < ((a1 + 15) >> 4); ++F) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int b0 = 16 * F + 4 * j;
+                            const uint32_t bm = bytemask(a1 - b0) & ~bytemask(a0 - b0);
+                            const uint32_t w = *reinterpret_cast<const uint32_t*>(Q + 16 * F + 4 * j) & bm;
+                            const uint32_t w7 = w & 0x7F7F7F7Fu;
+                            low -= __popc(~(w7 + limq) & 0x80808080u & bm);
+                            w20 -= __popc(((w7 + 0x4A4A4A4Au) & 0x80808080u) & bm);
+                            w30 -= __popc(((w7 + 0x40404040u) & 0x80808080u) & bm);
+                            tq -= (int)__builtin_amdgcn_sad_u8(w, 0u, 0u);
+                        }
+                    }
+                    // N bits of the same range (read 2's column is reverse-complemented)
+                    const int s0 = rc ? L - a1 : a0, s1 = rc ? L - a0 : a1;
+                    for (int c = s0 >> 4; c < ((s1 + 15) >> 4); ++c) {
+                        const uint32_t w = col[(kFN + c) * 64 + lane];
+                        nb -= __popc(w & posmask(s1 - 16 * c) & ~posmask(s0 - 16 * c));
                     }
                 }
                 tq -= 33 * n;
-                // N count from the N mask (read 2's column is reverse-complemented)
-                const int lo = mate ? L - st - n : st;
-                for (int c = lo >> 4; c < ((lo + n + 15) >> 4); ++c) {
-                    const uint32_t w = col[(kFN + c) * 64 + lane];
-                    nb += __popc(w & posmask(lo + n - 16 * c) & ~posmask(lo - 16 * c));
-                }
             }
             code = filter_verdict(p, n, low, nb, tq, [&]() {
+                if (LEAN) return 0;  // not reached: LEAN excludes the complexity filter
                 int diff = 0;
                 for (int i = 0; i < n - 1; ++i) diff += seq(st + i) != seq(st + i + 1);
                 return diff;
@@ -521,15 +576,22 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         const bool pair_pass = both && code == FQ_PASS_FILTER && code_o == FQ_PASS_FILTER;
         if (mate == 0 && valid) sadd(&small[FQ_ACC_FILTER + max(code, code_o)], 2ull);  // addFilterResult: +2
 
+        FQ_STAMP(5)
         // ---------------- Stats::statRead, pre and post (src/peprocessor.cpp:276-277,400-401) ----
         if (valid && !(abl & 4)) {
             const int wlen = pair_pass ? n : 0;  // post window [st, st + wlen)
             const int nchl = (L + 15) >> 4;
             const int dsel = r >> 2;
+            // chunk F+1's codes (LDS) and qualities (the row again, now from L2) are fetched while
+            // chunk F's atomics issue
+            Fwd fn = fwd_chunk(col, lane, 0, rc, L);
+            uint4 qn = *reinterpret_cast<const uint4*>(Q);
             for (int F = 0; F < nchl; ++F) {
-                const Fwd f = fwd_chunk(col, lane, F, rc, L);
-                const uint32_t q0 = col[(kFQ + 4 * F) * 64 + lane], q1 = col[(kFQ + 4 * F + 1) * 64 + lane];
-                const uint32_t q2 = col[(kFQ + 4 * F + 2) * 64 + lane], q3 = col[(kFQ + 4 * F + 3) * 64 + lane];
+                const Fwd f = fn;
+                const uint32_t q0 = qn.x, q1 = qn.y, q2 = qn.z, q3 = qn.w;
+                const int Fn = min(F + 1, nchunks - 1);
+                fn = fwd_chunk(col, lane, Fn, rc, L);
+                qn = *reinterpret_cast<const uint4*>(Q + 16 * Fn);
                 // rotate the chunk by r positions: position t of the rotated view is 16F + (t+r)%16
                 const uint32_t cr = __builtin_amdgcn_alignbit(f.c, f.c, 2 * r);
                 const uint32_t nr = __builtin_amdgcn_alignbit(f.n, f.n, 2 * r);
@@ -540,29 +602,35 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
                 const uint32_t qr[4] = {__builtin_amdgcn_alignbyte(a1, a0, r & 3), __builtin_amdgcn_alignbyte(a2, a1, r & 3),
                                         __builtin_amdgcn_alignbyte(a3, a2, r & 3), __builtin_amdgcn_alignbyte(a0, a3, r & 3)};
 #pragma unroll
-                for (int tt = 0; tt < 16; ++tt) {
-                    const int pos = 16 * F + ((tt + r) & 15);
-                    const uint32_t qv = (qr[tt >> 2] >> (8 * (tt & 3))) & 0xFFu;
-                    const int slot = (int)(((cr >> (2 * tt)) & 3u) + ((nr >> (2 * tt)) & 1u));
-                    const unsigned long long v = kCount1 | (unsigned long long)(qv | 0x80u);
-                    const int a = pos * kCycW + 2 * slot;
-                    if (!(abl & 16)) {
-                        hadd(my_pre, pos < L ? a : kDummy, v);
-                        hadd(my_post, (unsigned)(pos - st) < (unsigned)wlen ? a - st * kCycW : kDummy, v);
+                for (int wi = 0; wi < 4; ++wi) {
+                    const uint32_t qw = qr[wi];
+#pragma unroll
+                    for (int bi = 0; bi < 4; ++bi) {
+                        const int tt = 4 * wi + bi;
+                        const int pos = 16 * F + ((tt + r) & 15);
+                        const uint32_t qv = (qw >> (8 * bi)) & 0xFFu;
+                        const int slot = (int)(((cr >> (2 * tt)) & 3u) + ((nr >> (2 * tt)) & 1u));
+                        const unsigned long long v = kCount1 | (unsigned long long)(qv | 0x80u);
+                        if (!(abl & 16)) {
+                            hadd(my_pre, cell(pos, pos < L ? slot : kDummySlot), v);
+                            const bool inw = (unsigned)(pos - st) < (unsigned)wlen;
+                            hadd(my_post, inw ? cell(pos - st, slot) : cell(pos, kDummySlot), v);
+                        }
                     }
                 }
             }
             s_pre[0] += 1;
-            s_pre[1] += (unsigned long long)L;
+            s_pre[1] += (uint32_t)L;
             s_pre[2] += q20;
             s_pre[3] += q30;
             if (pair_pass) {
                 s_post[0] += 1;
-                s_post[1] += (unsigned long long)n;
+                s_post[1] += (uint32_t)n;
                 s_post[2] += w20;
                 s_post[3] += w30;
             }
         }
+        FQ_STAMP(6)
         if (valid) {
             rr.start = nn ? (uint16_t)st : 0;
             rr.len = nn ? (uint16_t)n : 0;
@@ -571,11 +639,17 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         }
     }
 
+    FQ_STAMP(7)
+#ifdef FQ_PHASE_STAMPS
+    if (stamps && lane == 0)
+        for (int i = 0; i < kPhases; ++i) atomicAdd(&g_phase_cycles[i], ph[i]);
+#endif
+#undef FQ_STAMP
     // per-lane stats scalars -> LDS
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-        if (s_pre[f]) sadd(&scal[4 * mate + f], s_pre[f]);
-        if (s_post[f]) sadd(&scal[4 * (2 + mate) + f], s_post[f]);
+        if (s_pre[f]) sadd(&scal[4 * mate + f], (unsigned long long)s_pre[f]);
+        if (s_post[f]) sadd(&scal[4 * (2 + mate) + f], (unsigned long long)s_post[f]);
     }
     __syncthreads();
 
@@ -595,7 +669,7 @@ __global__ void __launch_bounds__(kBlock) pe_fast_kernel(fq_params p, fq_batch b
         const int k = i / (ncyc * 5);
         const int rem = i - k * ncyc * 5;
         const int c = rem / 5, slot = rem - c * 5;
-        const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hist + k * kHistW + c * kCycW + 2 * slot);
+        const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hist + k * kHistW + cell(c, slot));
         const long long cnt = (long long)(v >> 40);
         const long long qs = (long long)(v & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
         if (cnt == 0) continue;
@@ -612,14 +686,34 @@ bool fq_pe_fast_supported(const fq_params& p) {
     return p.paired && !p.merge_enabled && p.insert_size_max <= 512 && p.insert_size_max >= 0;
 }
 
+// profiling aid (tools/ablate.py --phases): read and clear the per-phase cycle totals
+extern "C" __attribute__((visibility("default"))) int fq_debug_phase_cycles(unsigned long long* out, int n) {
+    unsigned long long h[kPhases];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase_cycles), sizeof h) != hipSuccess) return -3;
+    const unsigned long long z[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z) != hipSuccess) return -3;
+    for (int i = 0; i < n && i < kPhases; ++i) out[i] = h[i];
+    return 0;
+}
+
 hipError_t fq_pe_fast_prepare() {
-    return hipFuncSetAttribute((const void*)pe_fast_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)pe_fast_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       kLdsWords * 4);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)pe_fast_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                kLdsWords * 4);
 }
 
 hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
                              int* slow_tiles, int* slow_count, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL(pe_fast_kernel, dim3(grid), dim3(kBlock), kLdsWords * 4, stream, p, b, res, acc, slow_tiles,
-                       slow_count);
+    const bool lean = p.trim_front1 == 0 && p.trim_tail1 == 0 && p.trim_front2 == 0 && p.trim_tail2 == 0 &&
+                      !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
+                      p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled;
+    if (lean)
+        hipLaunchKernelGGL(pe_fast_kernel<true>, dim3(grid * kBlocksPerCU), dim3(kBlock), kLdsWords * 4, stream, p, b, res,
+                           acc, slow_tiles, slow_count);
+    else
+        hipLaunchKernelGGL(pe_fast_kernel<false>, dim3(grid * kBlocksPerCU), dim3(kBlock), kLdsWords * 4, stream, p, b,
+                           res, acc, slow_tiles, slow_count);
     return hipGetLastError();
 }

@@ -32,3 +32,20 @@ for rep in range(3):
 for name, _ in variants:
     v = sorted(results[name])
     print(f"{name:28s} median {v[len(v)//2]:8.2f} ms  min {v[0]:8.2f}  -> {n / (v[len(v)//2] / 1e3) / 1e9:.2f} G pairs/s", flush=True)
+
+# per-phase wave cycles (fq_params.reserved[1] = 1)
+names = ["staging", "trim", "polyG", "overlap", "polyX/maxlen", "filter", "stats", "store"]
+p = abi.default_params(True, 256); p.qual_filter_enabled = 1; p.adapter_trimming = 1; p.polyg_enabled = 1
+p.reserved[1] = 1
+h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
+lib.fq_debug_phase_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+out = (ctypes.c_ulonglong * 8)()
+lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_engine_sync(h)
+lib.fq_debug_phase_cycles(out, 8)
+lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_engine_sync(h)
+print("stamped run ms", lib.fq_engine_last_kernel_ms(h))
+lib.fq_debug_phase_cycles(out, 8)
+tot = sum(out)
+for nm, v in zip(names, out):
+    print(f"phase {nm:14s} {100.0 * v / tot:6.1f}%  {v / 2048:14.0f} cycles/wave")
+lib.fq_engine_destroy(h)

@@ -16,7 +16,7 @@ pass() {
     return $rc
 }
 if [ "${PMC_LIST:-0}" = 1 ]; then
-    timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc_list.txt 2>&1 || true
+    timeout -k 10 120 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
 fi
 for g in ${PMC_GROUPS:-fetch write sq lds}; do
     case $g in
@@ -24,6 +24,8 @@ for g in ${PMC_GROUPS:-fetch write sq lds}; do
     write) pass write WRITE_SIZE || exit $? ;;
     sq) pass sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit $? ;;
     lds) pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE || exit $? ;;
+    lds2) pass lds2 SQ_LDS_IDX_ACTIVE SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_LDS_ATOMIC SQ_BUSY_CU_CYCLES SQ_ACTIVE_INST_VALU || exit $? ;;
+    mem) pass mem SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY || exit $? ;;
     *) echo "unknown group $g"; exit 2 ;;
     esac
 done
