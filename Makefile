@@ -4,6 +4,10 @@
 HIPCC      ?= /opt/rocm/bin/hipcc
 ARCH       ?= gfx950
 HIPFLAGS   ?= -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+# make STAMPS=1: compile the per-phase cycle stamps of the fast kernel in (profiling only)
+ifneq ($(STAMPS),)
+HIPFLAGS   += -DFQ_PHASE_STAMPS
+endif
 CSRC       := fqtool_amd/csrc
 LIBDIR     := fqtool_amd/lib
 OBJDIR     := build/obj

@@ -5,25 +5,30 @@
 // PairEndProcessor::processPairEnd (reference src/peprocessor.cpp:261-508) keeps all 64 lanes
 // busy and the two mates of a pair are lanes l and l^32 of the same wave.
 //
+// Occupancy: 2 workgroups (16 waves) per CU; the only per-wave LDS is the 2-bit code / N-mask
+// column block (5 KB), and the workgroup's Stats histograms are shared by its 8 waves.
+//
 // Staging: each lane streams its seq and qual rows from HBM with 16-byte loads.  Sequence bytes
 // are reduced in registers to 2-bit base codes (A=0 C=1 T=2 G=3, N=3, i.e. (byte>>1)&3) plus a
-// spaced N mask; quality bytes are kept verbatim.  Both go to the lane's own LDS column (word
-// field*64 + lane: conflict-free for any per-lane position).  Read 1 codes are stored forward,
-// read 2 codes reverse-complemented (the orientation OverlapAnalysis::analyze compares,
-// src/overlapanalysis.cpp:7-72); qualities are forward for both.  A tile with a byte outside
-// {A,C,G,T,N}, a quality >= 128 or a read longer than 160 is handed to the general kernel
-// (pe_kernel.hip) through a device-side tile list, so everything here may assume that alphabet
-// and rebuild bases from codes.
+// spaced N mask and go to the lane's own LDS column (word field*64 + lane: conflict-free for any
+// per-lane position).  Read 1 codes are stored forward; read 2's column is the reverse complement
+// of its whole 160-position row (the orientation OverlapAnalysis::analyze compares,
+// src/overlapanalysis.cpp:7-72), so rc position j of a read of length L sits at index
+// j + 160 - L.  Whole-read quality sums (Q20/Q30, below-limit count, total) are taken from the
+// quality registers; qualities are not kept: later passes re-read the row (an L2 hit).  A tile
+// with a byte outside {A,C,G,T,N}, a quality >= 128 or a read longer than 160 is handed to the
+// general kernel (pe_kernel.hip) through a device-side tile list, so everything here may assume
+// that alphabet and rebuild bases from codes.
 //
-// Per read, in the reference's order: trimAndCut (integer windows over LDS qualities), polyG
-// (bit-parallel: the 3'-end scan only changes state at non-G bases, visited with find-last-set),
-// overlap analysis (read 1 lanes scan phase 1, read 2 lanes phase 2 through one code path: a
-// 16-position code-mismatch lower bound rejects offsets, survivors are verified exactly with
-// codes + N masks under the reference's break/accept rule), adapter trimming, polyX, maxLen,
-// passFilter (SWAR over the window's quality words), then Stats::statRead for the pre and post
-// blocks into workgroup-private LDS histograms of u64 cells (count << 40 | sum(q+128)); lanes
-// walk each 16-position chunk from a lane-dependent rotation so a wave's atomics spread over
-// cycles.
+// Per read, in the reference's order: trimAndCut (integer windows), polyG (bit-parallel: the
+// 3'-end scan only changes state at non-G bases, visited with find-last-set), overlap analysis
+// (read 1 lanes scan phase 1, read 2 lanes phase 2 through one code path: a 16-position
+// code-mismatch lower bound rejects offsets, survivors are verified exactly with codes + N masks
+// under the reference's break/accept rule), adapter trimming, polyX, maxLen, passFilter (whole-
+// read sums minus the trimmed ends), then Stats::statRead for the pre and post blocks into
+// workgroup-private LDS histograms of u64 cells (count << 40 | sum(q+128)); lanes walk each
+// 16-position chunk from a lane-dependent rotation so the lanes of an atomic hit distinct banks.
+// The LEAN instantiation drops the options the headline workloads do not use.
 #include <hip/hip_runtime.h>
 
 #include "device_ops.h"
@@ -101,12 +106,15 @@ struct Fwd {
     uint32_t c, n;
 };
 
-// forward codes / N mask of positions [16F, 16F+16) of lane c's read of length L (read 2
-// columns are stored reverse-complemented); positions >= L are garbage for the caller to mask
-__device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool rc, int L) {
-    const int s0 = rc ? L - 16 - 16 * F : 16 * F;
-    uint32_t cw = field_window(col, kFC, c, s0);
-    uint32_t nw = field_window(col, kFN, c, s0);
+// forward codes / N mask of positions [16F, 16F+16) of lane c's read.  Read 2 columns hold the
+// reverse complement of the whole 160-position row, so forward chunk F is stored word 9-F with
+// its fields reversed and complemented; positions >= L are garbage for the caller to mask.
+__device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool rc) {
+    const int w = rc ? kChunks - 1 - F : F;
+    const bool in = (unsigned)w < (unsigned)kChunks;
+    const int wc = in ? w : 0;
+    uint32_t cw = in ? col[(kFC + wc) * 64 + c] : 0u;
+    uint32_t nw = in ? col[(kFN + wc) * 64 + c] : 0u;
     if (rc) {
         cw = pairrev(cw);
         nw = pairrev(nw);
@@ -115,13 +123,12 @@ __device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool
     return Fwd{cw, nw};
 }
 
-
 struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N)
     const uint32_t* col;
-    int c, L;
+    int c;
     bool rc;
     __device__ __forceinline__ uint8_t operator()(int i) const {
-        const int q = rc ? L - 1 - i : i;
+        const int q = rc ? kMaxLen - 1 - i : i;
         const int w = q >> 4, sh = 2 * (q & 15);
         uint32_t code = (col[(kFC + w) * 64 + c] >> sh) & 3u;
         const uint32_t nb = (col[(kFN + w) * 64 + c] >> sh) & 1u;
@@ -211,12 +218,12 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int
                                  int compareReq, int& bases) {
     const int e = st + n - 1;  // last forward position of the window
     const int Fe = e >> 4, Fs = st >> 4;
-    const uint32_t g0 = gmask(fwd_chunk(col, c, Fe, rc, L));
-    const uint32_t g1 = gmask(fwd_chunk(col, c, Fe - 1, rc, L));
+    const uint32_t g0 = gmask(fwd_chunk(col, c, Fe, rc));
+    const uint32_t g1 = gmask(fwd_chunk(col, c, Fe - 1, rc));
     int mism = 0, iend = n;  // iend: scan index of the break, or rlen when the scan ran through
     if (maxMM < 0) iend = 0;  // mismatch 0 > allowed at the very first base
     for (int F = Fe; F >= Fs && iend == n; --F) {
-        const uint32_t g = F == Fe ? g0 : F == Fe - 1 ? g1 : gmask(fwd_chunk(col, c, F, rc, L));
+        const uint32_t g = F == Fe ? g0 : F == Fe - 1 ? g1 : gmask(fwd_chunk(col, c, F, rc));
         uint32_t m = ~g & 0x55555555u & posmask(e - 16 * F + 1) & ~posmask(st - 16 * F);
         while (m) {
             const int b = 31 - __clz(m);
@@ -236,7 +243,7 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int
     int firstG = n - 1;
     const int lo = e - iend + 1;
     for (int F = lo >> 4; F <= Fe; ++F) {
-        uint32_t g = F == Fe ? g0 : F == Fe - 1 ? g1 : gmask(fwd_chunk(col, c, F, rc, L));
+        uint32_t g = F == Fe ? g0 : F == Fe - 1 ? g1 : gmask(fwd_chunk(col, c, F, rc));
         g &= posmask(e - 16 * F + 1) & ~posmask(lo - 16 * F);
         if (g) {
             firstG = 16 * F + ((__ffs(g) - 1) >> 1) - st;
@@ -281,9 +288,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
     __syncthreads();
 
-    const int mate = lane >> 5, pl = lane & 31;
-    const int mlane = lane ^ 32;
-    const bool rc = mate == 1;
     // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
     // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics
     const int abl = p.reserved[0];
@@ -292,17 +296,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     const int limit = p.overlap_diff_limit;
     const int K = max(limit, 1);
     const int req = p.overlap_require;
-    const int front = mate ? p.trim_front2 : p.trim_front1;
-    const int tail = mate ? p.trim_tail2 : p.trim_tail1;
-    const uint8_t* my_ad = adp + (mate ? FQ_MAX_ADAPTER : 0);
-    const int my_alen = mate ? p.adapter2_len : p.adapter1_len;
-    const int my_maxlen = mate ? p.max_len2 : p.max_len1;
     const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
     const int g_per = max(p.polyg_one_mismatch_per, 1);
     const int g_inv = g_per > 256 ? 0 : (65536 + g_per - 1) / g_per;
-    uint32_t* my_pre = hist + mate * kHistW;
-    uint32_t* my_post = hist + (2 + mate) * kHistW;
-    const int r = lane & 15;  // stats rotation within a chunk
     // per-lane stats scalars: a lane sees at most a few hundred reads of <= 160 bases, so u32 holds them
     uint32_t s_pre[4] = {0, 0, 0, 0}, s_post[4] = {0, 0, 0, 0};
 #ifdef FQ_PHASE_STAMPS
@@ -320,6 +316,21 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 #endif
 
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
+        // Per-lane values are derived from an opaque copy of the lane id inside the loop: left to
+        // itself the compiler hoists dozens of them out of the tile loop and spills them.
+        int lane_x = lane;
+        asm volatile("" : "+v"(lane_x));
+        const int mate = lane_x >> 5, pl = lane_x & 31;
+        const int mlane = lane_x ^ 32;
+        const bool rc = mate == 1;
+        const int front = mate ? p.trim_front2 : p.trim_front1;
+        const int tail = mate ? p.trim_tail2 : p.trim_tail1;
+        const uint8_t* my_ad = adp + (mate ? FQ_MAX_ADAPTER : 0);
+        const int my_alen = mate ? p.adapter2_len : p.adapter1_len;
+        const int my_maxlen = mate ? p.max_len2 : p.max_len1;
+        uint32_t* my_pre = hist + mate * kHistW;
+        uint32_t* my_post = hist + (2 + mate) * kHistW;
+        const int r = lane_x & 15;  // stats rotation within a chunk
         const int idx = t * 32 + pl;
         const bool valid = idx < b.n;
         const int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
@@ -330,14 +341,32 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         const uint8_t* Q = (mate ? b.qual2 : b.qual1) + roff;
         const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4);
         uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0, lowf = 0, tqf = 0, nbf = 0;  // whole-read sums
-        // Loads are unconditional (every row of the batch is readable up to its stride) so the
-        // whole chunk sequence is one basic block and the loads can be issued early; only the
-        // chunks that some lane's read does not fill (wave-uniform test) pay for byte masks.
+        // column word of chunk k: k for read 1, 9-k for read 2 (stepped, not precomputed, so the
+        // ten addresses are not kept live across tiles)
+        uint32_t* wp = col + lane_x + (rc ? (kChunks - 1) * 64 : 0);
+        const int wstep = rc ? -64 : 64;
+        // Row chunks are requested three ahead of their use (software pipelining: one HBM round
+        // trip per tile instead of one per chunk); every row is readable up to its stride, so
+        // the look-ahead loads are clamped, never guarded.  Only the chunks that some lane's read
+        // does not fill (wave-uniform test) pay for byte masks.
+        const int lastc = nchunks - 1;
+        uint4 sA = *reinterpret_cast<const uint4*>(S), qA = *reinterpret_cast<const uint4*>(Q);
+        uint4 sB = *reinterpret_cast<const uint4*>(S + 16 * min(1, lastc));
+        uint4 qB = *reinterpret_cast<const uint4*>(Q + 16 * min(1, lastc));
+        uint4 sC = *reinterpret_cast<const uint4*>(S + 16 * min(2, lastc));
+        uint4 qC = *reinterpret_cast<const uint4*>(Q + 16 * min(2, lastc));
 #pragma unroll
         for (int k = 0; k < kChunks; ++k) {
+            const uint4 s4 = sA, q4 = qA;
+            sA = sB;
+            qA = qB;
+            sB = sC;
+            qB = qC;
+            if (k + 3 < kChunks) {
+                sC = *reinterpret_cast<const uint4*>(S + 16 * min(k + 3, lastc));
+                qC = *reinterpret_cast<const uint4*>(Q + 16 * min(k + 3, lastc));
+            }
             if (k < nchunks) {
-                const uint4 s4 = *reinterpret_cast<const uint4*>(S + 16 * k);
-                const uint4 q4 = *reinterpret_cast<const uint4*>(Q + 16 * k);
                 const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
                 const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
                 uint32_t cc = 0, nn4 = 0;
@@ -361,9 +390,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 }
                 const uint32_t fck = tr4x4(cc), fwk = tr4x4(nn4);
                 nbf += __popc(fwk & (full ? 0x55555555u : posmask(L - 16 * k)));
-                // forward codes for now; read 2 lanes reverse-complement their column below
-                col[(kFC + k) * 64 + lane] = fck;
-                col[(kFN + k) * 64 + lane] = fwk;
+                // read 2: the column is the reverse complement of the 160-position row, so the
+                // read's rc position j sits at index j + (160 - L); garbage beyond L lands below
+                const uint32_t rn = pairrev(fwk);
+                wp[kFC * 64] = rc ? (pairrev(fck) ^ (0xAAAAAAAAu & ~(rn << 1))) : fck;
+                wp[kFN * 64] = rc ? rn : fwk;
+                wp += wstep;
             }
         }
         const bool bad = odd || exo != 0 || (qhi & 0x80808080u) != 0;
@@ -371,42 +403,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             if (lane == 0) slow_tiles[atomicAdd(slow_count, 1)] = t;
             continue;
         }
-        for (int k = nchunks; k < kChunks; ++k) {  // unused tail of the column
-            col[(kFC + k) * 64 + lane] = 0u;
-            col[(kFN + k) * 64 + lane] = 0u;
-        }
-        if (mate == 1) {
-            // reverse-complement read 2's column in place: rc[j] = comp(code[L-1-j]); N stays N (3).
-            // Word m of the reversed 160-position column is pairrev(word 9-m); shifting by
-            // kMaxLen - L positions then aligns position L-1 to 0.
-#pragma unroll
-            for (int m = 0; m < kChunks / 2; ++m) {
-                const uint32_t c0 = col[(kFC + m) * 64 + lane], c1 = col[(kFC + kChunks - 1 - m) * 64 + lane];
-                const uint32_t w0 = col[(kFN + m) * 64 + lane], w1 = col[(kFN + kChunks - 1 - m) * 64 + lane];
-                col[(kFC + m) * 64 + lane] = pairrev(c1);
-                col[(kFC + kChunks - 1 - m) * 64 + lane] = pairrev(c0);
-                col[(kFN + m) * 64 + lane] = pairrev(w1);
-                col[(kFN + kChunks - 1 - m) * 64 + lane] = pairrev(w0);
-            }
-            const int sh = kMaxLen - L, q = sh >> 4, r2 = 2 * (sh & 15);
-            for (int m = 0; m < kChunks; ++m) {
-                const int a = m + q;
-                const uint32_t clo = a < kChunks ? col[(kFC + a) * 64 + lane] : 0u;
-                const uint32_t chi = a + 1 < kChunks ? col[(kFC + a + 1) * 64 + lane] : 0u;
-                const uint32_t wlo = a < kChunks ? col[(kFN + a) * 64 + lane] : 0u;
-                const uint32_t whi = a + 1 < kChunks ? col[(kFN + a + 1) * 64 + lane] : 0u;
-                const uint32_t w = __builtin_amdgcn_alignbit(whi, wlo, r2);
-                const uint32_t c = __builtin_amdgcn_alignbit(chi, clo, r2) ^ (0xAAAAAAAAu & ~(w << 1));
-                col[(kFC + m) * 64 + lane] = c;
-                col[(kFN + m) * 64 + lane] = w;
-            }
+        for (int k = nchunks; k < kChunks; ++k) {  // unused tail of the row
+            wp[kFC * 64] = 0u;
+            wp[kFN * 64] = 0u;
+            wp += wstep;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
         FQ_STAMP(0)
-        const CodeSeq seq{col, lane, L, rc};
+        const CodeSeq seq{col, lane, rc};
         const PtrQual qual{Q};  // trimAndCut windows read the row in HBM/L2 (only with cut options)
 
         // ---------------- trimAndCut (src/peprocessor.cpp:292-293) ----------------
@@ -441,11 +448,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         FQ_STAMP(2)
         // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
         if (both && !(abl & 1)) {
-            const int st_o = __shfl_xor(st, 32), n_o = __shfl_xor(n, 32), L_o = __shfl_xor(L, 32);
+            const int st_o = __shfl_xor(st, 32), n_o = __shfl_xor(n, 32);
             const int st1 = mate ? st_o : st, n1 = mate ? n_o : n;
-            const int st2 = mate ? st : st_o, n2 = mate ? n : n_o, L2 = mate ? L : L_o;
+            const int st2 = mate ? st : st_o, n2 = mate ? n : n_o;
             const int c1 = mate ? mlane : lane, c2 = mate ? lane : mlane;
-            const int off2 = L2 - st2 - n2;  // rc2 of the trimmed read starts here in rc coordinates
+            const int off2 = kMaxLen - st2 - n2;  // column index where rc2 of the trimmed read starts
             // read 1 lanes: phase 1 (offset o >= 0: r1 window moves, rc2 fixed);
             // read 2 lanes: phase 2 (offset -m <= 0: rc2 window moves, r1 fixed)
             const int cm = mate ? c2 : c1, mpos = mate ? off2 : st1;
@@ -540,26 +547,33 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             w30 = q30;
             if (!(abl & 2)) {
                 const int end = st + n;
+                const bool need_tq = p.avg_qual_limit > 0;  // the total quality only feeds -e
 #pragma unroll
                 for (int part = 0; part < 2; ++part) {
                     const int a0 = part ? end : 0, a1 = part ? L : st;  // forward range [a0, a1)
-                    for (int F = a0 >> 4; F < ((a1 + 15) >> 4); ++F) {
+                    const int F0 = a0 >> 4, F1 = (a1 + 15) >> 4;
+                    // row chunks come from L2; the next one is requested before this one is used
+                    uint4 cur = *reinterpret_cast<const uint4*>(Q + 16 * min(F0, nchunks - 1));
+                    for (int F = F0; F < F1; ++F) {
+                        const uint4 nxt = *reinterpret_cast<const uint4*>(Q + 16 * min(F + 1, nchunks - 1));
+                        const uint32_t wq[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const int b0 = 16 * F + 4 * j;
                             const uint32_t bm = bytemask(a1 - b0) & ~bytemask(a0 - b0);
-                            const uint32_t w = *reinterpret_cast<const uint32_t*>(Q + 16 * F + 4 * j) & bm;
+                            const uint32_t w = wq[j] & bm;
                             const uint32_t w7 = w & 0x7F7F7F7Fu;
                             low -= __popc(~(w7 + limq) & 0x80808080u & bm);
                             w20 -= __popc(((w7 + 0x4A4A4A4Au) & 0x80808080u) & bm);
                             w30 -= __popc(((w7 + 0x40404040u) & 0x80808080u) & bm);
-                            tq -= (int)__builtin_amdgcn_sad_u8(w, 0u, 0u);
+                            if (need_tq) tq -= (int)__builtin_amdgcn_sad_u8(w, 0u, 0u);
                         }
+                        cur = nxt;
                     }
                     // N bits of the same range (read 2's column is reverse-complemented)
-                    const int s0 = rc ? L - a1 : a0, s1 = rc ? L - a0 : a1;
+                    const int s0 = rc ? kMaxLen - a1 : a0, s1 = rc ? kMaxLen - a0 : a1;
                     for (int c = s0 >> 4; c < ((s1 + 15) >> 4); ++c) {
-                        const uint32_t w = col[(kFN + c) * 64 + lane];
+                        const uint32_t w = col[(kFN + c) * 64 + lane_x];
                         nb -= __popc(w & posmask(s1 - 16 * c) & ~posmask(s0 - 16 * c));
                     }
                 }
@@ -582,16 +596,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             const int wlen = pair_pass ? n : 0;  // post window [st, st + wlen)
             const int nchl = (L + 15) >> 4;
             const int dsel = r >> 2;
-            // chunk F+1's codes (LDS) and qualities (the row again, now from L2) are fetched while
-            // chunk F's atomics issue
-            Fwd fn = fwd_chunk(col, lane, 0, rc, L);
+            // chunk F+1's codes (LDS) and the qualities of chunks F+1, F+2 (the row again, now from
+            // L2) are in flight while chunk F's atomics issue
+            Fwd fn = fwd_chunk(col, lane_x, 0, rc);
             uint4 qn = *reinterpret_cast<const uint4*>(Q);
+            uint4 qnn = *reinterpret_cast<const uint4*>(Q + 16 * min(1, nchunks - 1));
             for (int F = 0; F < nchl; ++F) {
                 const Fwd f = fn;
                 const uint32_t q0 = qn.x, q1 = qn.y, q2 = qn.z, q3 = qn.w;
-                const int Fn = min(F + 1, nchunks - 1);
-                fn = fwd_chunk(col, lane, Fn, rc, L);
-                qn = *reinterpret_cast<const uint4*>(Q + 16 * Fn);
+                qn = qnn;
+                qnn = *reinterpret_cast<const uint4*>(Q + 16 * min(F + 2, nchunks - 1));
+                fn = fwd_chunk(col, lane_x, min(F + 1, nchunks - 1), rc);
                 // rotate the chunk by r positions: position t of the rotated view is 16F + (t+r)%16
                 const uint32_t cr = __builtin_amdgcn_alignbit(f.c, f.c, 2 * r);
                 const uint32_t nr = __builtin_amdgcn_alignbit(f.n, f.n, 2 * r);
@@ -648,8 +663,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     // per-lane stats scalars -> LDS
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-        if (s_pre[f]) sadd(&scal[4 * mate + f], (unsigned long long)s_pre[f]);
-        if (s_post[f]) sadd(&scal[4 * (2 + mate) + f], (unsigned long long)s_post[f]);
+        if (s_pre[f]) sadd(&scal[4 * (lane >> 5) + f], (unsigned long long)s_pre[f]);
+        if (s_post[f]) sadd(&scal[4 * (2 + (lane >> 5)) + f], (unsigned long long)s_post[f]);
     }
     __syncthreads();
 
