@@ -56,7 +56,8 @@ constexpr int kHistW = kChunks * kSlots * 32;
 __host__ __device__ constexpr int cell(int c, int slot) { return ((c >> 4) * kSlots + slot) * 32 + 2 * (c & 15); }
 constexpr int kSmallU64 = FQ_ACC_INSERT + 512 + 1;
 constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
-constexpr int kScalW = 2 * 16;  // [4 stats][reads, length_sum, q20, q30] u64
+constexpr int kScalCopies = 16;  // per-read scalars are spread over 16 copies (lane & 15)
+constexpr int kScalW = 2 * 16 * kScalCopies;  // [copy][4 stats][reads, length_sum, q20, q30] u64
 constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
 constexpr int kColsW = kWaves * kWaveW;
 constexpr int kLdsWords = kColsW + 4 * kHistW + kSmallW + kScalW + kAdW;
@@ -282,7 +283,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     uint32_t* hist = lds + kColsW;  // [pre1, pre2, post1, post2] x kHistW
     unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + 4 * kHistW);
     unsigned long long* scal = small + kSmallW / 2;
-    uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16);
+    uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16 * kScalCopies);
     for (int i = threadIdx.x; i < 4 * kHistW + kSmallW + kScalW; i += kBlock) hist[i] = 0;
     for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kBlock)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
@@ -299,8 +300,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
     const int g_per = max(p.polyg_one_mismatch_per, 1);
     const int g_inv = g_per > 256 ? 0 : (65536 + g_per - 1) / g_per;
-    // per-lane stats scalars: a lane sees at most a few hundred reads of <= 160 bases, so u32 holds them
-    uint32_t s_pre[4] = {0, 0, 0, 0}, s_post[4] = {0, 0, 0, 0};
 #ifdef FQ_PHASE_STAMPS
     const bool stamps = p.reserved[1] != 0;
     unsigned long long ph[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -634,15 +633,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     }
                 }
             }
-            s_pre[0] += 1;
-            s_pre[1] += (uint32_t)L;
-            s_pre[2] += q20;
-            s_pre[3] += q30;
+            // per-read scalars straight to LDS (lanes l, l+16 share a copy): nothing stays live
+            unsigned long long* sc = scal + 16 * (lane_x & 15) + 4 * mate;
+            sadd(&sc[0], 1ull);
+            sadd(&sc[1], (unsigned long long)L);
+            sadd(&sc[2], (unsigned long long)q20);
+            sadd(&sc[3], (unsigned long long)q30);
             if (pair_pass) {
-                s_post[0] += 1;
-                s_post[1] += (uint32_t)n;
-                s_post[2] += w20;
-                s_post[3] += w30;
+                sadd(&sc[8], 1ull);
+                sadd(&sc[9], (unsigned long long)n);
+                sadd(&sc[10], (unsigned long long)w20);
+                sadd(&sc[11], (unsigned long long)w30);
             }
         }
         FQ_STAMP(6)
@@ -660,12 +661,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         for (int i = 0; i < kPhases; ++i) atomicAdd(&g_phase_cycles[i], ph[i]);
 #endif
 #undef FQ_STAMP
-    // per-lane stats scalars -> LDS
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-        if (s_pre[f]) sadd(&scal[4 * (lane >> 5) + f], (unsigned long long)s_pre[f]);
-        if (s_post[f]) sadd(&scal[4 * (2 + (lane >> 5)) + f], (unsigned long long)s_post[f]);
-    }
     __syncthreads();
 
     // ---------------- flush to the global accumulator ----------------
@@ -676,7 +671,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     const size_t st_words = acc_stats_words(p.max_cycles);
     if (threadIdx.x < 16) {
         const int k = threadIdx.x >> 2, f = threadIdx.x & 3;
-        const unsigned long long v = scal[threadIdx.x];
+        unsigned long long v = 0;
+        for (int c = 0; c < kScalCopies; ++c) v += scal[16 * c + threadIdx.x];
         if (v) atomicAdd(&acc[st_base + k * st_words + f], v);
     }
     const int ncyc = min(kMaxLen, p.max_cycles);
