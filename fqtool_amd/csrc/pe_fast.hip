@@ -298,6 +298,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     const int K = max(limit, 1);
     const int req = p.overlap_require;
     const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
+    // Without front trimming every kept window starts at 0, so the post blocks are accumulated
+    // as "removed" (trimmed tails and failed pairs) and become pre - removed at the flush.
+    const bool removed_mode = LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front);
     const int g_per = max(p.polyg_one_mismatch_per, 1);
     const int g_inv = g_per > 256 ? 0 : (65536 + g_per - 1) / g_per;
 #ifdef FQ_PHASE_STAMPS
@@ -328,7 +331,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         const int my_alen = mate ? p.adapter2_len : p.adapter1_len;
         const int my_maxlen = mate ? p.max_len2 : p.max_len1;
         uint32_t* my_pre = hist + mate * kHistW;
-        uint32_t* my_post = hist + (2 + mate) * kHistW;
+        uint32_t* my_post = hist + (2 + mate) * kHistW;  // post block, or the "removed" block (see below)
         const int r = lane_x & 15;  // stats rotation within a chunk
         const int idx = t * 32 + pl;
         const bool valid = idx < b.n;
@@ -627,8 +630,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                         const unsigned long long v = kCount1 | (unsigned long long)(qv | 0x80u);
                         if (!(abl & 16)) {
                             hadd(my_pre, cell(pos, pos < L ? slot : kDummySlot), v);
-                            const bool inw = (unsigned)(pos - st) < (unsigned)wlen;
-                            hadd(my_post, inw ? cell(pos - st, slot) : cell(pos, kDummySlot), v);
+                            if (removed_mode) {
+                                // post = pre - removed: only the bases outside the kept window are
+                                // added, so these atomics run with few active lanes
+                                if (pos >= wlen && pos < L) hadd(my_post, cell(pos, slot), v);
+                            } else {
+                                const bool inw = (unsigned)(pos - st) < (unsigned)wlen;
+                                hadd(my_post, inw ? cell(pos - st, slot) : cell(pos, kDummySlot), v);
+                            }
                         }
                     }
                 }
@@ -681,9 +690,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         const int rem = i - k * ncyc * 5;
         const int c = rem / 5, slot = rem - c * 5;
         const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hist + k * kHistW + cell(c, slot));
-        const long long cnt = (long long)(v >> 40);
-        const long long qs = (long long)(v & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
-        if (cnt == 0) continue;
+        long long cnt = (long long)(v >> 40);
+        long long qs = (long long)(v & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
+        if (k >= 2 && removed_mode) {  // post = pre - removed
+            const unsigned long long pv =
+                *reinterpret_cast<const unsigned long long*>(hist + (k - 2) * kHistW + cell(c, slot));
+            const long long pc = (long long)(pv >> 40);
+            const long long pq = (long long)(pv & kQMask) - 161ll * pc;
+            cnt = pc - cnt;
+            qs = pq - qs;
+        }
+        if (cnt == 0 && qs == 0) continue;
         const int cls = slot_class(slot);
         unsigned long long* dst = acc + st_base + k * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
         atomicAdd(&dst[cls], (unsigned long long)cnt);
