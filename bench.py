@@ -30,19 +30,38 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 READ_LEN = 150
 STRIDE = 160
 SEED = 20261015
-WORKLOAD = "C3: synthetic PE 2x150bp, -q -a --detect_pe_adapter -g (BASELINE.json configs[2])"
+WORKLOADS = {
+    "C2": "C2: synthetic SE 150bp, -q (BASELINE.json configs[1])",
+    "C3": "C3: synthetic PE 2x150bp, -q -a --detect_pe_adapter -g (BASELINE.json configs[2])",
+    "C4": "C4: synthetic PE 2x150bp, -q -a -g --enable_cut_right -m (BASELINE.json configs[3])",
+    "C5": "C5: synthetic PE 2x150bp, -q -a -g -x --enable_cut_right (BASELINE.json configs[4], per GPU)",
+}
+WORKLOAD = WORKLOADS["C3"]
 
 
 def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def c3_params(abi, max_cycles=256):
-    p = abi.default_params(paired=True, max_cycles=max_cycles)
+def config_params(abi, name, max_cycles=256):
+    """Engine parameters of a BASELINE config (what the tool derives from its command line)."""
+    p = abi.default_params(paired=name != "C2", max_cycles=max_cycles)
     p.qual_filter_enabled = 1
-    p.adapter_trimming = 1
-    p.polyg_enabled = 1
+    if name in ("C3", "C4", "C5"):
+        p.adapter_trimming = 1
+        p.polyg_enabled = 1
+    if name in ("C4", "C5"):
+        p.cut_right = 1
+    if name == "C4":
+        p.merge_enabled = 1
+        p.max_cycles = max(max_cycles, 320)  # merged reads reach len1 + len2
+    if name == "C5":
+        p.polyx_enabled = 1
     return p
+
+
+def c3_params(abi, max_cycles=256):
+    return config_params(abi, "C3", max_cycles)
 
 
 def write_fastq_pair(seq1, qual1, seq2, qual2, first_index, d):
@@ -126,6 +145,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=100_000_000, help="pairs per GPU (BASELINE: 100 M)")
     ap.add_argument("--cpu-pairs", type=int, default=1_000_000, help="CPU-baseline sample size (pairs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS),
+                    help="workload (BASELINE.json configs); the headline metric is C3")
     args = ap.parse_args()
 
     import torch
@@ -146,7 +167,8 @@ def main():
     dev = torch.device("cuda", local)
 
     lib = abi.load_engine()
-    p = c3_params(abi)
+    p = config_params(abi, args.config)
+    paired = bool(p.paired)
     h = ctypes.c_void_p()
     if lib.fq_engine_create(ctypes.byref(p), local, 0, 0, ctypes.byref(h)) != 0:
         raise SystemExit("fq_engine_create: " + lib.fq_engine_last_error(None).decode())
@@ -163,6 +185,8 @@ def main():
     b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
     b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
     stream = torch.cuda.current_stream(dev)
+    sb = abi.FqBatch()  # single-end view (C2): read 1 planes only
+    sb.n, sb.stride, sb.seq1, sb.qual1, sb.len1 = b.n, b.stride, b.seq1, b.qual1, b.len1
     t0 = time.time()
     assert lib.fq_synth_fill_device(ctypes.byref(b), SEED, first, READ_LEN, ctypes.c_void_p(stream.cuda_stream)) == 0
     torch.cuda.synchronize(dev)
@@ -172,7 +196,8 @@ def main():
         acc.zero_()
         if ev:
             ev[0].record(stream)
-        rc = lib.fq_engine_process_device(h, ctypes.byref(b), results.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+        rc = lib.fq_engine_process_device(h, ctypes.byref(b if paired else sb), results.data_ptr(),
+                                          ctypes.c_void_p(stream.cuda_stream))
         if rc != 0:
             raise RuntimeError(lib.fq_engine_last_error(h).decode())
         if ev:
@@ -205,17 +230,17 @@ def main():
 
     acc_host = acc.cpu().numpy().view("uint64")
     total_pairs = n * world
-    reads = 2 * total_pairs
-    # sanity: every pair was counted by the pre-filter stats
+    reads = (2 if paired else 1) * total_pairs
+    # sanity: every pair (read) was counted by the pre-filter stats and by FilterResult
     st0 = abi.acc_stats_offset(p.insert_size_max, p.max_cycles, 0)
     assert int(acc_host[st0 + abi.FQ_ST_READS]) == total_pairs, "accumulator lost pairs"
     assert int(acc_host[abi.FQ_ACC_FILTER:abi.FQ_ACC_FILTER + 32].sum()) == reads
 
     value = reads * args.steps / elapsed / 1e6
-    bytes_per_pair = 2 * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result record per read
+    bytes_per_pair = (2 if paired else 1) * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result per read
     achieved = n * bytes_per_pair / (kavg / 1e3) / 1e9
     out = {
-        "metric": "Mreads/s (150 bp PE, q+adapter+polyG)",
+        "metric": "Mreads/s (150 bp PE, q+adapter+polyG)" if args.config == "C3" else f"Mreads/s ({args.config})",
         "value": round(value, 2),
         "unit": "Mreads/s",
         "n_gpus": world,
@@ -227,14 +252,14 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded counter-based generator in HBM, SURVEY.md 8(d))",
-        "config": {"workload": WORKLOAD, "pairs_per_gpu": n, "read_len": READ_LEN, "row_stride": STRIDE,
+        "config": {"workload": WORKLOADS[args.config], ("pairs_per_gpu" if paired else "reads_per_gpu"): n, "read_len": READ_LEN, "row_stride": STRIDE,
                    "parallelism": f"dp{world} (pairs sharded, RCCL sum of the accumulator block)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel_ms_avg": round(kavg, 3), "bytes_per_pair": bytes_per_pair},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C3":
         del bufs, lens, results
         torch.cuda.empty_cache()
         log(f"CPU baseline on {args.cpu_pairs} pairs ...")

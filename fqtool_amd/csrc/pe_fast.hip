@@ -44,8 +44,15 @@ constexpr int kMaxLen = 160;
 constexpr int kChunks = kMaxLen / 16;             // 16-position chunks per read
 constexpr int kFC = 0;                            // column fields (words): 2-bit codes,
 constexpr int kFN = kChunks;                      //   spaced N mask,
-constexpr int kWaveW = 2 * kChunks * 64;          // code + N columns of a wave
-constexpr int kBlocksPerCU = 2;                   // 16 waves per CU: LDS and VGPRs sized for it
+constexpr int kCodeW = 2 * kChunks * 64;          // code + N columns of a wave
+constexpr int kQS = kMaxLen / 4 + 1;              // quality row stride (odd: conflict-free per lane)
+// LEAN keeps qualities in HBM/L2 (2 workgroups = 16 waves per CU); the full variant, whose
+// trimming windows read qualities at random, stages them in LDS rows (1 workgroup per CU).
+template <bool LEAN>
+struct Layout {
+    static constexpr int kBlocksPerCU = LEAN ? 2 : 1;
+    static constexpr int kWaveW = kCodeW + (LEAN ? 0 : 64 * kQS);
+};
 // Stats histograms: u64 cells [cycle / 16][slot][cycle % 16], slots A C T G N + one dummy slot
 // that absorbs masked-off positions.  A cell's LDS bank pair depends only on cycle % 16, so the
 // 16 lanes of an atomic's lane group (distinct cycle % 16 by the per-lane rotation) never
@@ -59,10 +66,15 @@ constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
 constexpr int kScalCopies = 16;  // per-read scalars are spread over 16 copies (lane & 15)
 constexpr int kScalW = 2 * 16 * kScalCopies;  // [copy][4 stats][reads, length_sum, q20, q30] u64
 constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
-constexpr int kColsW = kWaves * kWaveW;
-constexpr int kLdsWords = kColsW + 4 * kHistW + kSmallW + kScalW + kAdW;
-static_assert(kLdsWords * 4 * kBlocksPerCU <= 160 * 1024, "LDS budget");
-static_assert((kColsW & 1) == 0 && (kHistW & 1) == 0, "u64 cells must stay 8-byte aligned");
+template <bool LEAN>
+constexpr int cols_words() { return kWaves * Layout<LEAN>::kWaveW; }
+constexpr int kTailW = 4 * kHistW + kSmallW + kScalW + kAdW;  // after the wave columns
+template <bool LEAN>
+constexpr int lds_words() { return cols_words<LEAN>() + kTailW; }
+static_assert(lds_words<true>() * 4 * Layout<true>::kBlocksPerCU <= 160 * 1024, "LDS budget");
+static_assert(lds_words<false>() * 4 * Layout<false>::kBlocksPerCU <= 160 * 1024, "LDS budget");
+static_assert((cols_words<true>() & 1) == 0 && (cols_words<false>() & 1) == 0 && (kHistW & 1) == 0,
+              "u64 cells must stay 8-byte aligned");
 
 constexpr unsigned long long kCount1 = 1ull << 40;
 constexpr unsigned long long kQMask = kCount1 - 1;
@@ -123,6 +135,11 @@ __device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool
     }
     return Fwd{cw, nw};
 }
+
+struct LdsQual {  // forward quality byte i of a lane's LDS quality row
+    const uint32_t* row;
+    __device__ __forceinline__ int operator()(int i) const { return (int)((row[i >> 2] >> ((i & 3) * 8)) & 0xFFu); }
+};
 
 struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N)
     const uint32_t* col;
@@ -274,13 +291,14 @@ __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) &
 // sequences, maxLen or low-complexity filter), instantiated separately so the hot loop carries
 // neither their code nor their parameters.
 template <bool LEAN>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 * kBlocksPerCU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 * Layout<LEAN>::kBlocksPerCU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t* col = lds + wave * kWaveW;  // code / N columns: word field*64 + lane
-    uint32_t* hist = lds + kColsW;  // [pre1, pre2, post1, post2] x kHistW
+    uint32_t* col = lds + wave * Layout<LEAN>::kWaveW;  // code / N columns: word field*64 + lane
+    uint32_t* qrows = col + kCodeW;                    // full variant: quality rows, row = lane
+    uint32_t* hist = lds + cols_words<LEAN>();         // [pre1, pre2, post1, post2] x kHistW
     unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + 4 * kHistW);
     unsigned long long* scal = small + kSmallW / 2;
     uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16 * kScalCopies);
@@ -333,6 +351,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         uint32_t* my_pre = hist + mate * kHistW;
         uint32_t* my_post = hist + (2 + mate) * kHistW;  // post block, or the "removed" block (see below)
         const int r = lane_x & 15;  // stats rotation within a chunk
+        uint32_t* qrow = qrows + lane_x * kQS;
         const int idx = t * 32 + pl;
         const bool valid = idx < b.n;
         const int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
@@ -341,6 +360,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         const size_t roff = (size_t)(valid ? idx : 0) * b.stride;
         const uint8_t* S = (mate ? b.seq2 : b.seq1) + roff;
         const uint8_t* Q = (mate ? b.qual2 : b.qual1) + roff;
+        // quality chunk F of this lane's row: from the LDS row (full) or the row in L2 (LEAN)
+        auto qchunk = [&](int F) -> uint4 {
+            if (LEAN) return *reinterpret_cast<const uint4*>(Q + 16 * F);
+            return make_uint4(qrow[4 * F], qrow[4 * F + 1], qrow[4 * F + 2], qrow[4 * F + 3]);
+        };
         const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4);
         uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0, lowf = 0, tqf = 0, nbf = 0;  // whole-read sums
         // column word of chunk k: k for read 1, 9-k for read 2 (stepped, not precomputed, so the
@@ -375,6 +399,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 const bool full = __all(L >= 16 * k + 16);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
+                    if (!LEAN) qrow[4 * k + j] = qw[j];
                     const uint32_t bm = full ? 0xFFFFFFFFu : bytemask(L - (16 * k + 4 * j));
                     const uint32_t kk = (sw[j] >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
@@ -416,7 +441,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 
         FQ_STAMP(0)
         const CodeSeq seq{col, lane, rc};
-        const PtrQual qual{Q};  // trimAndCut windows read the row in HBM/L2 (only with cut options)
+        const LdsQual qual{qrow};  // trimAndCut windows (full variant only)
 
         // ---------------- trimAndCut (src/peprocessor.cpp:292-293) ----------------
         int st = 0, n = 0;
@@ -555,9 +580,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     const int a0 = part ? end : 0, a1 = part ? L : st;  // forward range [a0, a1)
                     const int F0 = a0 >> 4, F1 = (a1 + 15) >> 4;
                     // row chunks come from L2; the next one is requested before this one is used
-                    uint4 cur = *reinterpret_cast<const uint4*>(Q + 16 * min(F0, nchunks - 1));
+                    uint4 cur = qchunk(min(F0, nchunks - 1));
                     for (int F = F0; F < F1; ++F) {
-                        const uint4 nxt = *reinterpret_cast<const uint4*>(Q + 16 * min(F + 1, nchunks - 1));
+                        const uint4 nxt = qchunk(min(F + 1, nchunks - 1));
                         const uint32_t wq[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
@@ -601,13 +626,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             // chunk F+1's codes (LDS) and the qualities of chunks F+1, F+2 (the row again, now from
             // L2) are in flight while chunk F's atomics issue
             Fwd fn = fwd_chunk(col, lane_x, 0, rc);
-            uint4 qn = *reinterpret_cast<const uint4*>(Q);
-            uint4 qnn = *reinterpret_cast<const uint4*>(Q + 16 * min(1, nchunks - 1));
+            uint4 qn = qchunk(0);
+            uint4 qnn = qchunk(min(1, nchunks - 1));
             for (int F = 0; F < nchl; ++F) {
                 const Fwd f = fn;
                 const uint32_t q0 = qn.x, q1 = qn.y, q2 = qn.z, q3 = qn.w;
                 qn = qnn;
-                qnn = *reinterpret_cast<const uint4*>(Q + 16 * min(F + 2, nchunks - 1));
+                qnn = qchunk(min(F + 2, nchunks - 1));
                 fn = fwd_chunk(col, lane_x, min(F + 1, nchunks - 1), rc);
                 // rotate the chunk by r positions: position t of the rotated view is 16F + (t+r)%16
                 const uint32_t cr = __builtin_amdgcn_alignbit(f.c, f.c, 2 * r);
@@ -726,10 +751,10 @@ extern "C" __attribute__((visibility("default"))) int fq_debug_phase_cycles(unsi
 
 hipError_t fq_pe_fast_prepare() {
     hipError_t e = hipFuncSetAttribute((const void*)pe_fast_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       kLdsWords * 4);
+                                       lds_words<true>() * 4);
     if (e != hipSuccess) return e;
     return hipFuncSetAttribute((const void*)pe_fast_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               kLdsWords * 4);
+                               lds_words<false>() * 4);
 }
 
 hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
@@ -738,10 +763,10 @@ hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_resu
                       !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
                       p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled;
     if (lean)
-        hipLaunchKernelGGL(pe_fast_kernel<true>, dim3(grid * kBlocksPerCU), dim3(kBlock), kLdsWords * 4, stream, p, b, res,
-                           acc, slow_tiles, slow_count);
+        hipLaunchKernelGGL(pe_fast_kernel<true>, dim3(grid * Layout<true>::kBlocksPerCU), dim3(kBlock),
+                           lds_words<true>() * 4, stream, p, b, res, acc, slow_tiles, slow_count);
     else
-        hipLaunchKernelGGL(pe_fast_kernel<false>, dim3(grid * kBlocksPerCU), dim3(kBlock), kLdsWords * 4, stream, p, b,
-                           res, acc, slow_tiles, slow_count);
+        hipLaunchKernelGGL(pe_fast_kernel<false>, dim3(grid * Layout<false>::kBlocksPerCU), dim3(kBlock),
+                           lds_words<false>() * 4, stream, p, b, res, acc, slow_tiles, slow_count);
     return hipGetLastError();
 }
