@@ -71,6 +71,10 @@ struct PtrQual {
     const uint8_t* p;
     __device__ __forceinline__ int operator()(int i) const { return (int)(int8_t)p[i]; }
 };
+struct LdsQual {  // quality byte i (signed, as the reference's char) of a row packed 4 per LDS word
+    const uint32_t* row;
+    __device__ __forceinline__ int operator()(int i) const { return (int)(int8_t)(row[i >> 2] >> ((i & 3) * 8)); }
+};
 struct Bytes {
     const uint8_t* p;
     __device__ __forceinline__ uint8_t operator()(int i) const { return p[i]; }
@@ -109,6 +113,57 @@ __device__ inline int pass_filter_t(const fq_params& p, SQ seq, QQ qual, int rle
 // Filter::trimAndCut are evaluated exactly in integers.
 __device__ __forceinline__ bool win_ge(int total, int w, int x) { return total >= x * w; }
 
+// The forward sliding-window scans of Filter::trimAndCut (cut_front src/filter.cpp:93-122, cut_right
+// :124-152): the first s in [s0, send) whose window sum q[s..s+w-1] satisfies (sum >= T) == WANT,
+// or send when there is none.
+template <bool WANT, class QQ>
+__device__ inline int window_scan(QQ qual, int s0, int send, int w, int T) {
+    int tot = 0;
+    for (int i = 0; i < w - 1; ++i) tot += qual(s0 + i);
+    int s = s0;
+    for (; s < send; ++s) {
+        tot += qual(s + w - 1);
+        if (s > s0) tot -= qual(s - 1);
+        if (win_ge(tot, w, T) == WANT) break;
+    }
+    return s;
+}
+
+// The same scan over an LDS row, 4 positions per step: the added (q[s+w-1]) and removed (q[s-1])
+// bytes arrive as words realigned with v_alignbyte, one LDS word per stream per step, prefetched
+// one step ahead (the byte loop waits out the LDS latency at every position).
+template <bool WANT>
+__device__ inline int window_scan(LdsQual qual, int s0, int send, int w, int T) {
+    if (s0 >= send) return send;
+    const int TW = T * w;
+    int tot = 0;
+    for (int i = 0; i < w; ++i) tot += qual(s0 + i);
+    if ((tot >= TW) == WANT) return s0;
+    const uint32_t* row = qual.row;
+    int oa = s0 + w, orr = s0;  // byte offsets of q[s+w-1] and q[s-1] for s = s0 + 1
+    const uint32_t sha = oa & 3, shr = orr & 3;
+    const uint32_t* pa = row + (oa >> 2);
+    const uint32_t* pr = row + (orr >> 2);
+    uint32_t alo = pa[0], ahi = pa[1], rlo = pr[0], rhi = pr[1];
+    for (int s = s0 + 1; s < send; s += 4) {
+        const uint32_t an = pa[2], rn = pr[2];
+        const uint32_t aw = __builtin_amdgcn_alignbyte(ahi, alo, sha);
+        const uint32_t rw = __builtin_amdgcn_alignbyte(rhi, rlo, shr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            tot += ((int)(aw << (24 - 8 * k)) >> 24) - ((int)(rw << (24 - 8 * k)) >> 24);
+            if (s + k < send && (tot >= TW) == WANT) return s + k;
+        }
+        alo = ahi;
+        ahi = an;
+        rlo = rhi;
+        rhi = rn;
+        ++pa;
+        ++pr;
+    }
+    return send;
+}
+
 // Filter::trimAndCut, reference src/filter.cpp:69-189. Returns false for NULL.
 template <class SQ, class QQ>
 __device__ inline bool trim_and_cut_t(const fq_params& p, SQ seq, QQ qual, int l, int front, int tail,
@@ -128,15 +183,8 @@ __device__ inline bool trim_and_cut_t(const fq_params& p, SQ seq, QQ qual, int l
     }
     if (enF) {
         const int w = p.cut_front_window, thr = 33 + p.cut_front_quality;
-        int s = front;
         if (l - front - tail - w <= 0) return false;
-        int tot = 0;
-        for (int i = 0; i < w - 1; ++i) tot += qual(s + i);
-        for (s = front; s + w < l - tail; ++s) {
-            tot += qual(s + w - 1);
-            if (s > front) tot -= qual(s - 1);
-            if (win_ge(tot, w, thr)) break;
-        }
+        int s = window_scan<true>(qual, front, l - tail - w, w, thr);
         if (s > 0) s = s + w - 1;
         while (s < l && seq(s) == 'N') ++s;
         front = s;
@@ -144,20 +192,9 @@ __device__ inline bool trim_and_cut_t(const fq_params& p, SQ seq, QQ qual, int l
     }
     if (enR) {
         const int w = p.cut_right_window, thr = 33 + p.cut_right_quality;
-        int s = front;
         if (l - front - tail - w <= 0) return false;
-        int tot = 0;
-        bool found = false;
-        for (int i = 0; i < w - 1; ++i) tot += qual(s + i);
-        for (s = front; s + w < l - tail; ++s) {
-            tot += qual(s + w - 1);
-            if (s > front) tot -= qual(s - 1);
-            if (!win_ge(tot, w, thr)) {
-                found = true;
-                break;
-            }
-        }
-        if (found) {
+        int s = window_scan<false>(qual, front, l - tail - w, w, thr);
+        if (s < l - tail - w) {
             while (s < l - 1 && qual(s) >= thr) ++s;
             rlen = s - front;
         }

@@ -136,11 +136,6 @@ __device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool
     return Fwd{cw, nw};
 }
 
-struct LdsQual {  // forward quality byte i of a lane's LDS quality row
-    const uint32_t* row;
-    __device__ __forceinline__ int operator()(int i) const { return (int)((row[i >> 2] >> ((i & 3) * 8)) & 0xFFu); }
-};
-
 struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N)
     const uint32_t* col;
     int c;

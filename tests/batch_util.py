@@ -157,12 +157,23 @@ def config(name, max_cycles=256):
         p.length_filter_enabled, p.min_len, p.max_len = 1, 20, 100
         p.complexity_enabled = 1
         p.low_qual_base_limit = 10
+    elif name.startswith("PE_cutR"):  # cut_right alone (removed-mode stats), window w
+        w = int(name[7:])
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.cut_right, p.cut_right_window, p.cut_right_quality = 1, w, 30
+    elif name.startswith("PE_cut"):  # both forward window scans from unaligned starts, window w
+        w = int(name[6:])
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.cut_front, p.cut_front_window, p.cut_front_quality = 1, max(1, w // 2), 15
+        p.cut_right, p.cut_right_window, p.cut_right_quality = 1, w, 28
+        p.trim_front1, p.trim_front2 = 1, 3
     else:
         raise KeyError(name)
     return p
 
 
-ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all"]
+ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
+               "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR5"]
 
 
 def run_oracle(oracle, p, pk):

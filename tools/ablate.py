@@ -19,7 +19,7 @@ torch.cuda.synchronize()
 variants = [("full", 0), ("no_overlap", 1), ("no_filter", 2), ("no_stats", 4), ("no_polyg", 8),
             ("no_lds_atomics", 16), ("no_overlap_filter_stats", 7), ("stage_only", 15)]
 results = {}
-for rep in range(3):
+for rep in range(3 if os.environ.get("CONFIG", "C3") == "C3" else 0):
     for name, bits in variants:
         p = abi.default_params(True, 256); p.qual_filter_enabled = 1; p.adapter_trimming = 1; p.polyg_enabled = 1
         p.reserved[0] = bits
@@ -29,13 +29,14 @@ for rep in range(3):
         ms = lib.fq_engine_last_kernel_ms(h)
         results.setdefault(name, []).append(ms)
         lib.fq_engine_destroy(h)
-for name, _ in variants:
+for name in results:
     v = sorted(results[name])
     print(f"{name:28s} median {v[len(v)//2]:8.2f} ms  min {v[0]:8.2f}  -> {n / (v[len(v)//2] / 1e3) / 1e9:.2f} G pairs/s", flush=True)
 
 # per-phase wave cycles (fq_params.reserved[1] = 1)
 names = ["staging", "trim", "polyG", "overlap", "polyX/maxlen", "filter", "stats", "store"]
-p = abi.default_params(True, 256); p.qual_filter_enabled = 1; p.adapter_trimming = 1; p.polyg_enabled = 1
+from bench import config_params
+p = config_params(abi, os.environ.get("CONFIG", "C3"))
 p.reserved[1] = 1
 h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
 lib.fq_debug_phase_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
