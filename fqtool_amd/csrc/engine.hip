@@ -159,7 +159,7 @@ static int grid_for(const fq_engine* e, int n) {
 static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStream_t s) {
     if (db.n <= 0) return FQ_OK;
     if (e->fast) {
-        const size_t ntiles = ((size_t)db.n + 31) / 32;
+        const size_t ntiles = ((size_t)db.n + 31) / 32 + 1;  // single-end 64-read tiles enter as two
         if (ntiles > e->slow_cap) {
             HIP_TRY(e, hipStreamSynchronize(s));
             if (e->slow_tiles) HIP_TRY(e, hipFree(e->slow_tiles));

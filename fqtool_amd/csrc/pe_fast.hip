@@ -285,7 +285,10 @@ __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) &
 // LEAN: the option set of the headline workloads (no trimming/cutting windows, polyX, adapter
 // sequences, maxLen or low-complexity filter), instantiated separately so the hot loop carries
 // neither their code nor their parameters.
-template <bool LEAN>
+// PAIRED: a tile is 32 pairs, lanes l and l+32 holding the two mates of a pair (read 2's column
+// reverse-complemented for the overlap scan); single-end: a tile is 64 reads, one per lane, with
+// SingleEndProcessor::processSingleEnd's order (src/seprocessor.cpp:290-360).
+template <bool LEAN, bool PAIRED>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 * Layout<LEAN>::kBlocksPerCU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
@@ -305,7 +308,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
     // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics
     const int abl = p.reserved[0];
-    const int ntiles = (b.n + 31) >> 5;
+    const int ntiles = PAIRED ? (b.n + 31) >> 5 : (b.n + 63) >> 6;
     const int nchunks = min(kChunks, b.stride >> 4);
     const int limit = p.overlap_diff_limit;
     const int K = max(limit, 1);
@@ -335,9 +338,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         // itself the compiler hoists dozens of them out of the tile loop and spills them.
         int lane_x = lane;
         asm volatile("" : "+v"(lane_x));
-        const int mate = lane_x >> 5, pl = lane_x & 31;
+        const int mate = PAIRED ? lane_x >> 5 : 0, pl = lane_x & 31;
         const int mlane = lane_x ^ 32;
-        const bool rc = mate == 1;
+        const bool rc = PAIRED && mate == 1;
         const int front = mate ? p.trim_front2 : p.trim_front1;
         const int tail = mate ? p.trim_tail2 : p.trim_tail1;
         const uint8_t* my_ad = adp + (mate ? FQ_MAX_ADAPTER : 0);
@@ -347,7 +350,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         uint32_t* my_post = hist + (2 + mate) * kHistW;  // post block, or the "removed" block (see below)
         const int r = lane_x & 15;  // stats rotation within a chunk
         uint32_t* qrow = qrows + lane_x * kQS;
-        const int idx = t * 32 + pl;
+        const int idx = PAIRED ? t * 32 + pl : t * 64 + lane_x;
         const bool valid = idx < b.n;
         const int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
 
@@ -422,7 +425,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         }
         const bool bad = odd || exo != 0 || (qhi & 0x80808080u) != 0;
         if (__any(bad)) {
-            if (lane == 0) slow_tiles[atomicAdd(slow_count, 1)] = t;
+            if (lane == 0) {  // the general kernel takes 32-read (single-end) / 32-pair tiles
+                if (PAIRED) {
+                    slow_tiles[atomicAdd(slow_count, 1)] = t;
+                } else {
+                    const int k = atomicAdd(slow_count, 2);
+                    slow_tiles[k] = 2 * t;
+                    slow_tiles[k + 1] = 2 * t + 1;
+                }
+            }
             continue;
         }
         for (int k = nchunks; k < kChunks; ++k) {  // unused tail of the row
@@ -449,7 +460,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         }
         // the shuffle must run in every lane: ds_bpermute from a lane that is switched off returns
         // whatever its register held before (e.g. the previous tile's value)
-        const int nn_o = __shfl_xor(nn ? 1 : 0, 32);
+        const int nn_o = PAIRED ? __shfl_xor(nn ? 1 : 0, 32) : 1;
         const bool both = nn && nn_o != 0;
         fq_read_result rr;
         rr.flags = nn ? 0 : FQ_RF_NULL;
@@ -468,8 +479,31 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         }
 
         FQ_STAMP(2)
+        // AdapterTrimmer::trimBySequence, src/adaptertrimmer.cpp:29-90
+        auto by_sequence = [&]() {
+            int pos;
+            if (trim_by_sequence_t(at(seq, st), n, my_ad, my_alen, pos)) {
+                int ad_len;
+                if (pos < 0) {
+                    ad_len = my_alen + pos;
+                    rr.flags |= FQ_RF_AD_SEQ | FQ_RF_AD_NEG;
+                    rr.ad_pos = (uint16_t)(-pos);
+                    n = 0;
+                } else {
+                    ad_len = n - pos;
+                    rr.flags |= FQ_RF_AD_SEQ;
+                    rr.ad_pos = (uint16_t)(st + pos);
+                    n = pos;
+                }
+                rr.ad_len = (uint16_t)ad_len;
+                if (ad_len > 0) {
+                    sadd(&small[FQ_ACC_ADAPTER_READS], 1ull);
+                    sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)ad_len);
+                }
+            }
+        };
         // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
-        if (both && !(abl & 1)) {
+        if (PAIRED && both && !(abl & 1)) {
             const int st_o = __shfl_xor(st, 32), n_o = __shfl_xor(n, 32);
             const int st1 = mate ? st_o : st, n1 = mate ? n_o : n;
             const int st2 = mate ? st : st_o, n2 = mate ? n : n_o;
@@ -519,30 +553,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                         sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)((n1 - ol) + (n2 - ol)));
                     }
                     n = ol;
-                } else if (!LEAN && my_alen > 0) {  // AdapterTrimmer::trimBySequence, src/adaptertrimmer.cpp:29-90
-                    int pos;
-                    if (trim_by_sequence_t(at(seq, st), n, my_ad, my_alen, pos)) {
-                        int ad_len;
-                        if (pos < 0) {
-                            ad_len = my_alen + pos;
-                            rr.flags |= FQ_RF_AD_SEQ | FQ_RF_AD_NEG;
-                            rr.ad_pos = (uint16_t)(-pos);
-                            n = 0;
-                        } else {
-                            ad_len = n - pos;
-                            rr.flags |= FQ_RF_AD_SEQ;
-                            rr.ad_pos = (uint16_t)(st + pos);
-                            n = pos;
-                        }
-                        rr.ad_len = (uint16_t)ad_len;
-                        if (ad_len > 0) {
-                            sadd(&small[FQ_ACC_ADAPTER_READS], 1ull);
-                            sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)ad_len);
-                        }
-                    }
+                } else if (!LEAN && my_alen > 0) {
+                    by_sequence();
                 }
             }
         }
+        if (!PAIRED && !LEAN && nn && p.adapter_trimming && my_alen > 0) by_sequence();  // src/seprocessor.cpp:320-323
 
         FQ_STAMP(3)
         // ---------------- polyX, maxLen (src/peprocessor.cpp:335-349) ----------------
@@ -608,9 +624,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 return diff;
             });
         }
-        const int code_o = __shfl_xor(code, 32);
+        const int code_o = PAIRED ? __shfl_xor(code, 32) : code;
         const bool pair_pass = both && code == FQ_PASS_FILTER && code_o == FQ_PASS_FILTER;
-        if (mate == 0 && valid) sadd(&small[FQ_ACC_FILTER + max(code, code_o)], 2ull);  // addFilterResult: +2
+        if (PAIRED) {
+            if (mate == 0 && valid) sadd(&small[FQ_ACC_FILTER + max(code, code_o)], 2ull);  // addFilterResult: +2
+        } else if (valid) {
+            sadd(&small[FQ_ACC_FILTER + code], 1ull);  // src/seprocessor.cpp:339
+        }
 
         FQ_STAMP(5)
         // ---------------- Stats::statRead, pre and post (src/peprocessor.cpp:276-277,400-401) ----
@@ -680,7 +700,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             rr.start = nn ? (uint16_t)st : 0;
             rr.len = nn ? (uint16_t)n : 0;
             rr.code = (uint8_t)code;
-            if (res) *reinterpret_cast<uint4*>(&res[2 * (size_t)idx + mate]) = *reinterpret_cast<const uint4*>(&rr);
+            if (res)
+                *reinterpret_cast<uint4*>(&res[PAIRED ? 2 * (size_t)idx + mate : (size_t)idx]) =
+                    *reinterpret_cast<const uint4*>(&rr);
         }
     }
 
@@ -731,7 +753,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 }  // namespace
 
 bool fq_pe_fast_supported(const fq_params& p) {
-    return p.paired && !p.merge_enabled && p.insert_size_max <= 512 && p.insert_size_max >= 0;
+    return !p.merge_enabled && p.insert_size_max <= 512 && p.insert_size_max >= 0;
 }
 
 // profiling aid (tools/ablate.py --phases): read and clear the per-phase cycle totals
@@ -745,11 +767,14 @@ extern "C" __attribute__((visibility("default"))) int fq_debug_phase_cycles(unsi
 }
 
 hipError_t fq_pe_fast_prepare() {
-    hipError_t e = hipFuncSetAttribute((const void*)pe_fast_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       lds_words<true>() * 4);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)pe_fast_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               lds_words<false>() * 4);
+    const void* k[4] = {(const void*)pe_fast_kernel<true, true>, (const void*)pe_fast_kernel<false, true>,
+                        (const void*)pe_fast_kernel<true, false>, (const void*)pe_fast_kernel<false, false>};
+    for (int i = 0; i < 4; ++i) {
+        const int words = (i & 1) ? lds_words<false>() : lds_words<true>();
+        hipError_t e = hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, words * 4);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
@@ -757,11 +782,19 @@ hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_resu
     const bool lean = p.trim_front1 == 0 && p.trim_tail1 == 0 && p.trim_front2 == 0 && p.trim_tail2 == 0 &&
                       !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
                       p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled;
-    if (lean)
-        hipLaunchKernelGGL(pe_fast_kernel<true>, dim3(grid * Layout<true>::kBlocksPerCU), dim3(kBlock),
-                           lds_words<true>() * 4, stream, p, b, res, acc, slow_tiles, slow_count);
+    const dim3 gl(grid * Layout<true>::kBlocksPerCU), gf(grid * Layout<false>::kBlocksPerCU);
+    const size_t ll = lds_words<true>() * 4, lf = lds_words<false>() * 4;
+    if (p.paired && lean)
+        hipLaunchKernelGGL((pe_fast_kernel<true, true>), gl, dim3(kBlock), ll, stream, p, b, res, acc, slow_tiles,
+                           slow_count);
+    else if (p.paired)
+        hipLaunchKernelGGL((pe_fast_kernel<false, true>), gf, dim3(kBlock), lf, stream, p, b, res, acc, slow_tiles,
+                           slow_count);
+    else if (lean)
+        hipLaunchKernelGGL((pe_fast_kernel<true, false>), gl, dim3(kBlock), ll, stream, p, b, res, acc, slow_tiles,
+                           slow_count);
     else
-        hipLaunchKernelGGL(pe_fast_kernel<false>, dim3(grid * Layout<false>::kBlocksPerCU), dim3(kBlock),
-                           lds_words<false>() * 4, stream, p, b, res, acc, slow_tiles, slow_count);
+        hipLaunchKernelGGL((pe_fast_kernel<false, false>), gf, dim3(kBlock), lf, stream, p, b, res, acc, slow_tiles,
+                           slow_count);
     return hipGetLastError();
 }

@@ -78,23 +78,26 @@ def test_edge_case_parity(eng_lib, oracle, name, mode):
     assert_same(p, res_o, acc_o, res_e, acc_e)
 
 
-@pytest.mark.parametrize("name", ["C3", "C3b", "C5", "PE_all"])
+@pytest.mark.parametrize("name", ["C3", "C3b", "C5", "PE_all", "C2", "SE_all"])
 def test_mixed_fast_and_handoff_tiles(eng_lib, oracle, name):
     """Mostly clean synthetic tiles plus scattered tiles with IUPAC bases, quality bytes >= 128
     and over-long reads: the fast kernel hands those tiles to the general kernel."""
     p = config(name, max_cycles=512)
-    pk = synth_pack(oracle, 8000, True, first=555, stride=176)
+    paired = bool(p.paired)
+    n = 8001 if paired else 8033  # a ragged last tile
+    pk = synth_pack(oracle, n, paired, first=555, stride=176)
     rng = np.random.default_rng(3)
-    for i in rng.choice(8000, 40, replace=False):
+    m2 = (pk.seq2, pk.qual2, pk.len2) if paired else (pk.seq1, pk.qual1, pk.len1)
+    for i in rng.choice(n, 40, replace=False):
         kind = i % 3
         if kind == 0:
             pk.seq1[i, rng.integers(0, 150)] = ord("R")
         elif kind == 1:
-            pk.qual2[i, rng.integers(0, 150)] = 200
+            m2[1][i, rng.integers(0, 150)] = 200
         else:
-            pk.seq2[i, 150:170] = ord("A")
-            pk.qual2[i, 150:170] = ord("I")
-            pk.len2[i] = 170
+            m2[0][i, 150:170] = ord("A")
+            m2[1][i, 150:170] = ord("I")
+            m2[2][i] = 170
     res_o, acc_o = run_oracle(oracle, p, pk)
     res_e, acc_e = run_engine(eng_lib, p, pk)
     assert_same(p, res_o, acc_o, res_e, acc_e)

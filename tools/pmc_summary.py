@@ -21,7 +21,7 @@ def main(root):
         for (d, c), v in per.items():
             acc[names[d]][c].append(v)
     for k, cs in acc.items():
-        short = k.split("(")[0][:80]
+        short = k.replace("(anonymous namespace)::", "").split("(")[0][:80]
         print(short)
         for c, vs in sorted(cs.items()):
             print(f"    {c:28s} mean {sum(vs) / len(vs):16.4g}   n={len(vs)}")
