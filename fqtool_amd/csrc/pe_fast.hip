@@ -38,21 +38,13 @@ using namespace fqdev;
 
 namespace {
 
-constexpr int kWaves = 8;
-constexpr int kBlock = 64 * kWaves;
+constexpr int kBlock = 512;  // launch bound: 8 waves (7 in the merge variant)
 constexpr int kMaxLen = 160;
 constexpr int kChunks = kMaxLen / 16;             // 16-position chunks per read
 constexpr int kFC = 0;                            // column fields (words): 2-bit codes,
 constexpr int kFN = kChunks;                      //   spaced N mask,
 constexpr int kCodeW = 2 * kChunks * 64;          // code + N columns of a wave
 constexpr int kQS = kMaxLen / 4 + 1;              // quality row stride (odd: conflict-free per lane)
-// LEAN keeps qualities in HBM/L2 (2 workgroups = 16 waves per CU); the full variant, whose
-// trimming windows read qualities at random, stages them in LDS rows (1 workgroup per CU).
-template <bool LEAN>
-struct Layout {
-    static constexpr int kBlocksPerCU = LEAN ? 2 : 1;
-    static constexpr int kWaveW = kCodeW + (LEAN ? 0 : 64 * kQS);
-};
 // Stats histograms: u64 cells [cycle / 16][slot][cycle % 16], slots A C T G N + one dummy slot
 // that absorbs masked-off positions.  A cell's LDS bank pair depends only on cycle % 16, so the
 // 16 lanes of an atomic's lane group (distinct cycle % 16 by the per-lane rotation) never
@@ -66,15 +58,23 @@ constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
 constexpr int kScalCopies = 16;  // per-read scalars are spread over 16 copies (lane & 15)
 constexpr int kScalW = 2 * 16 * kScalCopies;  // [copy][4 stats][reads, length_sum, q20, q30] u64
 constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
-template <bool LEAN>
-constexpr int cols_words() { return kWaves * Layout<LEAN>::kWaveW; }
-constexpr int kTailW = 4 * kHistW + kSmallW + kScalW + kAdW;  // after the wave columns
-template <bool LEAN>
-constexpr int lds_words() { return cols_words<LEAN>() + kTailW; }
-static_assert(lds_words<true>() * 4 * Layout<true>::kBlocksPerCU <= 160 * 1024, "LDS budget");
-static_assert(lds_words<false>() * 4 * Layout<false>::kBlocksPerCU <= 160 * 1024, "LDS budget");
-static_assert((cols_words<true>() & 1) == 0 && (cols_words<false>() & 1) == 0 && (kHistW & 1) == 0,
-              "u64 cells must stay 8-byte aligned");
+// LEAN keeps qualities in HBM/L2 (2 workgroups = 16 waves per CU); the full variant, whose
+// trimming windows read qualities at random, stages them in LDS rows (1 workgroup per CU).  The
+// merge variant adds the post-stats block of read 1's cycles 160..319 (merged reads reach
+// len1 + len2) and gives up a wave for it.
+template <bool LEAN, bool MERGE = false>
+struct Layout {
+    static constexpr int kBlocksPerCU = LEAN ? 2 : 1;
+    static constexpr int kWaves = MERGE ? 7 : 8;
+    static constexpr int kThreads = 64 * kWaves;
+    static constexpr int kWaveW = kCodeW + (LEAN ? 0 : 64 * kQS);
+    static constexpr int kHists = MERGE ? 5 : 4;  // [pre1, pre2, post1 (x2 with MERGE), post2]
+    static constexpr int kColsW = kWaves * kWaveW;
+    static constexpr int kLdsW = kColsW + kHists * kHistW + kSmallW + kScalW + kAdW;
+    static_assert(kLdsW * 4 * kBlocksPerCU <= 160 * 1024, "LDS budget");
+    static_assert((kColsW & 1) == 0 && (kHistW & 1) == 0, "u64 cells must stay 8-byte aligned");
+    static_assert(kThreads <= kBlock, "launch bound");
+};
 
 constexpr unsigned long long kCount1 = 1ull << 40;
 constexpr unsigned long long kQMask = kCount1 - 1;
@@ -288,20 +288,22 @@ __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) &
 // PAIRED: a tile is 32 pairs, lanes l and l+32 holding the two mates of a pair (read 2's column
 // reverse-complemented for the overlap scan); single-end: a tile is 64 reads, one per lane, with
 // SingleEndProcessor::processSingleEnd's order (src/seprocessor.cpp:290-360).
-template <bool LEAN, bool PAIRED>
+template <bool LEAN, bool PAIRED, bool MERGE>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 * Layout<LEAN>::kBlocksPerCU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t* col = lds + wave * Layout<LEAN>::kWaveW;  // code / N columns: word field*64 + lane
-    uint32_t* qrows = col + kCodeW;                    // full variant: quality rows, row = lane
-    uint32_t* hist = lds + cols_words<LEAN>();         // [pre1, pre2, post1, post2] x kHistW
-    unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + 4 * kHistW);
+    using LY = Layout<LEAN, MERGE>;
+    constexpr int kWaves = LY::kWaves, kThreads = LY::kThreads;
+    uint32_t* col = lds + wave * LY::kWaveW;  // code / N columns: word field*64 + lane
+    uint32_t* qrows = col + kCodeW;           // full variant: quality rows, row = lane
+    uint32_t* hist = lds + LY::kColsW;        // [pre1, pre2, post1, post2] x kHistW (post1 x2 with MERGE)
+    unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + LY::kHists * kHistW);
     unsigned long long* scal = small + kSmallW / 2;
     uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16 * kScalCopies);
-    for (int i = threadIdx.x; i < 4 * kHistW + kSmallW + kScalW; i += kBlock) hist[i] = 0;
-    for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kBlock)
+    for (int i = threadIdx.x; i < LY::kHists * kHistW + kSmallW + kScalW; i += kThreads) hist[i] = 0;
+    for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kThreads)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
     __syncthreads();
 
@@ -316,7 +318,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
     // Without front trimming every kept window starts at 0, so the post blocks are accumulated
     // as "removed" (trimmed tails and failed pairs) and become pre - removed at the flush.
-    const bool removed_mode = LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front);
+    const bool removed_mode = !MERGE && (LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front));
     const int g_per = max(p.polyg_one_mismatch_per, 1);
     const int g_inv = g_per > 256 ? 0 : (65536 + g_per - 1) / g_per;
 #ifdef FQ_PHASE_STAMPS
@@ -347,7 +349,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         const int my_alen = mate ? p.adapter2_len : p.adapter1_len;
         const int my_maxlen = mate ? p.max_len2 : p.max_len1;
         uint32_t* my_pre = hist + mate * kHistW;
-        uint32_t* my_post = hist + (2 + mate) * kHistW;  // post block, or the "removed" block (see below)
+        uint32_t* my_post = hist + (2 + (MERGE ? 2 : 1) * mate) * kHistW;  // post block, or the "removed" block
         const int r = lane_x & 15;  // stats rotation within a chunk
         uint32_t* qrow = qrows + lane_x * kQS;
         const int idx = PAIRED ? t * 32 + pl : t * 64 + lane_x;
@@ -363,7 +365,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             if (LEAN) return *reinterpret_cast<const uint4*>(Q + 16 * F);
             return make_uint4(qrow[4 * F], qrow[4 * F + 1], qrow[4 * F + 2], qrow[4 * F + 3]);
         };
-        const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4);
+        // (merge: a merged read, at most len1 + len2 long, must fit max_cycles as well)
+        const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4) ||
+                         (MERGE && L + __shfl_xor(L, 32) > p.max_cycles);
         uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0, lowf = 0, tqf = 0, nbf = 0;  // whole-read sums
         // column word of chunk k: k for read 1, 9-k for read 2 (stepped, not precomputed, so the
         // ten addresses are not kept live across tiles)
@@ -502,8 +506,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 }
             }
         };
-        // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
-        if (PAIRED && both && !(abl & 1)) {
+        // OverlapAnalysis::analyze (src/overlapanalysis.cpp:7-72) of the pair's current windows;
+        // both lanes of the pair call it together and get the same result
+        auto pair_overlap = [&]() -> Overlap {
             const int st_o = __shfl_xor(st, 32), n_o = __shfl_xor(n, 32);
             const int st1 = mate ? st_o : st, n1 = mate ? n_o : n;
             const int st2 = mate ? st : st_o, n2 = mate ? n : n_o;
@@ -536,6 +541,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             Overlap ov{0, 0, 0, 0};
             if (f1) ov = mate ? Overlap{1, off_o, ol_o, d_o} : Overlap{1, mine.off, mine.ol, mine.diff};
             else if (f2) ov = mate ? Overlap{1, mine.off, mine.ol, mine.diff} : Overlap{1, off_o, ol_o, d_o};
+            return ov;
+        };
+        // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
+        if (PAIRED && both && !(abl & 1)) {
+            const Overlap ov = pair_overlap();
+            const int n_o = __shfl_xor(n, 32);
+            const int n1 = mate ? n_o : n, n2 = mate ? n : n_o;
             if (mate == 0) {  // PairEndProcessor::statInsertSize, src/peprocessor.cpp:510-523
                 int isize = p.insert_size_max;
                 if (ov.overlapped) isize = ov.offset > 0 ? n1 + n2 - ov.len : ov.len;
@@ -573,22 +585,47 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         }
         if (!LEAN && both && my_maxlen > 0 && my_maxlen < n) n = my_maxlen;
 
+        // ---------------- merge (src/peprocessor.cpp:351-385, OverlapAnalysis::merge
+        // src/overlapanalysis.cpp:74-104): the merged read is r1[0, m1) + revcomp(r2)[ol, ol+m2) ----
+        bool merged = false;
+        int m1 = 0, m2 = 0, mol = 0;
+        if (MERGE && both) {
+            const Overlap ov2 = pair_overlap();
+            if (ov2.overlapped) {
+                merged = true;
+                mol = ov2.len;
+                const int n_o = __shfl_xor(n, 32);
+                const int n1 = mate ? n_o : n, n2 = mate ? n : n_o;
+                if (mol) {
+                    m1 = min(mol + max(0, ov2.offset), n1);
+                    m2 = ov2.offset > 0 ? max(0, n2 - mol) : 0;
+                }
+            }
+        }
+        // the window that the filter and the post stats see: the read's own [st, st+n), or its
+        // part of the merged read (read 2: forward positions [st+n-ol-m2, st+n-ol), reversed)
+        const int ws = (MERGE && merged && mate) ? st + n - mol - m2 : st;
+        const int wn = (MERGE && merged) ? (mate ? m2 : m1) : n;
+
         FQ_STAMP(4)
         // ---------------- passFilter (src/filter.cpp:3-52) ----------------
         int code = FQ_FAIL_LENGTH;
         uint32_t w20 = 0, w30 = 0;  // Q20/Q30 of the window, for the post stats
-        if (nn && n > 0) {
-            // window sums = whole-read sums (from staging) minus the trimmed head [0, st) and
-            // tail [st+n, L): the trimmed parts are usually a few bases
-            int low = (int)lowf, tq = (int)tqf, nb = (int)nbf;
+        int low = 0, tq = 0, nb = 0;
+        if (nn && wn > 0) {
+            // window sums = whole-read sums (from staging) minus the trimmed head [0, ws) and
+            // tail [ws+wn, L): the trimmed parts are usually a few bases
+            low = (int)lowf;
+            tq = (int)tqf;
+            nb = (int)nbf;
             w20 = q20;
             w30 = q30;
             if (!(abl & 2)) {
-                const int end = st + n;
+                const int end = ws + wn;
                 const bool need_tq = p.avg_qual_limit > 0;  // the total quality only feeds -e
 #pragma unroll
                 for (int part = 0; part < 2; ++part) {
-                    const int a0 = part ? end : 0, a1 = part ? L : st;  // forward range [a0, a1)
+                    const int a0 = part ? end : 0, a1 = part ? L : ws;  // forward range [a0, a1)
                     const int F0 = a0 >> 4, F1 = (a1 + 15) >> 4;
                     // row chunks come from L2; the next one is requested before this one is used
                     uint4 cur = qchunk(min(F0, nchunks - 1));
@@ -615,27 +652,60 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                         nb -= __popc(w & posmask(s1 - 16 * c) & ~posmask(s0 - 16 * c));
                     }
                 }
-                tq -= 33 * n;
             }
-            code = filter_verdict(p, n, low, nb, tq, [&]() {
-                if (LEAN) return 0;  // not reached: LEAN excludes the complexity filter
-                int diff = 0;
-                for (int i = 0; i < n - 1; ++i) diff += seq(st + i) != seq(st + i + 1);
-                return diff;
-            });
+            if (!(MERGE && merged))
+                code = filter_verdict(p, n, low, nb, tq - 33 * n, [&]() {
+                    if (LEAN) return 0;  // not reached: LEAN excludes the complexity filter
+                    int diff = 0;
+                    for (int i = 0; i < n - 1; ++i) diff += seq(st + i) != seq(st + i + 1);
+                    return diff;
+                });
+        }
+        int mlen = 0;
+        if (MERGE && merged) {  // passFilter of the merged read: the sums of its two parts
+            mlen = m1 + m2;
+            low += __shfl_xor(low, 32);
+            nb += __shfl_xor(nb, 32);
+            tq += __shfl_xor(tq, 32);
+            w20 += __shfl_xor(w20, 32);
+            w30 += __shfl_xor(w30, 32);
+            // (OverlapAnalysis::merge returns NULL for ol 0; the complexity filter is excluded
+            // from the merge variant)
+            code = (mol == 0 || mlen == 0) ? FQ_FAIL_LENGTH
+                                           : filter_verdict(p, mlen, low, nb, tq - 33 * mlen, [&]() { return 0; });
         }
         const int code_o = PAIRED ? __shfl_xor(code, 32) : code;
         const bool pair_pass = both && code == FQ_PASS_FILTER && code_o == FQ_PASS_FILTER;
-        if (PAIRED) {
+        bool post_on;  // this lane's window goes to a post block
+        if (MERGE && merged) {
+            if (mate == 0) {
+                sadd(&small[FQ_ACC_FILTER + code], 2ull);  // addFilterResult(result, 2)
+                if (code == FQ_PASS_FILTER) sadd(&small[FQ_ACC_MERGED_PAIRS], 1ull);
+                rr.flags |= FQ_RF_OVERLAP | FQ_RF_MERGED;
+                rr.m_len1 = (uint16_t)m1;
+                rr.m_len2 = (uint16_t)m2;
+            }
+            post_on = code == FQ_PASS_FILTER;
+        } else if (MERGE && both && !p.discard_unmerged) {  // unmerged reads are filtered one by one
+            sadd(&small[FQ_ACC_FILTER + code], 1ull);
+            post_on = code == FQ_PASS_FILTER;
+        } else if (PAIRED) {
             if (mate == 0 && valid) sadd(&small[FQ_ACC_FILTER + max(code, code_o)], 2ull);  // addFilterResult: +2
-        } else if (valid) {
-            sadd(&small[FQ_ACC_FILTER + code], 1ull);  // src/seprocessor.cpp:339
+            post_on = !MERGE && pair_pass;
+        } else {
+            if (valid) sadd(&small[FQ_ACC_FILTER + code], 1ull);  // src/seprocessor.cpp:339
+            post_on = pair_pass;
         }
 
         FQ_STAMP(5)
         // ---------------- Stats::statRead, pre and post (src/peprocessor.cpp:276-277,400-401) ----
         if (valid && !(abl & 4)) {
-            const int wlen = pair_pass ? n : 0;  // post window [st, st + wlen)
+            const int wlen = post_on ? wn : 0;  // post window [ws, ws + wlen)
+            // merged pairs: both parts go to read 1's post block, read 2's part reversed and
+            // complemented (merged cycle c0 - pos)
+            uint32_t* post_h = (MERGE && merged) ? hist + 2 * kHistW : my_post;
+            const bool rev = MERGE && merged && mate;
+            const int c0 = st + n - 1 - mol + m1;
             const int nchl = (L + 15) >> 4;
             const int dsel = r >> 2;
             // chunk F+1's codes (LDS) and the qualities of chunks F+1, F+2 (the row again, now from
@@ -675,8 +745,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                                 // added, so these atomics run with few active lanes
                                 if (pos >= wlen && pos < L) hadd(my_post, cell(pos, slot), v);
                             } else {
-                                const bool inw = (unsigned)(pos - st) < (unsigned)wlen;
-                                hadd(my_post, inw ? cell(pos - st, slot) : cell(pos, kDummySlot), v);
+                                const bool inw = (unsigned)(pos - ws) < (unsigned)wlen;
+                                int cyc = pos - ws, sl = slot;
+                                if (MERGE && rev) {
+                                    cyc = c0 - pos;
+                                    sl = slot < 4 ? slot ^ 2 : 4;  // A<->T, C<->G
+                                }
+                                hadd(post_h, inw ? cell(cyc, sl) : cell(pos, kDummySlot), v);
                             }
                         }
                     }
@@ -688,7 +763,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             sadd(&sc[1], (unsigned long long)L);
             sadd(&sc[2], (unsigned long long)q20);
             sadd(&sc[3], (unsigned long long)q30);
-            if (pair_pass) {
+            if (MERGE && merged) {
+                if (post_on && mate == 0) {
+                    sadd(&sc[8], 1ull);
+                    sadd(&sc[9], (unsigned long long)mlen);
+                    sadd(&sc[10], (unsigned long long)w20);
+                    sadd(&sc[11], (unsigned long long)w30);
+                }
+            } else if (post_on) {
                 sadd(&sc[8], 1ull);
                 sadd(&sc[9], (unsigned long long)n);
                 sadd(&sc[10], (unsigned long long)w20);
@@ -716,7 +798,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 
     // ---------------- flush to the global accumulator ----------------
     const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
-    for (int i = threadIdx.x; i < nsmall; i += kBlock)
+    for (int i = threadIdx.x; i < nsmall; i += kThreads)
         if (small[i]) atomicAdd(&acc[i], small[i]);
     const size_t st_base = acc_stats_offset(p.insert_size_max, p.max_cycles, 0);
     const size_t st_words = acc_stats_words(p.max_cycles);
@@ -726,12 +808,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         for (int c = 0; c < kScalCopies; ++c) v += scal[16 * c + threadIdx.x];
         if (v) atomicAdd(&acc[st_base + k * st_words + f], v);
     }
-    const int ncyc = min(kMaxLen, p.max_cycles);
-    for (int i = threadIdx.x; i < 4 * ncyc * 5; i += kBlock) {
-        const int k = i / (ncyc * 5);
-        const int rem = i - k * ncyc * 5;
-        const int c = rem / 5, slot = rem - c * 5;
-        const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hist + k * kHistW + cell(c, slot));
+    for (int k = 0; k < 4; ++k) {
+      const int ncyc = min((MERGE && k == 2) ? 2 * kMaxLen : kMaxLen, p.max_cycles);
+      const uint32_t* hk = hist + (k == 3 && MERGE ? 4 : k) * kHistW;
+      for (int i = threadIdx.x; i < ncyc * 5; i += kThreads) {
+        const int c = i / 5, slot = i - c * 5;
+        const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hk + cell(c, slot));
         long long cnt = (long long)(v >> 40);
         long long qs = (long long)(v & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
         if (k >= 2 && removed_mode) {  // post = pre - removed
@@ -747,13 +829,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         unsigned long long* dst = acc + st_base + k * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
         atomicAdd(&dst[cls], (unsigned long long)cnt);
         atomicAdd(&dst[8 + cls], (unsigned long long)qs);
+      }
     }
 }
 
 }  // namespace
 
 bool fq_pe_fast_supported(const fq_params& p) {
-    return !p.merge_enabled && p.insert_size_max <= 512 && p.insert_size_max >= 0;
+    return p.insert_size_max <= 512 && p.insert_size_max >= 0 &&
+           (!p.merge_enabled || (p.paired && !p.complexity_enabled));
 }
 
 // profiling aid (tools/ablate.py --phases): read and clear the per-phase cycle totals
@@ -767,10 +851,11 @@ extern "C" __attribute__((visibility("default"))) int fq_debug_phase_cycles(unsi
 }
 
 hipError_t fq_pe_fast_prepare() {
-    const void* k[4] = {(const void*)pe_fast_kernel<true, true>, (const void*)pe_fast_kernel<false, true>,
-                        (const void*)pe_fast_kernel<true, false>, (const void*)pe_fast_kernel<false, false>};
-    for (int i = 0; i < 4; ++i) {
-        const int words = (i & 1) ? lds_words<false>() : lds_words<true>();
+    const void* k[5] = {(const void*)pe_fast_kernel<true, true, false>, (const void*)pe_fast_kernel<false, true, false>,
+                        (const void*)pe_fast_kernel<true, false, false>, (const void*)pe_fast_kernel<false, false, false>,
+                        (const void*)pe_fast_kernel<false, true, true>};
+    for (int i = 0; i < 5; ++i) {
+        const int words = i == 4 ? Layout<false, true>::kLdsW : (i & 1) ? Layout<false>::kLdsW : Layout<true>::kLdsW;
         hipError_t e = hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, words * 4);
         if (e != hipSuccess) return e;
     }
@@ -782,19 +867,24 @@ hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_resu
     const bool lean = p.trim_front1 == 0 && p.trim_tail1 == 0 && p.trim_front2 == 0 && p.trim_tail2 == 0 &&
                       !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
                       p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled;
-    const dim3 gl(grid * Layout<true>::kBlocksPerCU), gf(grid * Layout<false>::kBlocksPerCU);
-    const size_t ll = lds_words<true>() * 4, lf = lds_words<false>() * 4;
-    if (p.paired && lean)
-        hipLaunchKernelGGL((pe_fast_kernel<true, true>), gl, dim3(kBlock), ll, stream, p, b, res, acc, slow_tiles,
-                           slow_count);
+    using LL = Layout<true>;
+    using LF = Layout<false>;
+    using LM = Layout<false, true>;
+    const dim3 gl(grid * LL::kBlocksPerCU), gf(grid * LF::kBlocksPerCU);
+    if (p.merge_enabled)
+        hipLaunchKernelGGL((pe_fast_kernel<false, true, true>), dim3(grid * LM::kBlocksPerCU), dim3(LM::kThreads),
+                           LM::kLdsW * 4, stream, p, b, res, acc, slow_tiles, slow_count);
+    else if (p.paired && lean)
+        hipLaunchKernelGGL((pe_fast_kernel<true, true, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4, stream, p, b,
+                           res, acc, slow_tiles, slow_count);
     else if (p.paired)
-        hipLaunchKernelGGL((pe_fast_kernel<false, true>), gf, dim3(kBlock), lf, stream, p, b, res, acc, slow_tiles,
-                           slow_count);
+        hipLaunchKernelGGL((pe_fast_kernel<false, true, false>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
+                           res, acc, slow_tiles, slow_count);
     else if (lean)
-        hipLaunchKernelGGL((pe_fast_kernel<true, false>), gl, dim3(kBlock), ll, stream, p, b, res, acc, slow_tiles,
-                           slow_count);
+        hipLaunchKernelGGL((pe_fast_kernel<true, false, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4, stream, p, b,
+                           res, acc, slow_tiles, slow_count);
     else
-        hipLaunchKernelGGL((pe_fast_kernel<false, false>), gf, dim3(kBlock), lf, stream, p, b, res, acc, slow_tiles,
-                           slow_count);
+        hipLaunchKernelGGL((pe_fast_kernel<false, false, false>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
+                           res, acc, slow_tiles, slow_count);
     return hipGetLastError();
 }

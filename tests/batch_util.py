@@ -157,6 +157,14 @@ def config(name, max_cycles=256):
         p.length_filter_enabled, p.min_len, p.max_len = 1, 20, 100
         p.complexity_enabled = 1
         p.low_qual_base_limit = 10
+    elif name == "PE_merge_q":  # merge with polyX, adapters by sequence, maxLen, a short overlap requirement
+        p.merge_enabled = 1
+        p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
+        abi.set_adapter(p, 1, AD1[:16])
+        p.max_len2 = 120
+        p.overlap_diff_limit, p.overlap_require = 5, 12
+        p.avg_qual_limit = 20.0
+        p.length_filter_enabled, p.min_len = 1, 40
     elif name.startswith("PE_cutR"):  # cut_right alone (removed-mode stats), window w
         w = int(name[7:])
         p.adapter_trimming = p.polyg_enabled = 1
@@ -173,7 +181,7 @@ def config(name, max_cycles=256):
 
 
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
-               "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR5"]
+               "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR5", "PE_merge_q"]
 
 
 def run_oracle(oracle, p, pk):

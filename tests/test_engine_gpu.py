@@ -78,7 +78,7 @@ def test_edge_case_parity(eng_lib, oracle, name, mode):
     assert_same(p, res_o, acc_o, res_e, acc_e)
 
 
-@pytest.mark.parametrize("name", ["C3", "C3b", "C5", "PE_all", "C2", "SE_all"])
+@pytest.mark.parametrize("name", ["C3", "C3b", "C4", "C5", "PE_all", "C2", "SE_all"])
 def test_mixed_fast_and_handoff_tiles(eng_lib, oracle, name):
     """Mostly clean synthetic tiles plus scattered tiles with IUPAC bases, quality bytes >= 128
     and over-long reads: the fast kernel hands those tiles to the general kernel."""
