@@ -39,6 +39,21 @@ WORKLOADS = {
 WORKLOAD = WORKLOADS["C3"]
 
 
+def pmc_traffic(cfg, pairs):
+    """HBM bytes per launch of the fast kernel for this workload, from the latest committed PMC
+    profile (tools/profile_round.sh: rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this same bench
+    command, corrected per MI355X_MICROARCH.md); None when no profile matches the batch size."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{cfg}.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    if int(d.get("pairs", -1)) != pairs:
+        return None, None
+    return int(d["traffic_bytes"]), os.path.relpath(paths[-1], REPO)
+
+
 def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -237,6 +252,7 @@ def main():
     assert int(acc_host[abi.FQ_ACC_FILTER:abi.FQ_ACC_FILTER + 32].sum()) == reads
 
     value = reads * args.steps / elapsed / 1e6
+    traffic, traffic_src = pmc_traffic(args.config, args.pairs) if world == 1 else (None, None)
     bytes_per_pair = (2 if paired else 1) * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result per read
     achieved = n * bytes_per_pair / (kavg / 1e3) / 1e9
     out = {
@@ -255,8 +271,11 @@ def main():
         "config": {"workload": WORKLOADS[args.config], ("pairs_per_gpu" if paired else "reads_per_gpu"): n, "read_len": READ_LEN, "row_stride": STRIDE,
                    "parallelism": f"dp{world} (pairs sharded, RCCL sum of the accumulator block)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel_ms_avg": round(kavg, 3), "bytes_per_pair": bytes_per_pair},
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes per launch (PMC)", "traffic_src": traffic_src,
+                     "algorithmic_bytes": n * bytes_per_pair,
+                     "kernel_ms_avg": round(kavg, 3),
+                     ("bytes_per_pair" if paired else "bytes_per_read"): bytes_per_pair},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C3":

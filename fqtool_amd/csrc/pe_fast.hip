@@ -316,8 +316,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     const int K = max(limit, 1);
     const int req = p.overlap_require;
     const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
-    // Without front trimming every kept window starts at 0, so the post blocks are accumulated
-    // as "removed" (trimmed tails and failed pairs) and become pre - removed at the flush.
+    // Without front trimming every kept window starts at 0, so each base lands in exactly one of
+    // two disjoint blocks: "kept" (inside a passing read's window; the post block) or "removed"
+    // (trimmed tails, failed pairs; the pre block), one LDS atomic per base.  At the flush
+    // pre = kept + removed and post = kept.
     const bool removed_mode = !MERGE && (LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front));
     const int g_per = max(p.polyg_one_mismatch_per, 1);
     const int g_inv = g_per > 256 ? 0 : (65536 + g_per - 1) / g_per;
@@ -739,12 +741,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                         const int slot = (int)(((cr >> (2 * tt)) & 3u) + ((nr >> (2 * tt)) & 1u));
                         const unsigned long long v = kCount1 | (unsigned long long)(qv | 0x80u);
                         if (!(abl & 16)) {
-                            hadd(my_pre, cell(pos, pos < L ? slot : kDummySlot), v);
+                            const int cl = cell(pos, pos < L ? slot : kDummySlot);
                             if (removed_mode) {
-                                // post = pre - removed: only the bases outside the kept window are
-                                // added, so these atomics run with few active lanes
-                                if (pos >= wlen && pos < L) hadd(my_post, cell(pos, slot), v);
+                                hadd(pos < wlen ? my_post : my_pre, cl, v);  // kept : removed
                             } else {
+                                hadd(my_pre, cl, v);
                                 const bool inw = (unsigned)(pos - ws) < (unsigned)wlen;
                                 int cyc = pos - ws, sl = slot;
                                 if (MERGE && rev) {
@@ -814,16 +815,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
       for (int i = threadIdx.x; i < ncyc * 5; i += kThreads) {
         const int c = i / 5, slot = i - c * 5;
         const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hk + cell(c, slot));
-        long long cnt = (long long)(v >> 40);
-        long long qs = (long long)(v & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
-        if (k >= 2 && removed_mode) {  // post = pre - removed
-            const unsigned long long pv =
-                *reinterpret_cast<const unsigned long long*>(hist + (k - 2) * kHistW + cell(c, slot));
-            const long long pc = (long long)(pv >> 40);
-            const long long pq = (long long)(pv & kQMask) - 161ll * pc;
-            cnt = pc - cnt;
-            qs = pq - qs;
-        }
+        // removed mode: pre = removed (this block) + kept (the post block); post = kept
+        const unsigned long long w =
+            v + ((k < 2 && removed_mode) ? *reinterpret_cast<const unsigned long long*>(hk + 2 * kHistW + cell(c, slot))
+                                         : 0ull);
+        const long long cnt = (long long)(w >> 40);
+        const long long qs = (long long)(w & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
         if (cnt == 0 && qs == 0) continue;
         const int cls = slot_class(slot);
         unsigned long long* dst = acc + st_base + k * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
