@@ -8,6 +8,10 @@ HIPFLAGS   ?= -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-resu
 ifneq ($(STAMPS),)
 HIPFLAGS   += -DFQ_PHASE_STAMPS
 endif
+# make AHEAD=n: staging look-ahead of the fast kernel (profiling)
+ifneq ($(AHEAD),)
+HIPFLAGS   += -DFQ_AHEAD=$(AHEAD)
+endif
 CSRC       := fqtool_amd/csrc
 LIBDIR     := fqtool_amd/lib
 OBJDIR     := build/obj

@@ -38,6 +38,10 @@ using namespace fqdev;
 
 namespace {
 
+#ifndef FQ_AHEAD
+#define FQ_AHEAD 3
+#endif
+constexpr int kAhead = FQ_AHEAD;  // staging: row chunks requested this many chunks ahead of their use
 constexpr int kBlock = 512;  // launch bound: 8 waves (7 in the merge variant)
 constexpr int kMaxLen = 160;
 constexpr int kChunks = kMaxLen / 16;             // 16-position chunks per read
@@ -380,21 +384,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         // the look-ahead loads are clamped, never guarded.  Only the chunks that some lane's read
         // does not fill (wave-uniform test) pay for byte masks.
         const int lastc = nchunks - 1;
-        uint4 sA = *reinterpret_cast<const uint4*>(S), qA = *reinterpret_cast<const uint4*>(Q);
-        uint4 sB = *reinterpret_cast<const uint4*>(S + 16 * min(1, lastc));
-        uint4 qB = *reinterpret_cast<const uint4*>(Q + 16 * min(1, lastc));
-        uint4 sC = *reinterpret_cast<const uint4*>(S + 16 * min(2, lastc));
-        uint4 qC = *reinterpret_cast<const uint4*>(Q + 16 * min(2, lastc));
+        uint4 sb[kChunks], qb[kChunks];
+#pragma unroll
+        for (int k = 0; k < kAhead && k < kChunks; ++k) {
+            sb[k] = *reinterpret_cast<const uint4*>(S + 16 * min(k, lastc));
+            qb[k] = *reinterpret_cast<const uint4*>(Q + 16 * min(k, lastc));
+        }
 #pragma unroll
         for (int k = 0; k < kChunks; ++k) {
-            const uint4 s4 = sA, q4 = qA;
-            sA = sB;
-            qA = qB;
-            sB = sC;
-            qB = qC;
-            if (k + 3 < kChunks) {
-                sC = *reinterpret_cast<const uint4*>(S + 16 * min(k + 3, lastc));
-                qC = *reinterpret_cast<const uint4*>(Q + 16 * min(k + 3, lastc));
+            const uint4 s4 = sb[k], q4 = qb[k];
+            if (k + kAhead < kChunks) {
+                sb[k + kAhead] = *reinterpret_cast<const uint4*>(S + 16 * min(k + kAhead, lastc));
+                qb[k + kAhead] = *reinterpret_cast<const uint4*>(Q + 16 * min(k + kAhead, lastc));
             }
             if (k < nchunks) {
                 const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
