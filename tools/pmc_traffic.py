@@ -44,7 +44,7 @@ def main():
     w_kb = sum(write[k]) / len(write[k])
     traffic = (2 * f_kb + w_kb) * 1024
     print(json.dumps({
-        "config": a.config, "pairs": a.pairs, "kernel": k.split("(")[0],
+        "config": a.config, "pairs": a.pairs, "kernel": k.replace("(anonymous namespace)::", "").split("(")[0],
         "dispatches": len(fetch[k]), "FETCH_SIZE_kB": round(f_kb, 1), "WRITE_SIZE_kB": round(w_kb, 1),
         "traffic_bytes": int(traffic),
         "correction": "traffic = 2 x FETCH_SIZE + WRITE_SIZE (kB x 1024); FETCH_SIZE doubled on gfx950 "
