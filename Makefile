@@ -9,6 +9,21 @@ ifneq ($(STAMPS),)
 HIPFLAGS   += -DFQ_PHASE_STAMPS
 endif
 # make AHEAD=n: staging look-ahead of the fast kernel (profiling)
+ifneq ($(ABLATE_STAGE),)
+HIPFLAGS   += -DFQ_ABLATE_STAGE=$(ABLATE_STAGE)
+endif
+ifneq ($(OPAQUE_NCH),)
+HIPFLAGS   += -DFQ_OPAQUE_NCH=$(OPAQUE_NCH)
+endif
+ifneq ($(OPAQUE_LK),)
+HIPFLAGS   += -DFQ_OPAQUE_LK=$(OPAQUE_LK)
+endif
+ifneq ($(SCHED_PIN),)
+HIPFLAGS   += -DFQ_SCHED_PIN=$(SCHED_PIN)
+endif
+ifneq ($(FIXED_STRIDE),)
+HIPFLAGS   += -DFQ_FIXED_STRIDE=1
+endif
 ifneq ($(AHEAD),)
 HIPFLAGS   += -DFQ_AHEAD=$(AHEAD)
 endif

@@ -38,6 +38,18 @@ using namespace fqdev;
 
 namespace {
 
+#ifndef FQ_ABLATE_STAGE
+#define FQ_ABLATE_STAGE 0
+#endif
+#ifndef FQ_OPAQUE_NCH
+#define FQ_OPAQUE_NCH 1
+#endif
+#ifndef FQ_OPAQUE_LK
+#define FQ_OPAQUE_LK 1
+#endif
+#ifndef FQ_SCHED_PIN
+#define FQ_SCHED_PIN 1
+#endif
 #ifndef FQ_AHEAD
 #define FQ_AHEAD 3
 #endif
@@ -315,7 +327,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics
     const int abl = p.reserved[0];
     const int ntiles = PAIRED ? (b.n + 31) >> 5 : (b.n + 63) >> 6;
+#if FQ_FIXED_STRIDE  // profiling only: assume rows of >= 160 bytes
+    constexpr int nchunks = kChunks;
+#else
     const int nchunks = min(kChunks, b.stride >> 4);
+#endif
     const int limit = p.overlap_diff_limit;
     const int K = max(limit, 1);
     const int req = p.overlap_require;
@@ -383,7 +399,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         // trip per tile instead of one per chunk); every row is readable up to its stride, so
         // the look-ahead loads are clamped, never guarded.  Only the chunks that some lane's read
         // does not fill (wave-uniform test) pay for byte masks.
-        const int lastc = nchunks - 1;
+        // opaque per tile: the per-chunk offsets and in-row flags derived from it would otherwise
+        // be hoisted out of the tile loop and spilled
+        int nch = nchunks;
+#if FQ_OPAQUE_NCH
+        asm volatile("" : "+s"(nch));
+#endif
+        const int lastc = nch - 1;
         uint4 sb[kChunks], qb[kChunks];
 #pragma unroll
         for (int k = 0; k < kAhead && k < kChunks; ++k) {
@@ -397,15 +419,31 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 sb[k + kAhead] = *reinterpret_cast<const uint4*>(S + 16 * min(k + kAhead, lastc));
                 qb[k + kAhead] = *reinterpret_cast<const uint4*>(Q + 16 * min(k + kAhead, lastc));
             }
-            if (k < nchunks) {
+#if FQ_SCHED_PIN
+            // keep the loads where they are: left alone, the scheduler hoists them all to the top
+            // of the tile and then waits for every one of them before chunk 0
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+#if FQ_ABLATE_STAGE == 1  // profiling only: loads consumed, nothing computed (results invalid)
+            if (k < nch) tqf ^= s4.x ^ s4.y ^ s4.z ^ s4.w ^ q4.x ^ q4.y ^ q4.z ^ q4.w;
+            if (false) {
+#else
+            if (k < nch) {
+#endif
                 const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
                 const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
                 uint32_t cc = 0, nn4 = 0;
-                const bool full = __all(L >= 16 * k + 16);
+                // bases of this chunk still in the read; opaque, or the masks of all ten chunks
+                // (functions of L alone) are computed up front and kept live across the loop
+                int Lk = L - 16 * k;
+#if FQ_OPAQUE_LK
+                asm volatile("" : "+v"(Lk));
+#endif
+                const bool full = __all(Lk >= 16);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (!LEAN) qrow[4 * k + j] = qw[j];
-                    const uint32_t bm = full ? 0xFFFFFFFFu : bytemask(L - (16 * k + 4 * j));
+                    const uint32_t bm = full ? 0xFFFFFFFFu : bytemask(Lk - 4 * j);
                     const uint32_t kk = (sw[j] >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
                     const uint32_t canon = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, kk);
@@ -421,16 +459,25 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     nn4 |= ((kk >> 2) & 0x01010101u) << (2 * j);
                 }
                 const uint32_t fck = tr4x4(cc), fwk = tr4x4(nn4);
-                nbf += __popc(fwk & (full ? 0x55555555u : posmask(L - 16 * k)));
+                nbf += __popc(fwk & (full ? 0x55555555u : posmask(Lk)));
                 // read 2: the column is the reverse complement of the 160-position row, so the
                 // read's rc position j sits at index j + (160 - L); garbage beyond L lands below
                 const uint32_t rn = pairrev(fwk);
+#if FQ_ABLATE_STAGE == 2  // profiling only: no LDS column writes (results invalid)
+                tqf ^= (rc ? (pairrev(fck) ^ (0xAAAAAAAAu & ~(rn << 1))) : fck) ^ (rc ? rn : fwk);
+#else
                 wp[kFC * 64] = rc ? (pairrev(fck) ^ (0xAAAAAAAAu & ~(rn << 1))) : fck;
                 wp[kFN * 64] = rc ? rn : fwk;
+#endif
                 wp += wstep;
             }
         }
         const bool bad = odd || exo != 0 || (qhi & 0x80808080u) != 0;
+        for (int k = nch; k < kChunks; ++k) {  // unused tail of the row
+            wp[kFC * 64] = 0u;
+            wp[kFN * 64] = 0u;
+            wp += wstep;
+        }
         if (__any(bad)) {
             if (lane == 0) {  // the general kernel takes 32-read (single-end) / 32-pair tiles
                 if (PAIRED) {
@@ -443,14 +490,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             }
             continue;
         }
-        for (int k = nchunks; k < kChunks; ++k) {  // unused tail of the row
-            wp[kFC * 64] = 0u;
-            wp[kFN * 64] = 0u;
-            wp += wstep;
-        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if FQ_ABLATE_STAGE >= 3  // profiling only: staging, then straight to the result store
+        if (valid && res)
+            *reinterpret_cast<uint4*>(&res[PAIRED ? 2 * (size_t)idx + mate : (size_t)idx]) =
+                make_uint4(tqf, q20 + q30 + lowf + nbf, exo, FQ_ABLATE_STAGE == 4 ? L : 0);
+        continue;
+#endif
 
         FQ_STAMP(0)
         const CodeSeq seq{col, lane, rc};
@@ -784,9 +832,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             rr.start = nn ? (uint16_t)st : 0;
             rr.len = nn ? (uint16_t)n : 0;
             rr.code = (uint8_t)code;
-            if (res)
-                *reinterpret_cast<uint4*>(&res[PAIRED ? 2 * (size_t)idx + mate : (size_t)idx]) =
-                    *reinterpret_cast<const uint4*>(&rr);
+            // one 16-byte store (a struct copy compiles to four partial stores)
+            const uint4 w = make_uint4((uint32_t)rr.start | (uint32_t)rr.len << 16,
+                                       (uint32_t)rr.code | (uint32_t)rr.flags << 8 | (uint32_t)rr.ad_pos << 16,
+                                       (uint32_t)rr.ad_len | (uint32_t)rr.m_len1 << 16,
+                                       (uint32_t)rr.m_len2 | (uint32_t)rr.reserved << 16);
+            if (res) *reinterpret_cast<uint4*>(&res[PAIRED ? 2 * (size_t)idx + mate : (size_t)idx]) = w;
         }
     }
 

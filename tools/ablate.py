@@ -18,6 +18,9 @@ res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
 torch.cuda.synchronize()
 variants = [("full", 0), ("no_overlap", 1), ("no_filter", 2), ("no_stats", 4), ("no_polyg", 8),
             ("no_lds_atomics", 16), ("no_overlap_filter_stats", 7), ("stage_only", 15)]
+only = os.environ.get("VARIANTS")
+if only:
+    variants = [v for v in variants if v[0] in only.split(",")]
 results = {}
 for rep in range(3 if os.environ.get("CONFIG", "C3") == "C3" else 0):
     for name, bits in variants:
@@ -47,6 +50,8 @@ lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_e
 print("stamped run ms", lib.fq_engine_last_kernel_ms(h))
 lib.fq_debug_phase_cycles(out, 8)
 tot = sum(out)
-for nm, v in zip(names, out):
+if tot == 0:
+    print("no phase stamps (build with make STAMPS=1)")
+for nm, v in (zip(names, out) if tot else []):
     print(f"phase {nm:14s} {100.0 * v / tot:6.1f}%  {v / 2048:14.0f} cycles/wave")
 lib.fq_engine_destroy(h)

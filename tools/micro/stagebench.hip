@@ -1,0 +1,114 @@
+// Micro-benchmark (profiling aid): the fast kernel's staging access pattern (lane = row, ten
+// 16-byte loads per row per plane, tiles of 32 pairs) with the extras of the real tile loop
+// switched on one at a time, to find what separates it from a plain lane-row read.
+//   bit 0: 78 KB of dynamic LDS per workgroup (the LEAN layout: 2 workgroups per CU)
+//   bit 1: per-tile u16 length loads, used by a wave-wide vote
+//   bit 2: per-read 16-byte result store
+//   bit 3: 3-ahead software pipeline instead of all 20 loads up front
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+
+template <int MODE>
+__global__ void __launch_bounds__(512) stage_kernel(const uint8_t* __restrict__ s1, const uint8_t* __restrict__ q1,
+                                                    const uint8_t* __restrict__ s2, const uint8_t* __restrict__ q2,
+                                                    const uint16_t* __restrict__ len1, const uint16_t* __restrict__ len2,
+                                                    int n, uint4* __restrict__ res, uint32_t* out) {
+    extern __shared__ uint32_t lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t acc = 0;
+    const int ntiles = (n + 31) / 32;
+    for (int t = blockIdx.x * 8 + wave; t < ntiles; t += gridDim.x * 8) {
+        const int mate = lane >> 5;
+        const int idx = t * 32 + (lane & 31);
+        const bool valid = idx < n;
+        const size_t roff = (size_t)(valid ? idx : 0) * 160;
+        const uint8_t* S = (mate ? s2 : s1) + roff;
+        const uint8_t* Q = (mate ? q2 : q1) + roff;
+        int L = 150;
+        if (MODE & 2) L = valid ? (int)(mate ? len2[idx] : len1[idx]) : 0;
+        uint4 sb[10], qb[10];
+        if (MODE & 8) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                sb[k] = *reinterpret_cast<const uint4*>(S + 16 * k);
+                qb[k] = *reinterpret_cast<const uint4*>(Q + 16 * k);
+            }
+#pragma unroll
+            for (int k = 0; k < 10; ++k) {
+                if (k + 3 < 10) {
+                    sb[k + 3] = *reinterpret_cast<const uint4*>(S + 16 * (k + 3));
+                    qb[k + 3] = *reinterpret_cast<const uint4*>(Q + 16 * (k + 3));
+                }
+                acc += sb[k].x ^ sb[k].y ^ sb[k].z ^ sb[k].w ^ qb[k].x ^ qb[k].y ^ qb[k].z ^ qb[k].w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) {
+                sb[k] = *reinterpret_cast<const uint4*>(S + 16 * k);
+                qb[k] = *reinterpret_cast<const uint4*>(Q + 16 * k);
+            }
+#pragma unroll
+            for (int k = 0; k < 10; ++k)
+                acc += sb[k].x ^ sb[k].y ^ sb[k].z ^ sb[k].w ^ qb[k].x ^ qb[k].y ^ qb[k].z ^ qb[k].w;
+        }
+        if (MODE & 2) acc += __all(L >= 150) ? 1u : 0u;
+        if (MODE & 1) lds[threadIdx.x] = acc;
+        if ((MODE & 4) && valid) res[2 * (size_t)idx + mate] = make_uint4(acc, L, 0, 0);
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int MODE>
+float run(uint8_t** p, uint16_t** l, int n, uint4* res, uint32_t* out, int grid) {
+    const size_t lds = (MODE & 1) ? 78480 : 0;
+    hipFuncSetAttribute((const void*)stage_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    float best = 1e9f;
+    for (int rep = 0; rep < 5; ++rep) {
+        (void)hipEventRecord(e0);
+        hipLaunchKernelGGL(stage_kernel<MODE>, dim3(grid), dim3(512), lds, 0, p[0], p[1], p[2], p[3], l[0], l[1], n, res,
+                           out);
+        (void)hipEventRecord(e1);
+        (void)hipEventSynchronize(e1);
+        float ms;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best) best = ms;
+    }
+    return best;
+}
+
+int main() {
+    const int n = 20000000;
+    uint8_t* p[4];
+    uint16_t* l[2];
+    for (int i = 0; i < 4; ++i) {
+        if (hipMalloc(&p[i], (size_t)n * 160) != hipSuccess) return 1;
+        (void)hipMemset(p[i], 0x41 + i, (size_t)n * 160);
+    }
+    for (int i = 0; i < 2; ++i) {
+        if (hipMalloc(&l[i], (size_t)n * 2) != hipSuccess) return 1;
+        (void)hipMemset(l[i], 0, (size_t)n * 2);
+    }
+    uint4* res;
+    if (hipMalloc(&res, (size_t)n * 32) != hipSuccess) return 1;
+    uint32_t* out;
+    (void)hipMalloc(&out, 4);
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    const double bytes = 4.0 * n * 160;
+    const int grid = 2 * cus;
+    float ms[16];
+    ms[0] = run<0>(p, l, n, res, out, grid);
+    ms[1] = run<1>(p, l, n, res, out, grid);
+    ms[2] = run<2>(p, l, n, res, out, grid);
+    ms[4] = run<4>(p, l, n, res, out, grid);
+    ms[8] = run<8>(p, l, n, res, out, grid);
+    ms[15] = run<15>(p, l, n, res, out, grid);
+    const int modes[] = {0, 1, 2, 4, 8, 15};
+    for (int m : modes) printf("mode %2d  %.3f ms  %.0f GB/s\n", m, ms[m], bytes / (ms[m] / 1e3) / 1e9);
+    return 0;
+}
