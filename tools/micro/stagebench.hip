@@ -5,6 +5,8 @@
 //   bit 1: per-tile u16 length loads, used by a wave-wide vote
 //   bit 2: per-read 16-byte result store
 //   bit 3: 3-ahead software pipeline instead of all 20 loads up front
+//   bit 4: two lanes per row (lane pair reads 32 contiguous bytes: chunks 2c, 2c+1), one mate per
+//          instruction, instead of one lane per row
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -29,7 +31,23 @@ __global__ void __launch_bounds__(512) stage_kernel(const uint8_t* __restrict__ 
         int L = 150;
         if (MODE & 2) L = valid ? (int)(mate ? len2[idx] : len1[idx]) : 0;
         uint4 sb[10], qb[10];
-        if (MODE & 8) {
+        if (MODE & 16) {
+            // lanes 2r, 2r+1: row r of the tile, chunk parity lane & 1; 5 chunk pairs x 2 mates
+            const int r = lane >> 1, par = lane & 1;
+            const int id2 = t * 32 + r;
+            const size_t ro = (size_t)(id2 < n ? id2 : 0) * 160 + 16 * par;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+#pragma unroll
+                for (int c = 0; c < 5; ++c) {
+                    sb[5 * m + c] = *reinterpret_cast<const uint4*>((m ? s2 : s1) + ro + 32 * c);
+                    qb[5 * m + c] = *reinterpret_cast<const uint4*>((m ? q2 : q1) + ro + 32 * c);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 10; ++k)
+                acc += sb[k].x ^ sb[k].y ^ sb[k].z ^ sb[k].w ^ qb[k].x ^ qb[k].y ^ qb[k].z ^ qb[k].w;
+        } else if (MODE & 8) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 sb[k] = *reinterpret_cast<const uint4*>(S + 16 * k);
@@ -108,6 +126,11 @@ int main() {
     ms[4] = run<4>(p, l, n, res, out, grid);
     ms[8] = run<8>(p, l, n, res, out, grid);
     ms[15] = run<15>(p, l, n, res, out, grid);
+    float ms2[2];
+    ms2[0] = run<16>(p, l, n, res, out, grid);
+    ms2[1] = run<16 + 7>(p, l, n, res, out, grid);
+    printf("mode 16 (2 lanes/row)  %.3f ms  %.0f GB/s\n", ms2[0], bytes / (ms2[0] / 1e3) / 1e9);
+    printf("mode 23 (2 lanes/row + extras)  %.3f ms  %.0f GB/s\n", ms2[1], bytes / (ms2[1] / 1e3) / 1e9);
     const int modes[] = {0, 1, 2, 4, 8, 15};
     for (int m : modes) printf("mode %2d  %.3f ms  %.0f GB/s\n", m, ms[m], bytes / (ms[m] / 1e3) / 1e9);
     return 0;
