@@ -104,7 +104,7 @@ def cpu_baseline(lib, abi, torch, pairs):
 
     ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
     dev = torch.device("cuda:0")
-    bufs = [torch.empty(pairs * STRIDE, dtype=torch.uint8, device=dev) for _ in range(4)]
+    bufs = [torch.empty(abi.batch_bytes(pairs, STRIDE), dtype=torch.uint8, device=dev) for _ in range(4)]
     lens = [torch.empty(pairs, dtype=torch.int16, device=dev) for _ in range(2)]
     b = abi.FqBatch()
     b.n, b.stride = pairs, STRIDE
@@ -113,7 +113,7 @@ def cpu_baseline(lib, abi, torch, pairs):
     first = 10 ** 12  # a disjoint index range
     assert lib.fq_synth_fill_device(ctypes.byref(b), SEED, first, READ_LEN, None) == 0
     torch.cuda.synchronize()
-    arr = [t.cpu().numpy().reshape(pairs, STRIDE)[:, :READ_LEN] for t in bufs]
+    arr = [abi.untile_rows(t.cpu().numpy(), pairs, STRIDE)[:, :READ_LEN] for t in bufs]
     del bufs
     tmp = tempfile.mkdtemp(prefix="fqbench_")
     try:
@@ -190,7 +190,7 @@ def main():
 
     first, n = shard(rank, world, args.pairs)
     log(f"rank {rank}/{world}: allocating {4 * n * STRIDE / 1e9:.1f} GB of reads for {n} pairs")
-    bufs = [torch.empty(n * STRIDE, dtype=torch.uint8, device=dev) for _ in range(4)]
+    bufs = [torch.empty(abi.batch_bytes(n, STRIDE), dtype=torch.uint8, device=dev) for _ in range(4)]
     lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
     results = torch.empty(n * 2 * 16, dtype=torch.uint8, device=dev)
     acc = torch.zeros(lib.fq_engine_acc_words(h), dtype=torch.int64, device=dev)

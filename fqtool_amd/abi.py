@@ -80,6 +80,40 @@ class FqBatch(ctypes.Structure):
     ]
 
 
+# Batch planes hold rows in chunk-interleaved tiles (include/fqengine.h): byte j of read i at
+# (i // 32) * 32 * stride + (j // 16) * 512 + (i % 32) * 16 + j % 16.
+TILE_READS = 32
+CHUNK = 16
+
+
+def batch_bytes(n, stride):
+    """Bytes of one batch plane for n reads (whole tiles), fq_batch_bytes."""
+    return -(-n // TILE_READS) * TILE_READS * stride
+
+
+def batch_offset(stride, i, j=0):
+    """fq_batch_offset: plane offset of byte j of read i."""
+    return (i // TILE_READS) * TILE_READS * stride + (j // CHUNK) * TILE_READS * CHUNK + (i % TILE_READS) * CHUNK + j % CHUNK
+
+
+def tile_rows(rows):
+    """(n, stride) uint8 rows -> flat batch plane (numpy), padded to whole tiles."""
+    import numpy as np
+
+    n, stride = rows.shape
+    nt = -(-n // TILE_READS)
+    buf = np.zeros((nt * TILE_READS, stride), np.uint8)
+    buf[:n] = rows
+    return np.ascontiguousarray(buf.reshape(nt, TILE_READS, stride // CHUNK, CHUNK).transpose(0, 2, 1, 3)).reshape(-1)
+
+
+def untile_rows(plane, n, stride):
+    """Flat batch plane (numpy, >= batch_bytes(n, stride) bytes) -> (n, stride) rows."""
+    nt = -(-n // TILE_READS)
+    v = plane[: nt * TILE_READS * stride].reshape(nt, stride // CHUNK, TILE_READS, CHUNK).transpose(0, 2, 1, 3)
+    return v.reshape(nt * TILE_READS, stride)[:n]
+
+
 class FqReadResult(ctypes.Structure):
     _fields_ = [
         ("start", ctypes.c_uint16), ("len", ctypes.c_uint16),

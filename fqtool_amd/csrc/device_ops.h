@@ -1,7 +1,7 @@
 // device_ops.h -- per-read operations of the hot path as gfx950 device functions.
 //
 // Each function restates one reference function (file:line cited) on a read *view*: the
-// read's bytes stay where they are in HBM (row-major fq_batch rows) and trimming only moves
+// read's bytes stay where they are in HBM (fq_batch rows) and trimming only moves
 // (start, len).  Quality bytes are signed char, as std::string's char on x86-64.
 #pragma once
 
@@ -12,12 +12,22 @@
 
 namespace fqdev {
 
-struct View {
-    const uint8_t* s;  // row base: seq
-    const uint8_t* q;  // row base: qual
-    int start;         // surviving window [start, start+len)
-    int len;
+// A read's row in a batch plane (chunk-interleaved tiles, include/fqengine.h): byte j sits at
+// base[(j / 16) * 512 + j % 16], base = the read's chunk 0.  Indexable and offsettable like a
+// pointer, so the restatements below run on it unchanged.
+struct Row {
+    const uint8_t* base;
+    int off;
+    __device__ __forceinline__ uint8_t operator[](int i) const {
+        const int j = off + i;
+        return base[(j >> 4) * (FQ_TILE_READS * FQ_CHUNK) + (j & 15)];
+    }
+    __device__ __forceinline__ Row operator+(int k) const { return Row{base, off + k}; }
 };
+__device__ __forceinline__ Row batch_row(const uint8_t* plane, int stride, int idx) {
+    return Row{plane + (size_t)(idx / FQ_TILE_READS) * FQ_TILE_READS * stride + (idx % FQ_TILE_READS) * FQ_CHUNK, 0};
+}
+
 
 // Accumulator layout of include/fqengine.h, usable in device code.
 __device__ __forceinline__ size_t acc_stats_words(int max_cycles) {
@@ -29,7 +39,8 @@ __device__ __forceinline__ size_t acc_stats_offset(int insert_size_max, int max_
     return base + (size_t)k * acc_stats_words(max_cycles);
 }
 
-__device__ __forceinline__ int qv(const uint8_t* q, int i) { return (int)(int8_t)q[i]; }
+template <class P>
+__device__ __forceinline__ int qv(P q, int i) { return (int)(int8_t)q[i]; }
 
 __device__ __forceinline__ uint8_t comp(uint8_t c) {
     // Seq::reverseComplement, reference src/seq.h:24-48
@@ -67,16 +78,18 @@ __device__ inline int filter_verdict(const fq_params& p, int rlen, int low, int 
 // Accessors: every operation below reads bytes through functors seq(i) -> uint8_t and
 // qual(i) -> int (signed char value), so the same restatement runs on HBM rows (v1 kernel)
 // and on LDS-staged columns (v2 kernel).
+template <class P>
 struct PtrQual {
-    const uint8_t* p;
+    P p;
     __device__ __forceinline__ int operator()(int i) const { return (int)(int8_t)p[i]; }
 };
 struct LdsQual {  // quality byte i (signed, as the reference's char) of a row packed 4 per LDS word
     const uint32_t* row;
     __device__ __forceinline__ int operator()(int i) const { return (int)(int8_t)(row[i >> 2] >> ((i & 3) * 8)); }
 };
+template <class P>
 struct Bytes {
-    const uint8_t* p;
+    P p;
     __device__ __forceinline__ uint8_t operator()(int i) const { return p[i]; }
 };
 template <class A>
@@ -278,20 +291,22 @@ __device__ inline int trim_polyx_t(SQ d, int rlen, int mask, int compareReq, int
     return rlen;
 }
 
-// Pointer-based wrappers (v1 kernel).
-__device__ inline int pass_filter(const fq_params& p, const uint8_t* seq, const uint8_t* qual, int rlen, bool is_null) {
-    return pass_filter_t(p, Bytes{seq}, PtrQual{qual}, rlen, is_null);
+// Pointer-like wrappers (general kernel): P is a Row (or a plain byte pointer).
+template <class P>
+__device__ inline int pass_filter(const fq_params& p, P seq, P qual, int rlen, bool is_null) {
+    return pass_filter_t(p, Bytes<P>{seq}, PtrQual<P>{qual}, rlen, is_null);
 }
-__device__ inline bool trim_and_cut(const fq_params& p, const uint8_t* seq, const uint8_t* qual, int l, int front,
-                                    int tail, int& st, int& n) {
-    return trim_and_cut_t(p, Bytes{seq}, PtrQual{qual}, l, front, tail, st, n);
+template <class P>
+__device__ inline bool trim_and_cut(const fq_params& p, P seq, P qual, int l, int front, int tail, int& st, int& n) {
+    return trim_and_cut_t(p, Bytes<P>{seq}, PtrQual<P>{qual}, l, front, tail, st, n);
 }
-__device__ inline int trim_polyg(const uint8_t* d, int rlen, int compareReq, int maxMM, int per, int& bases) {
-    return trim_polyg_t(Bytes{d}, rlen, compareReq, maxMM, per, bases);
+template <class P>
+__device__ inline int trim_polyg(P d, int rlen, int compareReq, int maxMM, int per, int& bases) {
+    return trim_polyg_t(Bytes<P>{d}, rlen, compareReq, maxMM, per, bases);
 }
-__device__ inline int trim_polyx(const uint8_t* d, int rlen, int mask, int compareReq, int maxMM, int per, int& poly,
-                                 int& bases) {
-    return trim_polyx_t(Bytes{d}, rlen, mask, compareReq, maxMM, per, poly, bases);
+template <class P>
+__device__ inline int trim_polyx(P d, int rlen, int mask, int compareReq, int maxMM, int per, int& poly, int& bases) {
+    return trim_polyx_t(Bytes<P>{d}, rlen, mask, compareReq, maxMM, per, poly, bases);
 }
 
 struct Overlap {
@@ -300,8 +315,8 @@ struct Overlap {
 
 // OverlapAnalysis::analyze, reference src/overlapanalysis.cpp:7-72, on views.
 // revcomp(s2)[i] = comp(s2[len2-1-i]) is formed on the fly.
-__device__ inline Overlap analyze(const uint8_t* s1, int len1, const uint8_t* s2, int len2, int limit,
-                                  int require) {
+template <class P>
+__device__ inline Overlap analyze(P s1, int len1, P s2, int len2, int limit, int require) {
     const int ccr = 50;
     Overlap r;
     for (int offset = 0; offset < len1 - require; ++offset) {
@@ -370,8 +385,9 @@ __device__ inline bool trim_by_sequence_t(SQ r, int rlen, const uint8_t* ad, int
     }
     return false;
 }
-__device__ inline bool trim_by_sequence(const uint8_t* r, int rlen, const uint8_t* ad, int alen, int& pos_out) {
-    return trim_by_sequence_t(Bytes{r}, rlen, ad, alen, pos_out);
+template <class P>
+__device__ inline bool trim_by_sequence(P r, int rlen, const uint8_t* ad, int alen, int& pos_out) {
+    return trim_by_sequence_t(Bytes<P>{r}, rlen, ad, alen, pos_out);
 }
 
 }  // namespace fqdev

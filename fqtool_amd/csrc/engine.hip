@@ -22,7 +22,7 @@ struct fq_engine {
     size_t acc_words = 0;
     int* err = nullptr;
     // staging for the host-memory path
-    uint8_t* d_rows = nullptr;  // 4 x max_batch x max_stride
+    uint8_t* d_rows = nullptr;  // 4 planes of fq_batch_bytes(max_batch, max_stride)
     uint16_t* d_lens = nullptr;  // 2 x max_batch
     fq_read_result* d_res = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -106,7 +106,7 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     if ((he = hipMemset(e->acc, 0, e->acc_words * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
     if ((he = hipMemset(e->err, 0, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
     if (max_batch > 0 && max_stride > 0) {
-        const size_t rows = (size_t)4 * max_batch * max_stride;
+        const size_t rows = (size_t)4 * fq_batch_bytes(max_batch, max_stride);
         if ((he = hipMalloc(&e->d_rows, rows)) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc rows"));
         if ((he = hipMalloc(&e->d_lens, (size_t)2 * max_batch * sizeof(uint16_t))) != hipSuccess)
             return bail(hip_fail(e, he, "hipMalloc lens"));
@@ -206,8 +206,8 @@ int fq_engine_process(fq_engine* e, const fq_batch* hb, fq_read_result* results)
             return fail(e, FQ_E_TOO_LONG, "read longer than max_cycles / stride");
     }
     HIP_TRY(e, hipSetDevice(e->device));
-    const size_t rowbytes = (size_t)hb->n * hb->stride;
-    const size_t plane = (size_t)e->max_batch * e->max_stride;
+    const size_t rowbytes = fq_batch_bytes(hb->n, hb->stride);
+    const size_t plane = fq_batch_bytes(e->max_batch, e->max_stride);
     fq_batch db;
     db.n = hb->n;
     db.stride = hb->stride;

@@ -8,7 +8,8 @@
 // Occupancy: 2 workgroups (16 waves) per CU; the only per-wave LDS is the 2-bit code / N-mask
 // column block (5 KB), and the workgroup's Stats histograms are shared by its 8 waves.
 //
-// Staging: each lane streams its seq and qual rows from HBM with 16-byte loads.  Sequence bytes
+// Staging: each lane streams its seq and qual rows from HBM with 16-byte loads (the batch's
+// chunk-interleaved tiles make each wave-wide chunk load contiguous).  Sequence bytes
 // are reduced in registers to 2-bit base codes (A=0 C=1 T=2 G=3, N=3, i.e. (byte>>1)&3) plus a
 // spaced N mask and go to the lane's own LDS column (word field*64 + lane: conflict-free for any
 // per-lane position).  Read 1 codes are stored forward; read 2's column is the reverse complement
@@ -234,6 +235,20 @@ __device__ inline int ov_scan(const uint32_t* col, int cm, int mpos0, int k0, in
     return -1;
 }
 
+// the 8 two-bit fields of x's low half, each widened to a nibble
+__device__ __forceinline__ uint32_t spread2to4(uint32_t x) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    return (x | (x << 2)) & 0x33333333u;
+}
+
+
+// Removed-mode Stats rows: [cycle / 16][12 slots][cycle % 16] u64 cells per mate, slot =
+// 4 * kept + code for A C T G (codes 0-3), 8 + kept for N, 10 for positions beyond the read.
+constexpr int kRSlots = 12;
+__host__ __device__ constexpr int rcell(int c, int slot) { return ((c >> 4) * kRSlots + slot) * 32 + 2 * (c & 15); }
+
 __device__ __forceinline__ uint32_t gmask(const Fwd& f) { return ~fold2(~f.c) & ~f.n & 0x55555555u; }
 
 // PolyX::trimPolyG (src/polyx.cpp:14-38) on the code columns.  The scan from the 3' end changes
@@ -284,6 +299,8 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int
 }
 
 __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
+
+typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // a u64 at an LDS byte address
 
 // Profiling aid: per-phase wave cycles (s_memtime deltas summed over waves), compiled in with
 // -DFQ_PHASE_STAMPS (make STAMPS=1), collected when fq_params.reserved[1] != 0 and read back with
@@ -379,12 +396,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         const int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
 
         // ---------------- staging ----------------
-        const size_t roff = (size_t)(valid ? idx : 0) * b.stride;
+        // chunk-interleaved batch tiles (include/fqengine.h): chunk k of this lane's row is 512 B
+        // after chunk k-1, so each chunk load of the wave is one (PE: two planes x 32 rows) or
+        // two (SE: 64 rows) 512-byte contiguous runs
+        constexpr int cst = FQ_TILE_READS * FQ_CHUNK;
+        const int ridx = valid ? idx : 0;
+        const size_t roff = (size_t)(ridx / FQ_TILE_READS) * FQ_TILE_READS * b.stride + (ridx % FQ_TILE_READS) * FQ_CHUNK;
         const uint8_t* S = (mate ? b.seq2 : b.seq1) + roff;
         const uint8_t* Q = (mate ? b.qual2 : b.qual1) + roff;
         // quality chunk F of this lane's row: from the LDS row (full) or the row in L2 (LEAN)
         auto qchunk = [&](int F) -> uint4 {
-            if (LEAN) return *reinterpret_cast<const uint4*>(Q + 16 * F);
+            if (LEAN) return *reinterpret_cast<const uint4*>(Q + cst * F);
             return make_uint4(qrow[4 * F], qrow[4 * F + 1], qrow[4 * F + 2], qrow[4 * F + 3]);
         };
         // (merge: a merged read, at most len1 + len2 long, must fit max_cycles as well)
@@ -409,15 +431,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         uint4 sb[kChunks], qb[kChunks];
 #pragma unroll
         for (int k = 0; k < kAhead && k < kChunks; ++k) {
-            sb[k] = *reinterpret_cast<const uint4*>(S + 16 * min(k, lastc));
-            qb[k] = *reinterpret_cast<const uint4*>(Q + 16 * min(k, lastc));
+            sb[k] = *reinterpret_cast<const uint4*>(S + cst * min(k, lastc));
+            qb[k] = *reinterpret_cast<const uint4*>(Q + cst * min(k, lastc));
         }
 #pragma unroll
         for (int k = 0; k < kChunks; ++k) {
             const uint4 s4 = sb[k], q4 = qb[k];
             if (k + kAhead < kChunks) {
-                sb[k + kAhead] = *reinterpret_cast<const uint4*>(S + 16 * min(k + kAhead, lastc));
-                qb[k + kAhead] = *reinterpret_cast<const uint4*>(Q + 16 * min(k + kAhead, lastc));
+                sb[k + kAhead] = *reinterpret_cast<const uint4*>(S + cst * min(k + kAhead, lastc));
+                qb[k + kAhead] = *reinterpret_cast<const uint4*>(Q + cst * min(k + kAhead, lastc));
             }
 #if FQ_SCHED_PIN
             // keep the loads where they are: left alone, the scheduler hoists them all to the top
@@ -750,7 +772,86 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 
         FQ_STAMP(5)
         // ---------------- Stats::statRead, pre and post (src/peprocessor.cpp:276-277,400-401) ----
-        if (valid && !(abl & 4)) {
+        if (valid && !(abl & 4) && removed_mode) {
+            // Every kept window is a prefix [0, wlen): each base goes to exactly one cell, kept or
+            // removed (pre = kept + removed at the flush), one LDS atomic per base.  Per chunk the
+            // 16 slot numbers are built as nibbles (SWAR), rotated by r positions like the
+            // qualities, so a base costs a nibble extract, an address and a byte extract.
+            const int wlen = post_on ? wn : 0;
+            const int dsel = r >> 2, rr4 = 4 * (r & 7);
+            const bool rswap = r >= 8;
+            // LDS byte address of rotated position t's cell in slot 0 of chunk 0 (this mate's rows)
+            uint32_t rwb[16];
+            const uint32_t blk0 = (uint32_t)(LY::kColsW + mate * (kRSlots * 32 * kChunks)) * 4u;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                rwb[t] = blk0 + 8u * (uint32_t)((t + r) & 15);
+                asm volatile("" : "+v"(rwb[t]));  // kept whole (not re-split into base + offset per use)
+            }
+            Fwd fn = fwd_chunk(col, lane_x, 0, rc);
+            uint4 qn = qchunk(0);
+            uint4 qnn = qchunk(min(1, nchunks - 1));
+#pragma unroll
+            for (int F = 0; F < kChunks; ++F) {
+                if (F < nch) {  // wave-uniform; positions >= L are dummies
+                    const Fwd f = fn;
+                    const uint32_t q0 = qn.x, q1 = qn.y, q2 = qn.z, q3 = qn.w;
+                    qn = qnn;
+                    if (F + 2 < kChunks) qnn = qchunk(min(F + 2, nchunks - 1));
+                    if (F + 1 < kChunks) fn = fwd_chunk(col, lane_x, min(F + 1, nchunks - 1), rc);
+                    const int kl = wlen - 16 * F, vl = L - 16 * F;
+                    // slot 4 * kept + code; an N (code 3) is counted as a G here and moved below
+                    uint32_t lo = spread2to4(f.c) + (kl >= 8 ? 0x44444444u : __builtin_amdgcn_ubfe(0x44444444u, 0, 4 * max(kl, 0)));
+                    uint32_t hi = spread2to4(f.c >> 16) + (kl >= 16 ? 0x44444444u : __builtin_amdgcn_ubfe(0x44444444u, 0, 4 * min(max(kl - 8, 0), 7)));
+                    if (__any(vl < 16)) {  // positions beyond the read (kept is 0 there) -> dummy slot 10
+                        const uint32_t dlo = vl >= 8 ? 0u : ~__builtin_amdgcn_ubfe(~0u, 0, 4 * max(vl, 0));
+                        const uint32_t dhi = vl >= 16 ? 0u : ~__builtin_amdgcn_ubfe(~0u, 0, 4 * min(max(vl - 8, 0), 7));
+                        lo = (lo & ~dlo) | (dlo & 0xAAAAAAAAu);
+                        hi = (hi & ~dhi) | (dhi & 0xAAAAAAAAu);
+                    }
+                    // N bases (rare): move each from its G cell (slot 4 * kept + 3) to slot 8 + kept
+                    uint32_t nv = f.n & posmask(vl);
+                    if (__any(nv != 0)) {
+                        const uint32_t qs[4] = {q0 | 0x80808080u, q1 | 0x80808080u, q2 | 0x80808080u, q3 | 0x80808080u};
+                        while (nv) {
+                            const int t = (__ffs(nv) - 1) >> 1;
+                            nv &= nv - 1;
+                            const int kept = 16 * F + t < wlen ? 1 : 0;
+                            const unsigned long long v = kCount1 | (unsigned long long)__builtin_amdgcn_ubfe(qs[t >> 2], 8 * (t & 3), 8);
+                            const uint32_t a = (uint32_t)(LY::kColsW + mate * (kRSlots * 32 * kChunks)) * 4u +
+                                               (uint32_t)(F * kRSlots * 32 * 4) + 8u * (uint32_t)t;
+                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(8 + kept) * 128u)), v,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(4 * kept + 3) * 128u)), 0ull - v,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    }
+                    // rotate by r positions: rotated position t is 16F + (t + r) % 16
+                    const uint32_t xa = rswap ? hi : lo, xb = rswap ? lo : hi;
+                    const uint32_t klo = __builtin_amdgcn_alignbit(xb, xa, rr4), khi = __builtin_amdgcn_alignbit(xa, xb, rr4);
+                    const uint32_t t0 = (dsel & 1) ? q1 : q0, t1 = (dsel & 1) ? q2 : q1;
+                    const uint32_t t2 = (dsel & 1) ? q3 : q2, t3 = (dsel & 1) ? q0 : q3;
+                    const uint32_t a0 = (dsel & 2) ? t2 : t0, a1 = (dsel & 2) ? t3 : t1;
+                    const uint32_t a2 = (dsel & 2) ? t0 : t2, a3 = (dsel & 2) ? t1 : t3;
+                    // qualities + 128 (bytes are < 128 here): the low word of a cell increment
+                    const uint32_t qr[4] = {__builtin_amdgcn_alignbyte(a1, a0, r & 3) | 0x80808080u,
+                                            __builtin_amdgcn_alignbyte(a2, a1, r & 3) | 0x80808080u,
+                                            __builtin_amdgcn_alignbyte(a3, a2, r & 3) | 0x80808080u,
+                                            __builtin_amdgcn_alignbyte(a0, a3, r & 3) | 0x80808080u};
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) {
+                        const uint32_t ks = __builtin_amdgcn_ubfe(t < 8 ? klo : khi, 4 * (t & 7), 4);
+                        const uint32_t qv = __builtin_amdgcn_ubfe(qr[t >> 2], 8 * (t & 3), 8);
+                        uint32_t a;  // (ks << 7) + rwb[t] in one instruction
+                        asm("v_lshl_add_u32 %0, %1, 7, %2" : "=v"(a) : "v"(ks), "v"(rwb[t]));
+                        a += (uint32_t)(F * kRSlots * 32 * 4);  // (folds into the ds offset)
+                        __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)a), kCount1 | (unsigned long long)qv,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+        }
+        if (valid && !(abl & 4) && !removed_mode) {
             const int wlen = post_on ? wn : 0;  // post window [ws, ws + wlen)
             // merged pairs: both parts go to read 1's post block, read 2's part reversed and
             // complemented (merged cycle c0 - pos)
@@ -790,23 +891,20 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                         const int slot = (int)(((cr >> (2 * tt)) & 3u) + ((nr >> (2 * tt)) & 1u));
                         const unsigned long long v = kCount1 | (unsigned long long)(qv | 0x80u);
                         if (!(abl & 16)) {
-                            const int cl = cell(pos, pos < L ? slot : kDummySlot);
-                            if (removed_mode) {
-                                hadd(pos < wlen ? my_post : my_pre, cl, v);  // kept : removed
-                            } else {
-                                hadd(my_pre, cl, v);
-                                const bool inw = (unsigned)(pos - ws) < (unsigned)wlen;
-                                int cyc = pos - ws, sl = slot;
-                                if (MERGE && rev) {
-                                    cyc = c0 - pos;
-                                    sl = slot < 4 ? slot ^ 2 : 4;  // A<->T, C<->G
-                                }
-                                hadd(post_h, inw ? cell(cyc, sl) : cell(pos, kDummySlot), v);
+                            hadd(my_pre, cell(pos, pos < L ? slot : kDummySlot), v);
+                            const bool inw = (unsigned)(pos - ws) < (unsigned)wlen;
+                            int cyc = pos - ws, sl = slot;
+                            if (MERGE && rev) {
+                                cyc = c0 - pos;
+                                sl = slot < 4 ? slot ^ 2 : 4;  // A<->T, C<->G
                             }
+                            hadd(post_h, inw ? cell(cyc, sl) : cell(pos, kDummySlot), v);
                         }
                     }
                 }
             }
+        }
+        if (valid && !(abl & 4)) {
             // per-read scalars straight to LDS (lanes l, l+16 share a copy): nothing stays live
             unsigned long long* sc = scal + 16 * (lane_x & 15) + 4 * mate;
             sadd(&sc[0], 1ull);
@@ -861,16 +959,34 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         for (int c = 0; c < kScalCopies; ++c) v += scal[16 * c + threadIdx.x];
         if (v) atomicAdd(&acc[st_base + k * st_words + f], v);
     }
-    for (int k = 0; k < 4; ++k) {
+    if (removed_mode) {  // pre = kept + removed, post = kept
+        const int ncyc = min(kMaxLen, p.max_cycles);
+        for (int i = threadIdx.x; i < 2 * ncyc * 5; i += kThreads) {
+            const int k = i / (ncyc * 5), j = i - k * ncyc * 5;
+            const int c = j / 5, slot = j - c * 5;  // slots A C T G N
+            const uint32_t* hk = hist + k * (kRSlots * 32 * kChunks);
+            const unsigned long long kept = *reinterpret_cast<const unsigned long long*>(hk + rcell(c, slot < 4 ? 4 + slot : 9));
+            const unsigned long long rem = *reinterpret_cast<const unsigned long long*>(hk + rcell(c, slot < 4 ? slot : 8));
+            const int cls = slot_class(slot);
+            const unsigned long long vals[2] = {kept + rem, kept};
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+                const long long cnt = (long long)(vals[pp] >> 40);
+                const long long qs = (long long)(vals[pp] & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
+                if (cnt == 0 && qs == 0) continue;
+                unsigned long long* dst = acc + st_base + (k + 2 * pp) * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
+                atomicAdd(&dst[cls], (unsigned long long)cnt);
+                atomicAdd(&dst[8 + cls], (unsigned long long)qs);
+            }
+        }
+    }
+    for (int k = 0; k < 4 && !removed_mode; ++k) {
       const int ncyc = min((MERGE && k == 2) ? 2 * kMaxLen : kMaxLen, p.max_cycles);
       const uint32_t* hk = hist + (k == 3 && MERGE ? 4 : k) * kHistW;
       for (int i = threadIdx.x; i < ncyc * 5; i += kThreads) {
         const int c = i / 5, slot = i - c * 5;
         const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hk + cell(c, slot));
-        // removed mode: pre = removed (this block) + kept (the post block); post = kept
-        const unsigned long long w =
-            v + ((k < 2 && removed_mode) ? *reinterpret_cast<const unsigned long long*>(hk + 2 * kHistW + cell(c, slot))
-                                         : 0ull);
+        const unsigned long long w = v;
         const long long cnt = (long long)(w >> 40);
         const long long qs = (long long)(w & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
         if (cnt == 0 && qs == 0) continue;

@@ -3,7 +3,7 @@
 // One lane owns one pair (PE) or one read (SE) and runs the loop body of
 // PairEndProcessor::processPairEnd (reference src/peprocessor.cpp:261-508) /
 // SingleEndProcessor::processSingleEnd (src/seprocessor.cpp:290-388) on read *views* over the
-// row-major batch in HBM; trimming only moves (start, len), nothing is copied.
+// batch rows in HBM (chunk-interleaved tiles, include/fqengine.h); trimming only moves (start, len), nothing is copied.
 //
 // Accumulation (the ThreadConfig-owned Stats x4 + FilterResult and the insert histogram):
 // every workgroup privatises all counters in LDS and flushes them once with 64-bit global
@@ -77,8 +77,7 @@ __device__ inline void stat_read(const Smem& sm, int k, int len, int skew, Fetch
     lds_add64(&scal[3], (unsigned long long)q30);
 }
 
-__device__ __forceinline__ void row_stat(const Smem& sm, int k, int C, const uint8_t* s, const uint8_t* q,
-                                         int len, int skew) {
+__device__ __forceinline__ void row_stat(const Smem& sm, int k, int C, Row s, Row q, int len, int skew) {
     (void)C;
     stat_read(sm, k, len, skew, [&](int i, uint8_t& b, int& qq) {
         b = s[i];
@@ -100,7 +99,7 @@ __device__ __forceinline__ fq_read_result make_result(bool nonnull, int start, i
     return r;
 }
 
-__device__ inline void apply_polyg(const fq_params& p, const Smem& sm, const uint8_t* s, int st, int& n) {
+__device__ inline void apply_polyg(const fq_params& p, const Smem& sm, Row s, int st, int& n) {
     int bases;
     n = trim_polyg(s + st, n, p.polyg_compare_req, p.polyg_max_mismatch, p.polyg_one_mismatch_per, bases);
     if (bases >= 0) {
@@ -109,7 +108,7 @@ __device__ inline void apply_polyg(const fq_params& p, const Smem& sm, const uin
     }
 }
 
-__device__ inline void apply_polyx(const fq_params& p, const Smem& sm, const uint8_t* s, int st, int& n) {
+__device__ inline void apply_polyx(const fq_params& p, const Smem& sm, Row s, int st, int& n) {
     int poly, bases;
     n = trim_polyx(s + st, n, p.polyx_mask, p.polyx_compare_req, p.polyx_max_mismatch, p.polyx_one_mismatch_per,
                    poly, bases);
@@ -119,7 +118,7 @@ __device__ inline void apply_polyx(const fq_params& p, const Smem& sm, const uin
     }
 }
 
-__device__ inline void apply_adapter_seq(const Smem& sm, const uint8_t* s, int st, int& n, const uint8_t* ad,
+__device__ inline void apply_adapter_seq(const Smem& sm, Row s, int st, int& n, const uint8_t* ad,
                                          int alen, fq_read_result& rr) {
     int pos;
     if (!trim_by_sequence(s + st, n, ad, alen, pos)) return;
@@ -161,14 +160,13 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
     __syncthreads();
 
     const int skew = threadIdx.x & 63;
-    const size_t stride = (size_t)b.stride;
     // all pairs of the pack, or (tile-list mode) the 32-pair tiles the fast kernel handed over
     const int total = tiles ? *ntiles * 32 : b.n;
     for (int item = blockIdx.x * blockDim.x + threadIdx.x; item < total; item += gridDim.x * blockDim.x) {
         const int idx = tiles ? tiles[item >> 5] * 32 + (item & 31) : item;
         if (idx >= b.n) continue;
-        const uint8_t* s1 = b.seq1 + idx * stride;
-        const uint8_t* q1 = b.qual1 + idx * stride;
+        const Row s1 = batch_row(b.seq1, b.stride, idx);
+        const Row q1 = batch_row(b.qual1, b.stride, idx);
         const int l1 = b.len1[idx];
         if (!PAIRED) {
             if (l1 > C || l1 > b.stride) {
@@ -192,8 +190,8 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
             if (res) store_result(&res[idx], rr);
             continue;
         }
-        const uint8_t* s2 = b.seq2 + idx * stride;
-        const uint8_t* q2 = b.qual2 + idx * stride;
+        const Row s2 = batch_row(b.seq2, b.stride, idx);
+        const Row q2 = batch_row(b.qual2, b.stride, idx);
         const int l2 = b.len2[idx];
         if (l1 > C || l2 > C || l1 > b.stride || l2 > b.stride) {
             atomicOr(err, 1);
@@ -256,10 +254,10 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
                     r1.m_len1 = (uint16_t)m1;
                     r1.m_len2 = (uint16_t)m2;
                     const int mlen = m1 + m2;
-                    const uint8_t* a_s = s1 + st1;
-                    const uint8_t* a_q = q1 + st1;
-                    const uint8_t* b_s = s2 + st2;
-                    const uint8_t* b_q = q2 + st2;
+                    const Row a_s = s1 + st1;
+                    const Row a_q = q1 + st1;
+                    const Row b_s = s2 + st2;
+                    const Row b_q = q2 + st2;
                     // merged base i: r1[i] for i < m1, else revcomp(r2)[ol + i - m1]
                     auto fetch = [&](int i, uint8_t& bb, int& qq) {
                         if (i < m1) {

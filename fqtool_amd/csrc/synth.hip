@@ -43,8 +43,10 @@ __global__ void synth_kernel(fq_batch b, uint64_t seed, uint64_t first, int L) {
     const uint64_t rm = sm64(key + 2 + (uint64_t)mate);
     const int polyg = ((rm & 0xFFFF) % 100 < 5) ? 10 + (int)(((rm >> 16) & 0xFFFF) % 51) : 0;
     const int lowq = (((rm >> 32) & 0xFFFF) % 100 < 2) ? 100 + (int)((rm >> 48) % 51) : L;
-    uint8_t* seq = (uint8_t*)(mate ? b.seq2 : b.seq1) + (size_t)pair * b.stride;
-    uint8_t* qual = (uint8_t*)(mate ? b.qual2 : b.qual1) + (size_t)pair * b.stride;
+    // the read's chunk 0 in the chunk-interleaved batch tiles; byte i at (i / 16) * 512 + i % 16
+    const size_t roff = (size_t)(pair / FQ_TILE_READS) * FQ_TILE_READS * b.stride + (pair % FQ_TILE_READS) * FQ_CHUNK;
+    uint8_t* seq = (uint8_t*)(mate ? b.seq2 : b.seq1) + roff;
+    uint8_t* qual = (uint8_t*)(mate ? b.qual2 : b.qual1) + roff;
     uint32_t sw = 0, qw = 0;
     for (int i = 0; i < L; ++i) {
         uint8_t base;
@@ -72,8 +74,9 @@ __global__ void synth_kernel(fq_batch b, uint64_t seed, uint64_t first, int L) {
         sw |= (uint32_t)base << (8 * (i & 3));
         qw |= (uint32_t)(q + 33) << (8 * (i & 3));
         if ((i & 3) == 3 || i == L - 1) {
-            *reinterpret_cast<uint32_t*>(seq + (i & ~3)) = sw;
-            *reinterpret_cast<uint32_t*>(qual + (i & ~3)) = qw;
+            const size_t o = (size_t)(i >> 4) * (FQ_TILE_READS * FQ_CHUNK) + (i & 12);
+            *reinterpret_cast<uint32_t*>(seq + o) = sw;
+            *reinterpret_cast<uint32_t*>(qual + o) = qw;
             sw = qw = 0;
         }
     }

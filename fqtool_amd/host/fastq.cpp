@@ -129,8 +129,9 @@ bool PackReader::next(Pack& pk, size_t max_n) {
     for (int m = 0; m < 2; ++m) {
         pk.name[m].clear();
         pk.strand[m].clear();
+        pk.seq_text[m].clear();
+        pk.qual_text[m].clear();
     }
-    std::vector<std::string> seqs[2], quals[2];
     size_t maxlen = 0;
     std::string nm, sq, sd, ql;
     while ((size_t)pk.n < max_n) {
@@ -148,8 +149,8 @@ bool PackReader::next(Pack& pk, size_t max_n) {
             maxlen = std::max(maxlen, seqv[m].size());
             pk.name[m].push_back(std::move(names[m]));
             pk.strand[m].push_back(std::move(strands[m]));
-            seqs[m].push_back(std::move(seqv[m]));
-            quals[m].push_back(std::move(qualv[m]));
+            pk.seq_text[m].push_back(std::move(seqv[m]));
+            pk.qual_text[m].push_back(std::move(qualv[m]));
         }
         ++pk.n;
     }
@@ -157,14 +158,20 @@ bool PackReader::next(Pack& pk, size_t max_n) {
     if (maxlen > 65535) throw std::runtime_error("read longer than 65535 bases");
     pk.stride = (int)std::max<size_t>(16, (maxlen + 15) & ~(size_t)15);
     for (int m = 0; m < mates; ++m) {
-        pk.seq[m].assign((size_t)pk.n * pk.stride, 0);
-        pk.qual[m].assign((size_t)pk.n * pk.stride, 0);
+        const size_t bytes = fq_batch_bytes(pk.n, pk.stride);
+        pk.seq[m].assign(bytes, 0);
+        pk.qual[m].assign(bytes, 0);
         pk.len[m].resize((size_t)pk.n);
         for (int i = 0; i < pk.n; ++i) {
-            const std::string& s = seqs[m][i];
-            const std::string& q = quals[m][i];
-            std::memcpy(&pk.seq[m][(size_t)i * pk.stride], s.data(), s.size());
-            std::memcpy(&pk.qual[m][(size_t)i * pk.stride], q.data(), q.size());
+            const std::string& s = pk.seq_text[m][i];
+            const std::string& q = pk.qual_text[m][i];
+            // chunk-interleaved tiles: 16-byte pieces of the row, 512 bytes apart
+            for (size_t j = 0; j < s.size(); j += FQ_CHUNK) {
+                const size_t k = std::min<size_t>(FQ_CHUNK, s.size() - j);
+                const size_t o = fq_batch_offset(pk.stride, i, (int32_t)j);
+                std::memcpy(&pk.seq[m][o], s.data() + j, k);
+                std::memcpy(&pk.qual[m][o], q.data() + j, k);
+            }
             pk.len[m][i] = (uint16_t)s.size();
         }
     }

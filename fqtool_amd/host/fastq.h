@@ -42,19 +42,22 @@ class FqReader {
     bool eof_ = false;
 };
 
-// One pack of reads (pairs when paired): engine rows + text fields.
+// One pack of reads (pairs when paired): the engine's batch planes (chunk-interleaved tiles,
+// include/fqengine.h) + the records' text fields, kept for output formatting.
 struct Pack {
     int n = 0;
     int stride = 0;
     bool paired = false;
-    std::vector<uint8_t> seq[2], qual[2];
+    std::vector<uint8_t> seq[2], qual[2];  // batch planes
+    std::vector<std::string> seq_text[2], qual_text[2];
     std::vector<uint16_t> len[2];
     std::vector<std::string> name[2], strand[2];
     uint64_t seq_no = 0;
     fq_batch batch() const;
 };
 
-// Reads up to max_n records (pairs) into a pack; rows are padded to a multiple of 16 bytes.
+// Reads up to max_n records (pairs) into a pack; rows are padded to a multiple of 16 bytes and
+// the planes to whole tiles.
 // Returns false when no record could be read.
 class PackReader {
    public:

@@ -53,8 +53,8 @@ struct View {
 };
 
 View view(const Pack& pk, int m, int i, const fq_read_result* r) {
-    const char* s = reinterpret_cast<const char*>(pk.seq[m].data()) + (size_t)i * pk.stride;
-    const char* q = reinterpret_cast<const char*>(pk.qual[m].data()) + (size_t)i * pk.stride;
+    const char* s = pk.seq_text[m][(size_t)i].data();
+    const char* q = pk.qual_text[m][(size_t)i].data();
     View v{&pk.name[m][(size_t)i], &pk.strand[m][(size_t)i], s, q, (int)pk.len[m][(size_t)i]};
     if (r && !(r->flags & FQ_RF_NULL)) {  // trimmed in place; a NULL read keeps the original
         v.seq += r->start;

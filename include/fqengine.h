@@ -14,7 +14,8 @@
  * This header replaces that seam with plain pointers and sizes (no C++ / torch types):
  *   - fq_params       : POD snapshot of every derived Options field the loop body reads
  *                        (src/options.h:15-386 after Options::update, src/options.cpp:24-58)
- *   - fq_batch        : one pack of reads as SoA uint8 seq/qual rows + uint16 lengths
+ *   - fq_batch        : one pack of reads as SoA uint8 seq/qual planes (chunk-interleaved
+ *                        tiles, see below) + uint16 lengths
  *                        (replaces ReadPairPack / ReadPack, src/peprocessor.h:28-31)
  *   - fq_read_result  : per-read trim window + filter code + adapter/merge descriptors, i.e.
  *                        everything the in-place std::string mutations of the loop body produce
@@ -34,7 +35,7 @@
 extern "C" {
 #endif
 
-#define FQ_ABI_VERSION 1
+#define FQ_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define FQ_OK 0
@@ -119,7 +120,17 @@ typedef struct fq_params {
     int32_t reserved[7];
 } fq_params;
 
-/* One pack of reads, row-major: read i's bases are seq[i*stride .. i*stride+len[i]). */
+/* One pack of reads.  Each plane (seq1, qual1, seq2, qual2) holds every read's row of `stride`
+ * bytes in CHUNK-INTERLEAVED TILES: reads are grouped in tiles of FQ_TILE_READS consecutive reads,
+ * and inside a tile the 16-byte chunk k of all its reads is stored together, so
+ *     byte j of read i  is at  plane[fq_batch_offset(stride, i, j)]
+ *                          =  (i / 32) * 32 * stride + (j / 16) * 512 + (i % 32) * 16 + j % 16.
+ * One wave-wide load of chunk k of 32 (or 64) reads is then one (or two) 512-byte contiguous runs
+ * instead of 64 rows touched 16 bytes at a time.  A plane spans fq_batch_bytes(n, stride) bytes
+ * (whole tiles; the padding rows are never read as reads).  Bytes j >= len[i] of a row are
+ * ignored.  Packers: fq_batch_offset / fq_batch_put_row below. */
+#define FQ_TILE_READS 32
+#define FQ_CHUNK 16
 typedef struct fq_batch {
     int32_t n;      /* number of pairs (PE) or reads (SE) */
     int32_t stride; /* bytes per row, multiple of 16, >= every len */
@@ -130,6 +141,35 @@ typedef struct fq_batch {
     const uint8_t* qual2;
     const uint16_t* len2;
 } fq_batch;
+
+static inline size_t fq_batch_offset(int32_t stride, int64_t i, int32_t j) {
+    return (size_t)(i / FQ_TILE_READS) * FQ_TILE_READS * (size_t)stride +
+           (size_t)(j / FQ_CHUNK) * (FQ_TILE_READS * FQ_CHUNK) + (size_t)(i % FQ_TILE_READS) * FQ_CHUNK +
+           (size_t)(j % FQ_CHUNK);
+}
+static inline size_t fq_batch_bytes(int64_t n, int32_t stride) {
+    return (size_t)((n + FQ_TILE_READS - 1) / FQ_TILE_READS) * FQ_TILE_READS * (size_t)stride;
+}
+/* copy `len` bytes of `src` into read i's row of a plane (len <= stride) */
+static inline void fq_batch_put_row(uint8_t* plane, int32_t stride, int64_t i, const uint8_t* src, int32_t len) {
+    int32_t j;
+    for (j = 0; j < len; j += FQ_CHUNK) {
+        const int32_t m = len - j < FQ_CHUNK ? len - j : FQ_CHUNK;
+        const size_t o = fq_batch_offset(stride, i, j);
+        int32_t k;
+        for (k = 0; k < m; ++k) plane[o + k] = src[j + k];
+    }
+}
+/* copy read i's first `len` row bytes out of a plane */
+static inline void fq_batch_get_row(const uint8_t* plane, int32_t stride, int64_t i, uint8_t* dst, int32_t len) {
+    int32_t j;
+    for (j = 0; j < len; j += FQ_CHUNK) {
+        const int32_t m = len - j < FQ_CHUNK ? len - j : FQ_CHUNK;
+        const size_t o = fq_batch_offset(stride, i, j);
+        int32_t k;
+        for (k = 0; k < m; ++k) dst[j + k] = plane[o + k];
+    }
+}
 
 /* fq_read_result.flags */
 #define FQ_RF_NULL 0x01      /* trimAndCut returned NULL (src/filter.cpp:78,100,124,160,183) */

@@ -15,6 +15,14 @@
 
 static inline int qv(const uint8_t* q, int i) { return (int)(signed char)q[i]; }
 
+/* The batch planes hold rows in chunk-interleaved tiles (include/fqengine.h); the restatement
+ * below works on contiguous reads, gathered here one at a time. */
+static uint8_t g_row[4][65536];
+static const uint8_t* gather(int k, const uint8_t* plane, int stride, int i, int len) {
+    fq_batch_get_row(plane, stride, i, g_row[k], len);
+    return g_row[k];
+}
+
 /* src/filter.cpp:54-67 Filter::passLowComplexityFliter */
 static int low_complexity_pass(const fq_params* p, const uint8_t* seq, int rlen) {
     if (rlen <= 1) return 0;
@@ -370,9 +378,9 @@ static int process_se(const fq_params* p, const fq_batch* b, fq_read_result* res
     uint64_t* pre = acc + fq_acc_stats_offset(p->insert_size_max, p->max_cycles, 0);
     uint64_t* post = acc + fq_acc_stats_offset(p->insert_size_max, p->max_cycles, 2);
     for (int i = 0; i < b->n; ++i) {
-        const uint8_t* seq = b->seq1 + (size_t)i * b->stride;
-        const uint8_t* qual = b->qual1 + (size_t)i * b->stride;
         int l = b->len1[i];
+        const uint8_t* seq = gather(0, b->seq1, b->stride, i, l);
+        const uint8_t* qual = gather(1, b->qual1, b->stride, i, l);
         if (l > p->max_cycles) return FQ_E_TOO_LONG;
         fq_read_result* rr = &res[i];
         orc_stat_read(pre, p->max_cycles, seq, qual, l); /* :298 */
@@ -410,11 +418,11 @@ static int process_pe(const fq_params* p, const fq_batch* b, fq_read_result* res
     uint64_t* post2 = acc + fq_acc_stats_offset(p->insert_size_max, p->max_cycles, 3);
     static uint8_t ms[131072], mq[131072];
     for (int i = 0; i < b->n; ++i) {
-        const uint8_t* s1 = b->seq1 + (size_t)i * b->stride;
-        const uint8_t* q1 = b->qual1 + (size_t)i * b->stride;
-        const uint8_t* s2 = b->seq2 + (size_t)i * b->stride;
-        const uint8_t* q2 = b->qual2 + (size_t)i * b->stride;
         int l1 = b->len1[i], l2 = b->len2[i];
+        const uint8_t* s1 = gather(0, b->seq1, b->stride, i, l1);
+        const uint8_t* q1 = gather(1, b->qual1, b->stride, i, l1);
+        const uint8_t* s2 = gather(2, b->seq2, b->stride, i, l2);
+        const uint8_t* q2 = gather(3, b->qual2, b->stride, i, l2);
         if (l1 > p->max_cycles || l2 > p->max_cycles) return FQ_E_TOO_LONG;
         fq_read_result* rr1 = &res[2 * i];
         fq_read_result* rr2 = &res[2 * i + 1];
@@ -594,12 +602,14 @@ void orc_synth_fill(const fq_batch* b, uint64_t seed, uint64_t first_index, int 
         int64_t ins = 220 + (S - 131070) * 60 / 37837;
         if (ins < 60) ins = 60;
         if (ins > 600) ins = 600;
-        synth_read(key, 0, L, (int)ins, (uint8_t*)b->seq1 + (size_t)p * b->stride,
-                   (uint8_t*)b->qual1 + (size_t)p * b->stride);
+        synth_read(key, 0, L, (int)ins, g_row[0], g_row[1]);
+        fq_batch_put_row((uint8_t*)b->seq1, b->stride, p, g_row[0], L);
+        fq_batch_put_row((uint8_t*)b->qual1, b->stride, p, g_row[1], L);
         ((uint16_t*)b->len1)[p] = (uint16_t)L;
         if (b->seq2) {
-            synth_read(key, 1, L, (int)ins, (uint8_t*)b->seq2 + (size_t)p * b->stride,
-                       (uint8_t*)b->qual2 + (size_t)p * b->stride);
+            synth_read(key, 1, L, (int)ins, g_row[0], g_row[1]);
+            fq_batch_put_row((uint8_t*)b->seq2, b->stride, p, g_row[0], L);
+            fq_batch_put_row((uint8_t*)b->qual2, b->stride, p, g_row[1], L);
             ((uint16_t*)b->len2)[p] = (uint16_t)L;
         }
     }

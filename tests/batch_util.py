@@ -11,7 +11,8 @@ AD2 = "AGATCGGAAGAGCGTCGTGTAGGGAAAGAGTGT"
 
 
 class Pack:
-    """Row-major pack: rows of `stride` bytes, like the engine's fq_batch."""
+    """A pack as (n, stride) row arrays; batch() lays them out as the engine's fq_batch planes
+    (chunk-interleaved tiles, include/fqengine.h) and keeps those buffers alive."""
 
     def __init__(self, n, stride, paired):
         self.n, self.stride, self.paired = n, stride, paired
@@ -31,13 +32,22 @@ class Pack:
         q[i, : len(qual)] = np.frombuffer(qual, np.uint8)
         getattr(self, "len%d" % mate)[i] = len(seq)
 
+    def planes(self):
+        return ("seq1", "qual1", "seq2", "qual2") if self.paired else ("seq1", "qual1")
+
     def batch(self):
+        self._tiled = {k: abi.tile_rows(getattr(self, k)) for k in self.planes()}
         b = abi.FqBatch()
         b.n, b.stride = self.n, self.stride
-        b.seq1, b.qual1, b.len1 = self.seq1.ctypes.data, self.qual1.ctypes.data, self.len1.ctypes.data
+        b.seq1, b.qual1, b.len1 = self._tiled["seq1"].ctypes.data, self._tiled["qual1"].ctypes.data, self.len1.ctypes.data
         if self.paired:
-            b.seq2, b.qual2, b.len2 = self.seq2.ctypes.data, self.qual2.ctypes.data, self.len2.ctypes.data
+            b.seq2, b.qual2, b.len2 = self._tiled["seq2"].ctypes.data, self._tiled["qual2"].ctypes.data, self.len2.ctypes.data
         return b
+
+    def load_batch(self):
+        """Copy the planes of the last batch() back into the row arrays (after a fill)."""
+        for k in self.planes():
+            getattr(self, k)[:] = abi.untile_rows(self._tiled[k], self.n, self.stride)
 
     def result_array(self):
         return np.zeros(self.n * (2 if self.paired else 1), dtype=np.dtype(abi.RESULT_DTYPE_FIELDS))
@@ -47,6 +57,7 @@ def synth_pack(oracle, n, paired, seed=20261015, first=0, L=150, stride=160):
     pk = Pack(n, stride, paired)
     b = pk.batch()
     oracle.orc_synth_fill(ctypes.byref(b), seed, first, L)
+    pk.load_batch()
     return pk
 
 

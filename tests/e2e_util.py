@@ -134,6 +134,8 @@ def run_session_with_oracle(host, orc, argv, max_n=1500):
 
 
 def read_row(b, mate, i, length):
-    seq = ctypes.string_at((b.seq1 if mate == 0 else b.seq2) + i * b.stride, length)
-    qual = ctypes.string_at((b.qual1 if mate == 0 else b.qual2) + i * b.stride, length)
-    return seq, qual
+    def row(plane):
+        return b"".join(ctypes.string_at(plane + abi.batch_offset(b.stride, i, j), min(abi.CHUNK, length - j))
+                        for j in range(0, length, abi.CHUNK))
+
+    return row(b.seq1 if mate == 0 else b.seq2), row(b.qual1 if mate == 0 else b.qual2)

@@ -115,7 +115,7 @@ def test_device_synth_matches_host(eng_lib, oracle):
 
     n, stride, L = 5000, 160, 150
     dev = torch.device("cuda:0")
-    bufs = [torch.zeros(n * stride, dtype=torch.uint8, device=dev) for _ in range(4)]
+    bufs = [torch.zeros(abi.batch_bytes(n, stride), dtype=torch.uint8, device=dev) for _ in range(4)]
     lens = [torch.zeros(n, dtype=torch.int16, device=dev) for _ in range(2)]
     b = abi.FqBatch()
     b.n, b.stride = n, stride
@@ -124,7 +124,7 @@ def test_device_synth_matches_host(eng_lib, oracle):
     assert eng_lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 777, L, None) == 0
     torch.cuda.synchronize()
     pk = synth_pack(oracle, n, True, first=777, L=L, stride=stride)
-    got = [t.cpu().numpy().reshape(n, stride)[:, :L] for t in bufs]
+    got = [abi.untile_rows(t.cpu().numpy(), n, stride)[:, :L] for t in bufs]
     exp = [pk.seq1[:, :L], pk.qual1[:, :L], pk.seq2[:, :L], pk.qual2[:, :L]]
     for g, e in zip(got, exp):
         assert np.array_equal(g, e)
@@ -139,7 +139,7 @@ def test_device_path_accumulates_like_host_path(eng_lib, oracle):
     p = config("C3", max_cycles=256)
     n, stride, L = 20000, 160, 150
     dev = torch.device("cuda:0")
-    bufs = [torch.zeros(n * stride, dtype=torch.uint8, device=dev) for _ in range(4)]
+    bufs = [torch.zeros(abi.batch_bytes(n, stride), dtype=torch.uint8, device=dev) for _ in range(4)]
     lens = [torch.zeros(n, dtype=torch.int16, device=dev) for _ in range(2)]
     res_d = torch.zeros(n * 2 * 16, dtype=torch.uint8, device=dev)
     b = abi.FqBatch()
@@ -150,7 +150,7 @@ def test_device_path_accumulates_like_host_path(eng_lib, oracle):
     torch.cuda.synchronize()
     h = make_engine(eng_lib, p, max_batch=0, max_stride=0)
     try:
-        half = n // 2
+        half = n // 2 // abi.TILE_READS * abi.TILE_READS  # sub-batches start on a tile boundary
         for lo, hi in ((0, half), (half, n)):
             sub = abi.FqBatch()
             sub.n, sub.stride = hi - lo, stride

@@ -8,7 +8,7 @@ from fqtool_amd import abi
 lib = abi.load_engine()
 dev = torch.device("cuda:0")
 n, stride = int(os.environ.get("PAIRS", 20_000_000)), 160
-bufs = [torch.empty(n * stride, dtype=torch.uint8, device=dev) for _ in range(4)]
+bufs = [torch.empty(abi.batch_bytes(n, stride), dtype=torch.uint8, device=dev) for _ in range(4)]
 lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
 b = abi.FqBatch(); b.n, b.stride = n, stride
 b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]

@@ -7,7 +7,7 @@ dev = torch.device("cuda:0")
 p = abi.default_params(True, 256); p.qual_filter_enabled = 1; p.adapter_trimming = 1; p.polyg_enabled = 1
 h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
 for n in [10**4, 10**5, 10**6, 4*10**6, 16*10**6, 64*10**6]:
-    bufs = [torch.empty(n * 160, dtype=torch.uint8, device=dev) for _ in range(4)]
+    bufs = [torch.empty(abi.batch_bytes(n, 160), dtype=torch.uint8, device=dev) for _ in range(4)]
     lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
     b = abi.FqBatch(); b.n, b.stride = n, 160
     b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
