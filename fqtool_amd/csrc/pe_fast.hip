@@ -302,6 +302,26 @@ __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v
 
 typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // a u64 at an LDS byte address
 
+// base[v] += w for every lane with `on`: one LDS atomic per distinct v in the wave instead of one
+// per lane (lanes of a tile mostly share a value, e.g. the filter code 0).  Wave-uniform call.
+__device__ __forceinline__ void count_by_value(unsigned long long* base, bool on, int v, unsigned long long w) {
+    unsigned long long m = __ballot(on);
+    while (m) {
+        const int first = __ffsll((long long)m) - 1;
+        const int c = __builtin_amdgcn_readlane(v, first);
+        const unsigned long long mc = __ballot(on && v == c);
+        m &= ~mc;
+        if ((int)(threadIdx.x & 63) == first) atomicAdd(&base[c], w * (unsigned long long)__popcll(mc));
+    }
+}
+
+// Per-lane counters kept in registers across tiles and added to LDS once at the end (a lane
+// always holds the same mate): polyG and adapter FilterResult counters, Stats scalars.
+struct LaneAcc {
+    uint32_t pg_reads, pg_bases, ad_reads, ad_bases;
+    uint32_t pre_reads, pre_len, pre_q20, pre_q30, post_reads, post_len, post_q20, post_q30;
+};
+
 // Profiling aid: per-phase wave cycles (s_memtime deltas summed over waves), compiled in with
 // -DFQ_PHASE_STAMPS (make STAMPS=1), collected when fq_params.reserved[1] != 0 and read back with
 // fq_debug_phase_cycles().
@@ -341,7 +361,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     __syncthreads();
 
     // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
-    // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics
+    // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics,
+    // 32 skip the polyG counters
     const int abl = p.reserved[0];
     const int ntiles = PAIRED ? (b.n + 31) >> 5 : (b.n + 63) >> 6;
 #if FQ_FIXED_STRIDE  // profiling only: assume rows of >= 160 bytes
@@ -374,6 +395,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 #define FQ_STAMP(i)
 #endif
 
+    LaneAcc la = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
         // Per-lane values are derived from an opaque copy of the lane id inside the loop: left to
         // itself the compiler hoists dozens of them out of the tile loop and spills them.
@@ -549,9 +571,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         if (both && p.polyg_enabled && !(abl & 8)) {
             int bases;
             n = polyg_bits(col, lane, rc, L, st, n, p.polyg_max_mismatch, g_inv, p.polyg_compare_req, bases);
-            if (bases >= 0) {
-                sadd(&small[FQ_ACC_POLYX_READS + 3], 1ull);
-                sadd(&small[FQ_ACC_POLYX_BASES + 3], (unsigned long long)(long long)bases);
+            if (bases >= 0 && !(abl & 32)) {
+                ++la.pg_reads;
+                la.pg_bases += (uint32_t)bases;
             }
         }
 
@@ -574,8 +596,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 }
                 rr.ad_len = (uint16_t)ad_len;
                 if (ad_len > 0) {
-                    sadd(&small[FQ_ACC_ADAPTER_READS], 1ull);
-                    sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)ad_len);
+                    ++la.ad_reads;
+                    la.ad_bases += (uint32_t)ad_len;
                 }
             }
         };
@@ -634,8 +656,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     rr.ad_pos = (uint16_t)(st + ol);
                     rr.ad_len = (uint16_t)(n - ol);
                     if (mate == 0) {
-                        sadd(&small[FQ_ACC_ADAPTER_READS], 2ull);
-                        sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)((n1 - ol) + (n2 - ol)));
+                        la.ad_reads += 2;
+                        la.ad_bases += (uint32_t)((n1 - ol) + (n2 - ol));
                     }
                     n = ol;
                 } else if (!LEAN && my_alen > 0) {
@@ -763,10 +785,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             sadd(&small[FQ_ACC_FILTER + code], 1ull);
             post_on = code == FQ_PASS_FILTER;
         } else if (PAIRED) {
-            if (mate == 0 && valid) sadd(&small[FQ_ACC_FILTER + max(code, code_o)], 2ull);  // addFilterResult: +2
+            // addFilterResult(max(r1, r2), 2)
+            if (MERGE) {
+                if (mate == 0 && valid) sadd(&small[FQ_ACC_FILTER + max(code, code_o)], 2ull);
+            } else {
+                count_by_value(small + FQ_ACC_FILTER, mate == 0 && valid, max(code, code_o), 2ull);
+            }
             post_on = !MERGE && pair_pass;
         } else {
-            if (valid) sadd(&small[FQ_ACC_FILTER + code], 1ull);  // src/seprocessor.cpp:339
+            count_by_value(small + FQ_ACC_FILTER, valid, code, 1ull);  // src/seprocessor.cpp:339
             post_on = pair_pass;
         }
 
@@ -905,24 +932,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             }
         }
         if (valid && !(abl & 4)) {
-            // per-read scalars straight to LDS (lanes l, l+16 share a copy): nothing stays live
-            unsigned long long* sc = scal + 16 * (lane_x & 15) + 4 * mate;
-            sadd(&sc[0], 1ull);
-            sadd(&sc[1], (unsigned long long)L);
-            sadd(&sc[2], (unsigned long long)q20);
-            sadd(&sc[3], (unsigned long long)q30);
+            // per-read Stats scalars
+            ++la.pre_reads;
+            la.pre_len += (uint32_t)L;
+            la.pre_q20 += q20;
+            la.pre_q30 += q30;
             if (MERGE && merged) {
                 if (post_on && mate == 0) {
-                    sadd(&sc[8], 1ull);
-                    sadd(&sc[9], (unsigned long long)mlen);
-                    sadd(&sc[10], (unsigned long long)w20);
-                    sadd(&sc[11], (unsigned long long)w30);
+                    ++la.post_reads;
+                    la.post_len += (uint32_t)mlen;
+                    la.post_q20 += w20;
+                    la.post_q30 += w30;
                 }
             } else if (post_on) {
-                sadd(&sc[8], 1ull);
-                sadd(&sc[9], (unsigned long long)n);
-                sadd(&sc[10], (unsigned long long)w20);
-                sadd(&sc[11], (unsigned long long)w30);
+                ++la.post_reads;
+                la.post_len += (uint32_t)n;
+                la.post_q20 += w20;
+                la.post_q30 += w30;
             }
         }
         FQ_STAMP(6)
@@ -940,6 +966,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     }
 
     FQ_STAMP(7)
+    {  // the lane's register counters -> LDS (lanes l, l+16 share a scalar copy)
+        const int mate = PAIRED ? lane >> 5 : 0;
+        unsigned long long* sc = scal + 16 * (lane & 15) + 4 * mate;
+        const uint32_t v[8] = {la.pre_reads, la.pre_len, la.pre_q20, la.pre_q30,
+                               la.post_reads, la.post_len, la.post_q20, la.post_q30};
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (v[i]) sadd(&sc[i < 4 ? i : i + 4], (unsigned long long)v[i]);
+        if (la.pg_reads) sadd(&small[FQ_ACC_POLYX_READS + 3], (unsigned long long)la.pg_reads);
+        if (la.pg_bases) sadd(&small[FQ_ACC_POLYX_BASES + 3], (unsigned long long)la.pg_bases);
+        if (la.ad_reads) sadd(&small[FQ_ACC_ADAPTER_READS], (unsigned long long)la.ad_reads);
+        if (la.ad_bases) sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)la.ad_bases);
+    }
 #ifdef FQ_PHASE_STAMPS
     if (stamps && lane == 0)
         for (int i = 0; i < kPhases; ++i) atomicAdd(&g_phase_cycles[i], ph[i]);
