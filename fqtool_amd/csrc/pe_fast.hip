@@ -96,6 +96,16 @@ struct Layout {
 constexpr unsigned long long kCount1 = 1ull << 40;
 constexpr unsigned long long kQMask = kCount1 - 1;
 
+// x of lane l ^ 32 (the other mate of the pair): one v_permlane32_swap, no LDS round trip
+// (a ds_bpermute would queue behind the workgroup's LDS atomics).  With old = src = x the swap
+// leaves lanes 0-31 of x in both halves of the first result and lanes 32-63 in both halves of
+// the second.
+__device__ __forceinline__ int xor32(int x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (threadIdx.x & 32) ? r[0] : r[1];
+}
+__device__ __forceinline__ uint32_t xor32(uint32_t x) { return (uint32_t)xor32((int)x); }
+
 // reverse the order of the 16 two-bit fields of a word
 __device__ __forceinline__ uint32_t pairrev(uint32_t x) {
     uint32_t y = __builtin_bitreverse32(x);
@@ -173,19 +183,30 @@ struct OvOut {
 };
 
 // Exact OverlapAnalysis acceptance test at one offset (src/overlapanalysis.cpp:24-40 / :49-65):
-// positions compare r1 codes from p1 with rc2 codes from p2 over `ol` positions.
+// positions compare r1 codes from p1 with rc2 codes from p2 over `ol` positions.  The four
+// streams (codes and N masks of both sides) slide one LDS word per 16 positions; a candidate whose
+// K-th mismatch lies in the first 50 positions is rejected after the first four words.
 __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int p2, int ol, int limit, int K,
                                 int& diff_out) {
     int d50 = 0, D = 0;
     const int nw = (ol + 15) >> 4;
+    const int w1 = p1 >> 4, s1 = 2 * (p1 & 15), w2 = p2 >> 4, s2 = 2 * (p2 & 15);
+    // word w of field f of column c, 0 outside the column
+    auto word = [&](int f, int c, int w) -> uint32_t {
+        const uint32_t v = col[(f + min(max(w, 0), kChunks - 1)) * 64 + c];
+        return (unsigned)w < (unsigned)kChunks ? v : 0u;
+    };
+    uint32_t a0 = word(kFC, c1, w1), an0 = word(kFN, c1, w1), b0 = word(kFC, c2, w2), bn0 = word(kFN, c2, w2);
     for (int j = 0; j < nw; ++j) {
-        const uint32_t a = field_window(col, kFC, c1, p1 + 16 * j);
-        const uint32_t b = field_window(col, kFC, c2, p2 + 16 * j);
-        const uint32_t wa = field_window(col, kFN, c1, p1 + 16 * j);
-        const uint32_t wb = field_window(col, kFN, c2, p2 + 16 * j);
+        const uint32_t a1 = word(kFC, c1, w1 + j + 1), an1 = word(kFN, c1, w1 + j + 1);
+        const uint32_t b1 = word(kFC, c2, w2 + j + 1), bn1 = word(kFN, c2, w2 + j + 1);
+        const uint32_t a = __builtin_amdgcn_alignbit(a1, a0, s1), wa = __builtin_amdgcn_alignbit(an1, an0, s1);
+        const uint32_t b = __builtin_amdgcn_alignbit(b1, b0, s2), wb = __builtin_amdgcn_alignbit(bn1, bn0, s2);
         const uint32_t mism = (fold2(a ^ b) & ~(wa | wb)) | (wa ^ wb);
         D += __popc(mism & posmask(ol - 16 * j));
         d50 += __popc(mism & posmask(min(ol, 50) - 16 * j));
+        if (j == 3 && d50 >= K) break;  // rejected whatever follows (the break happens within 50)
+        a0 = a1; an0 = an1; b0 = b1; bn0 = bn1;
     }
     diff_out = D;
     // break (rejection) happens iff the K-th mismatch lies within the first min(ol,50) positions
@@ -204,33 +225,43 @@ __device__ inline int ov_scan(const uint32_t* col, int cm, int mpos0, int k0, in
     int w = (mpos0 + k0) >> 4;
     uint32_t lo = w < kChunks ? col[(kFC + min(w, kChunks - 1)) * 64 + cm] : 0u;
     uint32_t hi = w + 1 < kChunks ? col[(kFC + min(w + 1, kChunks - 1)) * 64 + cm] : 0u;
+    // the next two window words are requested a step ahead (clamped reads, zeroed past the column)
+    uint32_t nx = col[(kFC + min(w + 2, kChunks - 1)) * 64 + cm];
     for (int k = k0; k < cnt;) {
         const int P = mpos0 + k;
-        // the next window's high word is fetched while this one is scanned
-        const uint32_t nx = w + 2 < kChunks ? col[(kFC + min(w + 2, kChunks - 1)) * 64 + cm] : 0u;
-        uint32_t bits = 0;
+        const uint32_t nx_use = w + 2 < kChunks ? nx : 0u;
+        nx = col[(kFC + min(w + 3, kChunks - 1)) * 64 + cm];
+        // lower bounds of the 16 windows starting at absolute positions 16w + r
+        int lb[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            // window starting at absolute position 16w + r
             const uint32_t win = r == 0 ? lo : __builtin_amdgcn_alignbit(hi, lo, 2 * r);
             uint32_t m = pm;
             if (!FIXED_MASK) {
                 const int kk = 16 * w + r - mpos0;
                 m = posmask(min(olA - kk, olB));
             }
-            const int lb = __popc(fold2(win ^ fixed) & m);
-            bits |= (uint32_t)(lb < K) << r;
+            lb[r] = __popc(fold2(win ^ fixed) & m);
         }
-        // keep offsets within [k, cnt)
-        const int first_r = P & 15;
-        bits &= ~((1u << first_r) - 1u);
-        const int last = cnt - 1 - (16 * w - mpos0);  // last valid r
-        if (last < 15) bits &= (last < 0) ? 0u : ((2u << last) - 1u);
-        if (bits) return 16 * w + (__ffs(bits) - 1) - mpos0;
+        // common case: no window of this step comes under the bound (one min per two windows)
+        int mn = lb[0];
+#pragma unroll
+        for (int r = 1; r < 16; r += 2) mn = min(mn, min(lb[r], r + 1 < 16 ? lb[r + 1] : lb[r]));
+        if (mn < K) {
+            uint32_t bits = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bits |= (uint32_t)(lb[r] < K) << r;
+            // keep offsets within [k, cnt)
+            const int first_r = P & 15;
+            bits &= ~((1u << first_r) - 1u);
+            const int last = cnt - 1 - (16 * w - mpos0);  // last valid r
+            if (last < 15) bits &= (last < 0) ? 0u : ((2u << last) - 1u);
+            if (bits) return 16 * w + (__ffs(bits) - 1) - mpos0;
+        }
         k = 16 * (w + 1) - mpos0;
         ++w;
         lo = hi;
-        hi = nx;
+        hi = nx_use;
     }
     return -1;
 }
@@ -243,11 +274,99 @@ __device__ __forceinline__ uint32_t spread2to4(uint32_t x) {
     return (x | (x << 2)) & 0x33333333u;
 }
 
-
 // Removed-mode Stats rows: [cycle / 16][12 slots][cycle % 16] u64 cells per mate, slot =
 // 4 * kept + code for A C T G (codes 0-3), 8 + kept for N, 10 for positions beyond the read.
 constexpr int kRSlots = 12;
 __host__ __device__ constexpr int rcell(int c, int slot) { return ((c >> 4) * kRSlots + slot) * 32 + 2 * (c & 15); }
+
+// Unshuffle: the low bits of the 16 two-bit fields of x to bits 0-15, the high bits to 16-31.
+__device__ __forceinline__ uint32_t unzip2(uint32_t x) {
+    uint32_t t;
+    t = (x ^ (x >> 1)) & 0x22222222u;
+    x ^= t ^ (t << 1);
+    t = (x ^ (x >> 2)) & 0x0C0C0C0Cu;
+    x ^= t ^ (t << 2);
+    t = (x ^ (x >> 4)) & 0x00F000F0u;
+    x ^= t ^ (t << 4);
+    return __builtin_amdgcn_perm(x, x, 0x03010200u);  // swap bytes 1 and 2
+}
+
+// Full-adder step of the carry-save counters: (hi, lo) = a + b + c, bitwise
+__device__ __forceinline__ void csa(uint32_t& hi, uint32_t& lo, uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t h = (a & b) | (a & c) | (b & c), l = a ^ b ^ c;
+    hi = h;
+    lo = l;
+}
+
+// Candidate offsets of one overlap phase, all at once (overlap_require >= 16, both windows of >= 16
+// positions): bit k of cand[k >> 5] is set iff the 16 positions of the window at mpos + k of
+// column cm hold fewer than K code mismatches against `fixed` (the filter ov_scan applies one
+// offset at a time).  Branch-free: the moving column is realigned to mpos (LDS) and unzipped into
+// bit planes H and L over positions; for compared position j the mismatch vector over the 32
+// offsets of a block is ((H >> j) ^ FH_j) | ((L >> j) ^ FL_j) (FH_j, FL_j = the bits of fixed[j]
+// spread over a word), and the 16 vectors are summed per offset with carry-save adders.
+__device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint32_t fixed, int K, int cnt,
+                                     uint32_t cand[5]) {
+    // planes of the 32 positions from mpos + 32 * i (i = block): low-bit plane, high-bit plane
+    auto planes = [&](int i, uint32_t& lp, uint32_t& hp) {
+        const uint32_t u0 = unzip2(field_window(col, kFC, cm, mpos + 32 * i));
+        const uint32_t u1 = unzip2(field_window(col, kFC, cm, mpos + 32 * i + 16));
+        lp = __builtin_amdgcn_perm(u1, u0, 0x05040100u);  // u0 bits 0-15 | u1 bits 0-15 << 16
+        hp = __builtin_amdgcn_perm(u1, u0, 0x07060302u);  // u0 bits 16-31 | u1 bits 16-31 << 16
+    };
+    uint32_t L0, H0, L1, H1;
+    planes(0, L0, H0);
+    const uint32_t fu = unzip2(fixed);
+    const int nblk = __any(cnt > 128) ? 5 : __any(cnt > 96) ? 4 : __any(cnt > 64) ? 3 : 2;  // wave-uniform
+    for (int bk = nblk; bk < 5; ++bk) cand[bk] = 0u;
+#pragma unroll 1
+    for (int bk = 0; bk < nblk; ++bk) {
+        if (bk < 4) planes(bk + 1, L1, H1);
+        else L1 = H1 = 0u;
+        // mismatch vector of compared position j over the block's 32 offsets
+        auto m = [&](int j) -> uint32_t {
+            const uint32_t hs = j ? __builtin_amdgcn_alignbit(H1, H0, j) : H0;
+            const uint32_t ls = j ? __builtin_amdgcn_alignbit(L1, L0, j) : L0;
+            const uint32_t fh = (uint32_t)__builtin_amdgcn_sbfe((int)fu, 16 + j, 1);
+            const uint32_t fl = (uint32_t)__builtin_amdgcn_sbfe((int)fu, j, 1);
+            return (hs ^ fh) | (ls ^ fl);
+        };
+        // 16 vectors -> bit-sliced 5-bit counts, Harley-Seal carry-save order (few live values)
+        uint32_t ones = 0u, twos = 0u, fours = 0u, eights = 0u, sixteen, twosA, twosB, foursA, foursB, eightsA, eightsB;
+        csa(twosA, ones, ones, m(0), m(1));
+        csa(twosB, ones, ones, m(2), m(3));
+        csa(foursA, twos, twos, twosA, twosB);
+        csa(twosA, ones, ones, m(4), m(5));
+        csa(twosB, ones, ones, m(6), m(7));
+        csa(foursB, twos, twos, twosA, twosB);
+        csa(eightsA, fours, fours, foursA, foursB);
+        csa(twosA, ones, ones, m(8), m(9));
+        csa(twosB, ones, ones, m(10), m(11));
+        csa(foursA, twos, twos, twosA, twosB);
+        csa(twosA, ones, ones, m(12), m(13));
+        csa(twosB, ones, ones, m(14), m(15));
+        csa(foursB, twos, twos, twosA, twosB);
+        csa(eightsB, fours, fours, foursA, foursB);
+        csa(sixteen, eights, eights, eightsA, eightsB);
+        // count < K, bit-sliced against the wave-uniform K
+        uint32_t lt = 0u, eq = ~0u;
+        const uint32_t cb[5] = {ones, twos, fours, eights, sixteen};
+#pragma unroll
+        for (int i = 4; i >= 0; --i) {
+            if ((K >> i) & 1) {
+                lt |= eq & ~cb[i];
+                eq &= cb[i];
+            } else {
+                eq &= ~cb[i];
+            }
+        }
+        if (K > 31) lt = ~0u;
+        const int nb = cnt - 32 * bk;  // valid offsets of this block
+        cand[bk] = lt & (nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u));
+        L0 = L1;
+        H0 = H1;
+    }
+}
 
 __device__ __forceinline__ uint32_t gmask(const Fwd& f) { return ~fold2(~f.c) & ~f.n & 0x55555555u; }
 
@@ -317,9 +436,13 @@ __device__ __forceinline__ void count_by_value(unsigned long long* base, bool on
 
 // Per-lane counters kept in registers across tiles and added to LDS once at the end (a lane
 // always holds the same mate): polyG and adapter FilterResult counters, Stats scalars.
+// Read counts are packed two to a register (16 bits each: a lane sees at most one read per tile,
+// far fewer than 65536 tiles per launch).
 struct LaneAcc {
-    uint32_t pg_reads, pg_bases, ad_reads, ad_bases;
-    uint32_t pre_reads, pre_len, pre_q20, pre_q30, post_reads, post_len, post_q20, post_q30;
+    uint32_t reads;  // pre_reads | post_reads << 16
+    uint32_t pgad;   // polyG reads | adapter reads << 16
+    uint32_t pg_bases, ad_bases;
+    uint32_t pre_len, pre_q20, pre_q30, post_len, post_q20, post_q30;
 };
 
 // Profiling aid: per-phase wave cycles (s_memtime deltas summed over waves), compiled in with
@@ -362,7 +485,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 
     // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
     // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics,
-    // 32 skip the polyG counters
+    // 32 skip the polyG counters, 64 accept the first scan candidate unchecked, 128 skip the scan
     const int abl = p.reserved[0];
     const int ntiles = PAIRED ? (b.n + 31) >> 5 : (b.n + 63) >> 6;
 #if FQ_FIXED_STRIDE  // profiling only: assume rows of >= 160 bytes
@@ -395,7 +518,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 #define FQ_STAMP(i)
 #endif
 
-    LaneAcc la = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    LaneAcc la = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
         // Per-lane values are derived from an opaque copy of the lane id inside the loop: left to
         // itself the compiler hoists dozens of them out of the tile loop and spills them.
@@ -433,7 +556,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         };
         // (merge: a merged read, at most len1 + len2 long, must fit max_cycles as well)
         const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4) ||
-                         (MERGE && L + __shfl_xor(L, 32) > p.max_cycles);
+                         (MERGE && L + xor32(L) > p.max_cycles);
         uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0, lowf = 0, tqf = 0, nbf = 0;  // whole-read sums
         // column word of chunk k: k for read 1, 9-k for read 2 (stepped, not precomputed, so the
         // ten addresses are not kept live across tiles)
@@ -559,7 +682,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         }
         // the shuffle must run in every lane: ds_bpermute from a lane that is switched off returns
         // whatever its register held before (e.g. the previous tile's value)
-        const int nn_o = PAIRED ? __shfl_xor(nn ? 1 : 0, 32) : 1;
+        const int nn_o = PAIRED ? xor32(nn ? 1 : 0) : 1;
         const bool both = nn && nn_o != 0;
         fq_read_result rr;
         rr.flags = nn ? 0 : FQ_RF_NULL;
@@ -572,7 +695,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             int bases;
             n = polyg_bits(col, lane, rc, L, st, n, p.polyg_max_mismatch, g_inv, p.polyg_compare_req, bases);
             if (bases >= 0 && !(abl & 32)) {
-                ++la.pg_reads;
+                ++la.pgad;
                 la.pg_bases += (uint32_t)bases;
             }
         }
@@ -596,7 +719,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 }
                 rr.ad_len = (uint16_t)ad_len;
                 if (ad_len > 0) {
-                    ++la.ad_reads;
+                    la.pgad += 1u << 16;
                     la.ad_bases += (uint32_t)ad_len;
                 }
             }
@@ -604,7 +727,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         // OverlapAnalysis::analyze (src/overlapanalysis.cpp:7-72) of the pair's current windows;
         // both lanes of the pair call it together and get the same result
         auto pair_overlap = [&]() -> Overlap {
-            const int st_o = __shfl_xor(st, 32), n_o = __shfl_xor(n, 32);
+            const int st_o = xor32(st), n_o = xor32(n);
             const int st1 = mate ? st_o : st, n1 = mate ? n_o : n;
             const int st2 = mate ? st : st_o, n2 = mate ? n : n_o;
             const int c1 = mate ? mlane : lane, c2 = mate ? lane : mlane;
@@ -617,20 +740,43 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             const int cnt = max(0, olA - req);
             const uint32_t pm = posmask(olB);
             OvOut mine{false, 0, 0, 0};
-            for (int k0 = 0;;) {
+            if (abl & 512) atomicAdd(&g_phase_cycles[1], 1ull);  // profiling: scanning lanes
+            // bit-plane candidates when every lane compares full 16-position windows
+            const bool planes = req >= 16 && !__any(olB < 16) && !(abl & 128);
+            if (planes) {
+                uint32_t cand[5];
+                ov_candidates(col, cm, mpos, fixed, K, cnt, cand);
+                for (;;) {  // candidates in offset order until one passes the exact test
+                    int o = -1;
+#pragma unroll
+                    for (int bk = 4; bk >= 0; --bk)
+                        if (cand[bk]) o = 32 * bk + __ffs(cand[bk]) - 1;
+                    if (o < 0) break;
+                    cand[o >> 5] &= cand[o >> 5] - 1u;
+                    const int ol = min(olA - o, olB);
+                    int diff = 0;
+                    if (abl & 512) atomicAdd(&g_phase_cycles[0], 1ull);  // profiling: exact checks
+                    if ((abl & 64) || ov_exact(col, c1, mate ? st1 : st1 + o, c2, mate ? off2 + o : off2, ol, limit, K, diff)) {
+                        mine = OvOut{true, mate ? -o : o, ol, diff};
+                        break;
+                    }
+                }
+            }
+            for (int k0 = 0; !planes && !(abl & 128);) {
                 const int o = req >= 16 ? ov_scan<true>(col, cm, mpos, k0, cnt, fixed, olA, olB, K, pm)
                                         : ov_scan<false>(col, cm, mpos, k0, cnt, fixed, olA, olB, K, pm);
                 if (o < 0) break;
                 const int ol = min(olA - o, olB);
-                int diff;
-                if (ov_exact(col, c1, mate ? st1 : st1 + o, c2, mate ? off2 + o : off2, ol, limit, K, diff)) {
+                int diff = 0;
+                if (abl & 512) atomicAdd(&g_phase_cycles[0], 1ull);  // profiling: exact checks
+                if ((abl & 64) || ov_exact(col, c1, mate ? st1 : st1 + o, c2, mate ? off2 + o : off2, ol, limit, K, diff)) {
                     mine = OvOut{true, mate ? -o : o, ol, diff};
                     break;
                 }
                 k0 = o + 1;
             }
-            const int f_o = __shfl_xor(mine.found ? 1 : 0, 32);
-            const int off_o = __shfl_xor(mine.off, 32), ol_o = __shfl_xor(mine.ol, 32), d_o = __shfl_xor(mine.diff, 32);
+            const int f_o = xor32(mine.found ? 1 : 0);
+            const int off_o = xor32(mine.off), ol_o = xor32(mine.ol), d_o = xor32(mine.diff);
             const bool f1 = mate ? f_o != 0 : mine.found;
             const bool f2 = mate ? mine.found : f_o != 0;
             Overlap ov{0, 0, 0, 0};
@@ -641,7 +787,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
         if (PAIRED && both && !(abl & 1)) {
             const Overlap ov = pair_overlap();
-            const int n_o = __shfl_xor(n, 32);
+            const int n_o = xor32(n);
             const int n1 = mate ? n_o : n, n2 = mate ? n : n_o;
             if (mate == 0) {  // PairEndProcessor::statInsertSize, src/peprocessor.cpp:510-523
                 int isize = p.insert_size_max;
@@ -656,7 +802,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     rr.ad_pos = (uint16_t)(st + ol);
                     rr.ad_len = (uint16_t)(n - ol);
                     if (mate == 0) {
-                        la.ad_reads += 2;
+                        la.pgad += 2u << 16;
                         la.ad_bases += (uint32_t)((n1 - ol) + (n2 - ol));
                     }
                     n = ol;
@@ -689,7 +835,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             if (ov2.overlapped) {
                 merged = true;
                 mol = ov2.len;
-                const int n_o = __shfl_xor(n, 32);
+                const int n_o = xor32(n);
                 const int n1 = mate ? n_o : n, n2 = mate ? n : n_o;
                 if (mol) {
                     m1 = min(mol + max(0, ov2.offset), n1);
@@ -722,10 +868,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 for (int part = 0; part < 2; ++part) {
                     const int a0 = part ? end : 0, a1 = part ? L : ws;  // forward range [a0, a1)
                     const int F0 = a0 >> 4, F1 = (a1 + 15) >> 4;
-                    // row chunks come from L2; the next one is requested before this one is used
-                    uint4 cur = qchunk(min(F0, nchunks - 1));
-                    for (int F = F0; F < F1; ++F) {
-                        const uint4 nxt = qchunk(min(F + 1, nchunks - 1));
+                    // subtract the bytes of row chunk F inside [a0, a1)
+                    auto sub = [&](const uint4 cur, int F) {
                         const uint32_t wq[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
@@ -738,7 +882,25 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                             w30 -= __popc(((w7 + 0x40404040u) & 0x80808080u) & bm);
                             if (need_tq) tq -= (int)__builtin_amdgcn_sad_u8(w, 0u, 0u);
                         }
-                        cur = nxt;
+                    };
+                    if (part == 1) {
+                        // the tail, from the 3' end: its last four chunks are requested together
+                        // (one L2 round trip for almost every read), longer adapter tails loop
+                        uint4 qa[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) qa[i] = qchunk(max(F1 - 1 - i, 0));
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if (F1 - 1 - i >= F0) sub(qa[i], F1 - 1 - i);
+                        for (int F = F1 - 5; F >= F0; --F) sub(qchunk(F), F);
+                    } else if (!LEAN) {
+                        // row chunks come from L2; the next one is requested before this one is used
+                        uint4 cur = qchunk(min(F0, nchunks - 1));
+                        for (int F = F0; F < F1; ++F) {
+                            const uint4 nxt = qchunk(min(F + 1, nchunks - 1));
+                            sub(cur, F);
+                            cur = nxt;
+                        }
                     }
                     // N bits of the same range (read 2's column is reverse-complemented)
                     const int s0 = rc ? kMaxLen - a1 : a0, s1 = rc ? kMaxLen - a0 : a1;
@@ -759,17 +921,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         int mlen = 0;
         if (MERGE && merged) {  // passFilter of the merged read: the sums of its two parts
             mlen = m1 + m2;
-            low += __shfl_xor(low, 32);
-            nb += __shfl_xor(nb, 32);
-            tq += __shfl_xor(tq, 32);
-            w20 += __shfl_xor(w20, 32);
-            w30 += __shfl_xor(w30, 32);
+            low += xor32(low);
+            nb += xor32(nb);
+            tq += xor32(tq);
+            w20 += xor32(w20);
+            w30 += xor32(w30);
             // (OverlapAnalysis::merge returns NULL for ol 0; the complexity filter is excluded
             // from the merge variant)
             code = (mol == 0 || mlen == 0) ? FQ_FAIL_LENGTH
                                            : filter_verdict(p, mlen, low, nb, tq - 33 * mlen, [&]() { return 0; });
         }
-        const int code_o = PAIRED ? __shfl_xor(code, 32) : code;
+        const int code_o = PAIRED ? xor32(code) : code;
         const bool pair_pass = both && code == FQ_PASS_FILTER && code_o == FQ_PASS_FILTER;
         bool post_on;  // this lane's window goes to a post block
         if (MERGE && merged) {
@@ -933,25 +1095,33 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         }
         if (valid && !(abl & 4)) {
             // per-read Stats scalars
-            ++la.pre_reads;
+            ++la.reads;
             la.pre_len += (uint32_t)L;
             la.pre_q20 += q20;
             la.pre_q30 += q30;
             if (MERGE && merged) {
                 if (post_on && mate == 0) {
-                    ++la.post_reads;
+                    la.reads += 1u << 16;
                     la.post_len += (uint32_t)mlen;
                     la.post_q20 += w20;
                     la.post_q30 += w30;
                 }
             } else if (post_on) {
-                ++la.post_reads;
+                la.reads += 1u << 16;
                 la.post_len += (uint32_t)n;
                 la.post_q20 += w20;
                 la.post_q30 += w30;
             }
         }
         FQ_STAMP(6)
+        if (abl & 256) {  // profiling only: 512 extra independent VALU ops per tile (issue-rate probe)
+            uint32_t d0 = lane_x, d1 = lane_x + 1, d2 = lane_x + 2, d3 = lane_x + 3;
+#pragma unroll
+            for (int i = 0; i < 128; ++i)
+                asm volatile("v_xor_b32 %0, %0, %4\n\tv_xor_b32 %1, %1, %4\n\tv_xor_b32 %2, %2, %4\n\tv_xor_b32 %3, %3, %4"
+                             : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3) : "v"(L));
+            if ((d0 ^ d1 ^ d2 ^ d3) == 0x9E3779B9u) rr.reserved = 1;
+        }
         if (valid) {
             rr.start = nn ? (uint16_t)st : 0;
             rr.len = nn ? (uint16_t)n : 0;
@@ -969,14 +1139,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     {  // the lane's register counters -> LDS (lanes l, l+16 share a scalar copy)
         const int mate = PAIRED ? lane >> 5 : 0;
         unsigned long long* sc = scal + 16 * (lane & 15) + 4 * mate;
-        const uint32_t v[8] = {la.pre_reads, la.pre_len, la.pre_q20, la.pre_q30,
-                               la.post_reads, la.post_len, la.post_q20, la.post_q30};
+        const uint32_t v[8] = {la.reads & 0xFFFFu, la.pre_len, la.pre_q20, la.pre_q30,
+                               la.reads >> 16, la.post_len, la.post_q20, la.post_q30};
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             if (v[i]) sadd(&sc[i < 4 ? i : i + 4], (unsigned long long)v[i]);
-        if (la.pg_reads) sadd(&small[FQ_ACC_POLYX_READS + 3], (unsigned long long)la.pg_reads);
+        if (la.pgad & 0xFFFFu) sadd(&small[FQ_ACC_POLYX_READS + 3], (unsigned long long)(la.pgad & 0xFFFFu));
         if (la.pg_bases) sadd(&small[FQ_ACC_POLYX_BASES + 3], (unsigned long long)la.pg_bases);
-        if (la.ad_reads) sadd(&small[FQ_ACC_ADAPTER_READS], (unsigned long long)la.ad_reads);
+        if (la.pgad >> 16) sadd(&small[FQ_ACC_ADAPTER_READS], (unsigned long long)(la.pgad >> 16));
         if (la.ad_bases) sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)la.ad_bases);
     }
 #ifdef FQ_PHASE_STAMPS

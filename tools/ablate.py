@@ -17,7 +17,9 @@ assert lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 0, 150, None) == 0
 res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
 torch.cuda.synchronize()
 variants = [("full", 0), ("no_overlap", 1), ("no_filter", 2), ("no_stats", 4), ("no_polyg", 8),
-            ("no_lds_atomics", 16), ("no_overlap_filter_stats", 7), ("stage_only", 15), ("no_polyg_counters", 32)]
+            ("no_lds_atomics", 16), ("no_overlap_filter_stats", 7), ("stage_only", 15), ("no_polyg_counters", 32),
+            ("no_ov_exact", 64), ("no_ov_scan", 128),
+            ("plus_512_valu", 256)]
 only = os.environ.get("VARIANTS")
 if only:
     variants = [v for v in variants if v[0] in only.split(",")]
