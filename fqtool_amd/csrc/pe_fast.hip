@@ -434,16 +434,7 @@ __device__ __forceinline__ void count_by_value(unsigned long long* base, bool on
     }
 }
 
-// Per-lane counters kept in registers across tiles and added to LDS once at the end (a lane
-// always holds the same mate): polyG and adapter FilterResult counters, Stats scalars.
-// Read counts are packed two to a register (16 bits each: a lane sees at most one read per tile,
-// far fewer than 65536 tiles per launch).
-struct LaneAcc {
-    uint32_t reads;  // pre_reads | post_reads << 16
-    uint32_t pgad;   // polyG reads | adapter reads << 16
-    uint32_t pg_bases, ad_bases;
-    uint32_t pre_len, pre_q20, pre_q30, post_len, post_q20, post_q30;
-};
+
 
 // Profiling aid: per-phase wave cycles (s_memtime deltas summed over waves), compiled in with
 // -DFQ_PHASE_STAMPS (make STAMPS=1), collected when fq_params.reserved[1] != 0 and read back with
@@ -518,7 +509,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 #define FQ_STAMP(i)
 #endif
 
-    LaneAcc la = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
         // Per-lane values are derived from an opaque copy of the lane id inside the loop: left to
         // itself the compiler hoists dozens of them out of the tile loop and spills them.
@@ -694,10 +684,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         if (both && p.polyg_enabled && !(abl & 8)) {
             int bases;
             n = polyg_bits(col, lane, rc, L, st, n, p.polyg_max_mismatch, g_inv, p.polyg_compare_req, bases);
-            if (bases >= 0 && !(abl & 32)) {
-                ++la.pgad;
-                la.pg_bases += (uint32_t)bases;
-            }
+            if (bases >= 0 && !(abl & 32))  // (reads << 32 | bases) into the lane's scalar copy
+                sadd(&scal[16 * (lane_x & 15) + 4 * mate + 2], (1ull << 32) | (unsigned long long)bases);
         }
 
         FQ_STAMP(2)
@@ -718,10 +706,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     n = pos;
                 }
                 rr.ad_len = (uint16_t)ad_len;
-                if (ad_len > 0) {
-                    la.pgad += 1u << 16;
-                    la.ad_bases += (uint32_t)ad_len;
-                }
+                if (ad_len > 0) sadd(&scal[16 * (lane_x & 15) + 4 * mate + 3], (1ull << 32) | (unsigned long long)ad_len);
             }
         };
         // OverlapAnalysis::analyze (src/overlapanalysis.cpp:7-72) of the pair's current windows;
@@ -801,10 +786,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     rr.flags |= FQ_RF_AD_OVERLAP;
                     rr.ad_pos = (uint16_t)(st + ol);
                     rr.ad_len = (uint16_t)(n - ol);
-                    if (mate == 0) {
-                        la.pgad += 2u << 16;
-                        la.ad_bases += (uint32_t)((n1 - ol) + (n2 - ol));
-                    }
+                    if (mate == 0)
+                        sadd(&scal[16 * (lane_x & 15) + 3], (2ull << 32) | (unsigned long long)((n1 - ol) + (n2 - ol)));
                     n = ol;
                 } else if (!LEAN && my_alen > 0) {
                     by_sequence();
@@ -871,28 +854,30 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     // subtract the bytes of row chunk F inside [a0, a1)
                     auto sub = [&](const uint4 cur, int F) {
                         const uint32_t wq[4] = {cur.x, cur.y, cur.z, cur.w};
+                        // in-range flags at bit 7 of each byte, SWAR: byte k of dword j holds
+                        // 128 + (4j + k) - lo (resp. - hi), >= 128 iff the position is >= lo (>= hi)
+                        const uint32_t lo = (uint32_t)min(max(a0 - 16 * F, 0), 16), hi = (uint32_t)min(max(a1 - 16 * F, 0), 16);
+                        const uint32_t b1 = 0x83828180u - lo * 0x01010101u, b2 = 0x83828180u - hi * 0x01010101u;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            const int b0 = 16 * F + 4 * j;
-                            const uint32_t bm = bytemask(a1 - b0) & ~bytemask(a0 - b0);
-                            const uint32_t w = wq[j] & bm;
-                            const uint32_t w7 = w & 0x7F7F7F7Fu;
-                            low -= __popc(~(w7 + limq) & 0x80808080u & bm);
-                            w20 -= __popc(((w7 + 0x4A4A4A4Au) & 0x80808080u) & bm);
-                            w30 -= __popc(((w7 + 0x40404040u) & 0x80808080u) & bm);
-                            if (need_tq) tq -= (int)__builtin_amdgcn_sad_u8(w, 0u, 0u);
+                            const uint32_t rf = (b1 + 0x04040404u * j) & ~(b2 + 0x04040404u * j) & 0x80808080u;
+                            const uint32_t w7 = wq[j] & 0x7F7F7F7Fu;
+                            low -= __popc(~(w7 + limq) & rf);
+                            w20 -= __popc((w7 + 0x4A4A4A4Au) & rf);
+                            w30 -= __popc((w7 + 0x40404040u) & rf);
+                            if (need_tq) tq -= (int)__builtin_amdgcn_sad_u8(wq[j] & ((rf >> 7) * 0xFFu), 0u, 0u);
                         }
                     };
                     if (part == 1) {
-                        // the tail, from the 3' end: its last four chunks are requested together
-                        // (one L2 round trip for almost every read), longer adapter tails loop
-                        uint4 qa[4];
+                        // the tail, from the 3' end: its last two chunks are requested together
+                        // (one L2 round trip for most reads), longer adapter tails loop
+                        uint4 qa[2];
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) qa[i] = qchunk(max(F1 - 1 - i, 0));
+                        for (int i = 0; i < 2; ++i) qa[i] = qchunk(max(F1 - 1 - i, 0));
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
+                        for (int i = 0; i < 2; ++i)
                             if (F1 - 1 - i >= F0) sub(qa[i], F1 - 1 - i);
-                        for (int F = F1 - 5; F >= F0; --F) sub(qchunk(F), F);
+                        for (int F = F1 - 3; F >= F0; --F) sub(qchunk(F), F);
                     } else if (!LEAN) {
                         // row chunks come from L2; the next one is requested before this one is used
                         uint4 cur = qchunk(min(F0, nchunks - 1));
@@ -1001,7 +986,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     // N bases (rare): move each from its G cell (slot 4 * kept + 3) to slot 8 + kept
                     uint32_t nv = f.n & posmask(vl);
                     if (__any(nv != 0)) {
-                        const uint32_t qs[4] = {q0 | 0x80808080u, q1 | 0x80808080u, q2 | 0x80808080u, q3 | 0x80808080u};
+                        const uint32_t qs[4] = {q0, q1, q2, q3};
                         while (nv) {
                             const int t = (__ffs(nv) - 1) >> 1;
                             nv &= nv - 1;
@@ -1022,11 +1007,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     const uint32_t t2 = (dsel & 1) ? q3 : q2, t3 = (dsel & 1) ? q0 : q3;
                     const uint32_t a0 = (dsel & 2) ? t2 : t0, a1 = (dsel & 2) ? t3 : t1;
                     const uint32_t a2 = (dsel & 2) ? t0 : t2, a3 = (dsel & 2) ? t1 : t3;
-                    // qualities + 128 (bytes are < 128 here): the low word of a cell increment
-                    const uint32_t qr[4] = {__builtin_amdgcn_alignbyte(a1, a0, r & 3) | 0x80808080u,
-                                            __builtin_amdgcn_alignbyte(a2, a1, r & 3) | 0x80808080u,
-                                            __builtin_amdgcn_alignbyte(a3, a2, r & 3) | 0x80808080u,
-                                            __builtin_amdgcn_alignbyte(a0, a3, r & 3) | 0x80808080u};
+                    // quality bytes (< 128 here): the low word of a cell increment
+                    const uint32_t qr[4] = {__builtin_amdgcn_alignbyte(a1, a0, r & 3), __builtin_amdgcn_alignbyte(a2, a1, r & 3),
+                                            __builtin_amdgcn_alignbyte(a3, a2, r & 3), __builtin_amdgcn_alignbyte(a0, a3, r & 3)};
 #pragma unroll
                     for (int t = 0; t < 16; ++t) {
                         const uint32_t ks = __builtin_amdgcn_ubfe(t < 8 ? klo : khi, 4 * (t & 7), 4);
@@ -1094,23 +1077,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             }
         }
         if (valid && !(abl & 4)) {
-            // per-read Stats scalars
-            ++la.reads;
-            la.pre_len += (uint32_t)L;
-            la.pre_q20 += q20;
-            la.pre_q30 += q30;
-            if (MERGE && merged) {
-                if (post_on && mate == 0) {
-                    la.reads += 1u << 16;
-                    la.post_len += (uint32_t)mlen;
-                    la.post_q20 += w20;
-                    la.post_q30 += w30;
-                }
-            } else if (post_on) {
-                la.reads += 1u << 16;
-                la.post_len += (uint32_t)n;
-                la.post_q20 += w20;
-                la.post_q30 += w30;
+            // per-read Stats scalars: (reads, length_sum) packed as count << 32 | sum, plus
+            // q20 << 32 | q30, into one of 16 LDS copies (lanes l, l + 16 share one)
+            unsigned long long* sc = scal + 16 * (lane_x & 15) + 4 * mate;
+            sadd(&sc[0], (1ull << 32) | (unsigned long long)L);
+            sadd(&sc[1], ((unsigned long long)q20 << 32) | q30);
+            const bool post_here = (MERGE && merged) ? (post_on && mate == 0) : post_on;
+            if (post_here) {
+                sadd(&sc[8], (1ull << 32) | (unsigned long long)((MERGE && merged) ? mlen : n));
+                sadd(&sc[9], ((unsigned long long)w20 << 32) | w30);
             }
         }
         FQ_STAMP(6)
@@ -1136,19 +1111,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     }
 
     FQ_STAMP(7)
-    {  // the lane's register counters -> LDS (lanes l, l+16 share a scalar copy)
-        const int mate = PAIRED ? lane >> 5 : 0;
-        unsigned long long* sc = scal + 16 * (lane & 15) + 4 * mate;
-        const uint32_t v[8] = {la.reads & 0xFFFFu, la.pre_len, la.pre_q20, la.pre_q30,
-                               la.reads >> 16, la.post_len, la.post_q20, la.post_q30};
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (v[i]) sadd(&sc[i < 4 ? i : i + 4], (unsigned long long)v[i]);
-        if (la.pgad & 0xFFFFu) sadd(&small[FQ_ACC_POLYX_READS + 3], (unsigned long long)(la.pgad & 0xFFFFu));
-        if (la.pg_bases) sadd(&small[FQ_ACC_POLYX_BASES + 3], (unsigned long long)la.pg_bases);
-        if (la.pgad >> 16) sadd(&small[FQ_ACC_ADAPTER_READS], (unsigned long long)(la.pgad >> 16));
-        if (la.ad_bases) sadd(&small[FQ_ACC_ADAPTER_BASES], (unsigned long long)la.ad_bases);
-    }
 #ifdef FQ_PHASE_STAMPS
     if (stamps && lane == 0)
         for (int i = 0; i < kPhases; ++i) atomicAdd(&g_phase_cycles[i], ph[i]);
@@ -1162,11 +1124,25 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         if (small[i]) atomicAdd(&acc[i], small[i]);
     const size_t st_base = acc_stats_offset(p.insert_size_max, p.max_cycles, 0);
     const size_t st_words = acc_stats_words(p.max_cycles);
-    if (threadIdx.x < 16) {
+    if (threadIdx.x < 16) {  // stats k: [reads << 32 | length_sum, q20 << 32 | q30] -> the four words
         const int k = threadIdx.x >> 2, f = threadIdx.x & 3;
         unsigned long long v = 0;
-        for (int c = 0; c < kScalCopies; ++c) v += scal[16 * c + threadIdx.x];
-        if (v) atomicAdd(&acc[st_base + k * st_words + f], v);
+        for (int c = 0; c < kScalCopies; ++c) {
+            const unsigned long long w = scal[16 * c + 4 * k + (f >> 1)];
+            v += (f & 1) ? (w & 0xFFFFFFFFull) : (w >> 32);
+        }
+        if (v) atomicAdd(&acc[st_base + k * st_words + f], v);  // FQ_ST_READS, _LENGTH_SUM, _Q20, _Q30
+    } else if (threadIdx.x < 18) {  // polyG (slot 2) and adapter (slot 3) counters: reads << 32 | bases
+        const int slot = threadIdx.x - 14;
+        unsigned long long rd = 0, bs = 0;
+        for (int c = 0; c < kScalCopies; ++c)
+            for (int m = 0; m < 2; ++m) {
+                const unsigned long long w = scal[16 * c + 4 * m + slot];
+                rd += w >> 32;
+                bs += w & 0xFFFFFFFFull;
+            }
+        if (rd) atomicAdd(&acc[slot == 2 ? FQ_ACC_POLYX_READS + 3 : FQ_ACC_ADAPTER_READS], rd);
+        if (bs) atomicAdd(&acc[slot == 2 ? FQ_ACC_POLYX_BASES + 3 : FQ_ACC_ADAPTER_BASES], bs);
     }
     if (removed_mode) {  // pre = kept + removed, post = kept
         const int ncyc = min(kMaxLen, p.max_cycles);
@@ -1181,7 +1157,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 #pragma unroll
             for (int pp = 0; pp < 2; ++pp) {
                 const long long cnt = (long long)(vals[pp] >> 40);
-                const long long qs = (long long)(vals[pp] & kQMask) - 161ll * cnt;  // undo the +128 bias, -33
+                const long long qs = (long long)(vals[pp] & kQMask) - 33ll * cnt;  // cells hold sum(q), q = byte
                 if (cnt == 0 && qs == 0) continue;
                 unsigned long long* dst = acc + st_base + (k + 2 * pp) * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
                 atomicAdd(&dst[cls], (unsigned long long)cnt);
