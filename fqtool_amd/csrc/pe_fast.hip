@@ -32,6 +32,8 @@
 // The LEAN instantiation drops the options the headline workloads do not use.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "device_ops.h"
 #include "engine_internal.h"
 
@@ -449,7 +451,7 @@ __device__ __forceinline__ void hadd(uint32_t* base, int word, unsigned long lon
 // histogram slot (A C T G N) -> Stats base class (byte & 7), src/stats.cpp:249
 __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) & 0xF; }
 
-// LEAN: the option set of the headline workloads (no trimming/cutting windows, polyX, adapter
+// LEAN: the option set of the headline workloads (no trimming/cutting windows, -e, polyX, adapter
 // sequences, maxLen or low-complexity filter), instantiated separately so the hot loop carries
 // neither their code nor their parameters.
 // PAIRED: a tile is 32 pairs, lanes l and l+32 holding the two mates of a pair (read 2's column
@@ -597,23 +599,33 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 asm volatile("" : "+v"(Lk));
 #endif
                 const bool full = __all(Lk >= 16);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                // per dword: codes, N flags, exotic-byte check and the quality sums; bytes >= 128
+                // send the tile to the general kernel, so q + c (c < 128) never carries into the
+                // next byte for the bytes that count.  FULL: every byte is inside the read (the
+                // common case, no byte masks).
+                auto dword = [&](int j, auto full_c) {
+                    constexpr bool FULL = decltype(full_c)::value;
                     if (!LEAN) qrow[4 * k + j] = qw[j];
-                    const uint32_t bm = full ? 0xFFFFFFFFu : bytemask(Lk - 4 * j);
+                    const uint32_t bm = FULL ? 0xFFFFFFFFu : bytemask(Lk - 4 * j);
                     const uint32_t kk = (sw[j] >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
                     const uint32_t canon = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, kk);
-                    exo |= (canon ^ sw[j]) & bm;
-                    const uint32_t qm = qw[j] & bm;
+                    exo |= FULL ? (canon ^ sw[j]) : ((canon ^ sw[j]) & bm);
+                    const uint32_t qm = FULL ? qw[j] : (qw[j] & bm);
                     qhi |= qm;
-                    const uint32_t q7 = qm & 0x7F7F7F7Fu;
-                    q20 += __popc(((q7 + 0x4A4A4A4Au) & 0x80808080u) & bm);  // q > '5'
-                    q30 += __popc(((q7 + 0x40404040u) & 0x80808080u) & bm);  // q > '?'
-                    lowf += __popc(~(q7 + limq) & 0x80808080u & bm);          // q < limit
-                    tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);
+                    q20 += __popc((qm + 0x4A4A4A4Au) & (0x80808080u & bm));  // q > '5'
+                    q30 += __popc((qm + 0x40404040u) & (0x80808080u & bm));  // q > '?'
+                    lowf += __popc(~(qm + limq) & (0x80808080u & bm));        // q < limit
+                    if (!LEAN) tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);    // (LEAN excludes -e)
                     cc |= (kk & 0x03030303u) << (2 * j);
                     nn4 |= ((kk >> 2) & 0x01010101u) << (2 * j);
+                };
+                if (full) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) dword(j, std::true_type{});
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) dword(j, std::false_type{});
                 }
                 const uint32_t fck = tr4x4(cc), fwk = tr4x4(nn4);
                 nbf += __popc(fwk & (full ? 0x55555555u : posmask(Lk)));
@@ -1205,7 +1217,7 @@ hipError_t fq_pe_fast_prepare() {
                         (const void*)pe_fast_kernel<true, false, false>, (const void*)pe_fast_kernel<false, false, false>,
                         (const void*)pe_fast_kernel<false, true, true>};
     for (int i = 0; i < 5; ++i) {
-        const int words = i == 4 ? Layout<false, true>::kLdsW : (i & 1) ? Layout<false>::kLdsW : Layout<true>::kLdsW;
+        const int words = i == 4 ? Layout<false, true>::kLdsW : (i & 1) ? Layout<false>::kLdsW : 160 * 1024 / 4;
         hipError_t e = hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, words * 4);
         if (e != hipSuccess) return e;
     }
@@ -1215,6 +1227,7 @@ hipError_t fq_pe_fast_prepare() {
 hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
                              int* slow_tiles, int* slow_count, int grid, hipStream_t stream) {
     const bool lean = p.trim_front1 == 0 && p.trim_tail1 == 0 && p.trim_front2 == 0 && p.trim_tail2 == 0 &&
+                      !(p.avg_qual_limit > 0) &&
                       !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
                       p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled;
     using LL = Layout<true>;
@@ -1225,7 +1238,8 @@ hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_resu
         hipLaunchKernelGGL((pe_fast_kernel<false, true, true>), dim3(grid * LM::kBlocksPerCU), dim3(LM::kThreads),
                            LM::kLdsW * 4, stream, p, b, res, acc, slow_tiles, slow_count);
     else if (p.paired && lean)
-        hipLaunchKernelGGL((pe_fast_kernel<true, true, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4, stream, p, b,
+        // (fq_params.reserved[2]: extra LDS bytes per workgroup, profiling only -- lowers occupancy)
+        hipLaunchKernelGGL((pe_fast_kernel<true, true, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4 + p.reserved[2], stream, p, b,
                            res, acc, slow_tiles, slow_count);
     else if (p.paired)
         hipLaunchKernelGGL((pe_fast_kernel<false, true, false>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,

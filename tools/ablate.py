@@ -19,7 +19,7 @@ torch.cuda.synchronize()
 variants = [("full", 0), ("no_overlap", 1), ("no_filter", 2), ("no_stats", 4), ("no_polyg", 8),
             ("no_lds_atomics", 16), ("no_overlap_filter_stats", 7), ("stage_only", 15), ("no_polyg_counters", 32),
             ("no_ov_exact", 64), ("no_ov_scan", 128),
-            ("plus_512_valu", 256)]
+            ("plus_512_valu", 256), ("one_wg_per_cu", 70 << 16)]
 only = os.environ.get("VARIANTS")
 if only:
     variants = [v for v in variants if v[0] in only.split(",")]
@@ -27,7 +27,8 @@ results = {}
 for rep in range(3 if os.environ.get("CONFIG", "C3") == "C3" else 0):
     for name, bits in variants:
         p = abi.default_params(True, 256); p.qual_filter_enabled = 1; p.adapter_trimming = 1; p.polyg_enabled = 1
-        p.reserved[0] = bits
+        p.reserved[0] = bits & 0xFFFF
+        p.reserved[2] = (bits >> 16) * 1024  # extra LDS KiB per workgroup (occupancy probe)
         h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
         lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_engine_sync(h)
         lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_engine_sync(h)
