@@ -165,6 +165,18 @@ __device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool
     return Fwd{cw, nw};
 }
 
+// fwd_chunk for a chunk known to lie inside the column (0 <= F < kChunks): no bounds handling
+__device__ __forceinline__ Fwd fwd_chunk_in(const uint32_t* col, int c, int F, bool rc) {
+    const int w = rc ? kChunks - 1 - F : F;
+    uint32_t cw = col[(kFC + w) * 64 + c], nw = col[(kFN + w) * 64 + c];
+    if (rc) {
+        cw = pairrev(cw);
+        nw = pairrev(nw);
+        cw ^= 0xAAAAAAAAu & ~(nw << 1);  // complement back, N stays code 3
+    }
+    return Fwd{cw, nw};
+}
+
 struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N)
     const uint32_t* col;
     int c;
@@ -627,8 +639,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 #pragma unroll
                     for (int j = 0; j < 4; ++j) dword(j, std::false_type{});
                 }
-                const uint32_t fck = tr4x4(cc), fwk = tr4x4(nn4);
-                nbf += __popc(fwk & (full ? 0x55555555u : posmask(Lk)));
+                // N flags are kept only for positions inside the read (later passes rely on it)
+                const uint32_t fck = tr4x4(cc), fwk = tr4x4(nn4) & (full ? 0x55555555u : posmask(Lk));
+                nbf += __popc(fwk);
                 // read 2: the column is the reverse complement of the 160-position row, so the
                 // read's rc position j sits at index j + (160 - L); garbage beyond L lands below
                 const uint32_t rn = pairrev(fwk);
@@ -974,29 +987,35 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 rwb[t] = blk0 + 8u * (uint32_t)((t + r) & 15);
                 asm volatile("" : "+v"(rwb[t]));  // kept whole (not re-split into base + offset per use)
             }
-            Fwd fn = fwd_chunk(col, lane_x, 0, rc);
-            uint4 qn = qchunk(0);
-            uint4 qnn = qchunk(min(1, nchunks - 1));
+            // quality chunks rotate through three registers (requested two chunks ahead)
+            uint4 qb[3];
+            qb[0] = qchunk(0);
+            qb[1] = qchunk(min(1, nchunks - 1));
+            Fwd fn = fwd_chunk_in(col, lane_x, 0, rc);
+            // nibble prefix masks from one 64-bit shift: ~(~0 << 4 * clamp(len, 0, 16)), the
+            // 64th bit never needed (nibble 15's top bit is 0 in 0x4444... and 0xAAAA... masks)
+            const int w4 = 4 * wlen, l4 = 4 * L;
 #pragma unroll
             for (int F = 0; F < kChunks; ++F) {
                 if (F < nch) {  // wave-uniform; positions >= L are dummies
                     const Fwd f = fn;
-                    const uint32_t q0 = qn.x, q1 = qn.y, q2 = qn.z, q3 = qn.w;
-                    qn = qnn;
-                    if (F + 2 < kChunks) qnn = qchunk(min(F + 2, nchunks - 1));
-                    if (F + 1 < kChunks) fn = fwd_chunk(col, lane_x, min(F + 1, nchunks - 1), rc);
-                    const int kl = wlen - 16 * F, vl = L - 16 * F;
+                    const uint32_t q0 = qb[F % 3].x, q1 = qb[F % 3].y, q2 = qb[F % 3].z, q3 = qb[F % 3].w;
+                    if (F + 2 < kChunks) qb[(F + 2) % 3] = qchunk(min(F + 2, nchunks - 1));
+                    if (F + 1 < kChunks) fn = fwd_chunk_in(col, lane_x, min(F + 1, nchunks - 1), rc);
+                    const int vl = L - 16 * F;
                     // slot 4 * kept + code; an N (code 3) is counted as a G here and moved below
-                    uint32_t lo = spread2to4(f.c) + (kl >= 8 ? 0x44444444u : __builtin_amdgcn_ubfe(0x44444444u, 0, 4 * max(kl, 0)));
-                    uint32_t hi = spread2to4(f.c >> 16) + (kl >= 16 ? 0x44444444u : __builtin_amdgcn_ubfe(0x44444444u, 0, 4 * min(max(kl - 8, 0), 7)));
+                    const unsigned long long km = ~(~0ull << min(max(w4 - 64 * F, 0), 63));
+                    uint32_t lo = spread2to4(f.c) + ((uint32_t)km & 0x44444444u);
+                    uint32_t hi = spread2to4(f.c >> 16) + ((uint32_t)(km >> 32) & 0x44444444u);
                     if (__any(vl < 16)) {  // positions beyond the read (kept is 0 there) -> dummy slot 10
-                        const uint32_t dlo = vl >= 8 ? 0u : ~__builtin_amdgcn_ubfe(~0u, 0, 4 * max(vl, 0));
-                        const uint32_t dhi = vl >= 16 ? 0u : ~__builtin_amdgcn_ubfe(~0u, 0, 4 * min(max(vl - 8, 0), 7));
+                        const unsigned long long vm = ~0ull << min(max(l4 - 64 * F, 0), 63);
+                        const uint32_t dlo = (uint32_t)vm, dhi = vl >= 16 ? 0u : (uint32_t)(vm >> 32);
                         lo = (lo & ~dlo) | (dlo & 0xAAAAAAAAu);
                         hi = (hi & ~dhi) | (dhi & 0xAAAAAAAAu);
                     }
                     // N bases (rare): move each from its G cell (slot 4 * kept + 3) to slot 8 + kept
-                    uint32_t nv = f.n & posmask(vl);
+                    // (staging kept N flags only inside the read)
+                    uint32_t nv = f.n;
                     if (__any(nv != 0)) {
                         const uint32_t qs[4] = {q0, q1, q2, q3};
                         while (nv) {
