@@ -361,20 +361,25 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
         csa(twosB, ones, ones, m(14), m(15));
         csa(foursB, twos, twos, twosA, twosB);
         csa(eightsB, fours, fours, foursA, foursB);
-        csa(sixteen, eights, eights, eightsA, eightsB);
-        // count < K, bit-sliced against the wave-uniform K
-        uint32_t lt = 0u, eq = ~0u;
-        const uint32_t cb[5] = {ones, twos, fours, eights, sixteen};
+        uint32_t lt;
+        if (K == 5) {  // the default overlap_diff_limit: count < 5 <=> no 8s or 16s, not (4 and (2 or 1))
+            lt = ~(eights | eightsA | eightsB | (fours & (twos | ones)));
+        } else {  // count < K, bit-sliced against the wave-uniform K
+            csa(sixteen, eights, eights, eightsA, eightsB);
+            uint32_t eq = ~0u;
+            lt = 0u;
+            const uint32_t cb[5] = {ones, twos, fours, eights, sixteen};
 #pragma unroll
-        for (int i = 4; i >= 0; --i) {
-            if ((K >> i) & 1) {
-                lt |= eq & ~cb[i];
-                eq &= cb[i];
-            } else {
-                eq &= ~cb[i];
+            for (int i = 4; i >= 0; --i) {
+                if ((K >> i) & 1) {
+                    lt |= eq & ~cb[i];
+                    eq &= cb[i];
+                } else {
+                    eq &= ~cb[i];
+                }
             }
+            if (K > 31) lt = ~0u;
         }
-        if (K > 31) lt = ~0u;
         const int nb = cnt - 32 * bk;  // valid offsets of this block
         cand[bk] = lt & (nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u));
         L0 = L1;
