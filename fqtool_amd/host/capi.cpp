@@ -102,6 +102,7 @@ void fqh_free(char* p) { std::free(p); }
 // ---- host session: the tool's pipeline with the per-pack engine call left to the caller ----
 struct fqh_session {
     Options o;
+    std::unique_ptr<Pool> pool;  // -w threads: tile packing, formatting, gzip
     std::unique_ptr<PackReader> reader;
     Pack pk;
     std::unique_ptr<OutputSet> outs;
@@ -119,7 +120,8 @@ int fqh_session_open(int argc, char** argv, fqh_session** out) {
         s->o = prepare_options(argc, argv);
         s->acc = HostAcc(s->o.insert_size_max);
         s->reader.reset(new PackReader(s->o.in1, s->o.in2, s->o.interleaved, s->o.phred64));
-        s->outs.reset(new OutputSet(s->o));
+        s->pool.reset(new Pool(std::max(0, s->o.threads - 1)));
+        s->outs.reset(new OutputSet(s->o, s->pool.get()));
     } catch (const std::exception& e) {
         s->err = e.what();
         *out = s.release();
@@ -138,7 +140,7 @@ int fqh_session_params(fqh_session* s, int max_cycles, fq_params* out) {
 int fqh_session_next(fqh_session* s, int max_n, fq_batch* out) {
     try {
         s->pk = Pack();
-        if (!s->reader->next(s->pk, (size_t)max_n)) return 0;
+        if (!s->reader->next(s->pk, (size_t)max_n, s->pool.get())) return 0;
         *out = s->pk.batch();
         return 1;
     } catch (const std::exception& e) {
@@ -154,7 +156,7 @@ int fqh_session_consume(fqh_session* s, const fq_read_result* res, int max_cycle
         const fq_params p = s->o.to_params(max_cycles);
         if (s->o.adapter_trimming) s->ac.add(s->pk, res, p);
         PackOutput out;
-        format_pack(s->o, s->pk, res, out);
+        format_pack(s->o, s->pk, res, out, s->pool.get());
         s->outs->write(std::move(out));
         return 0;
     } catch (const std::exception& e) {

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <iostream>
 #include <memory>
 #include <sstream>
 
@@ -143,15 +144,24 @@ int evaluate_read_len(const std::string& path) {  // Evaluator::computeReadLen, 
 }
 
 // Evaluator::evaluateAdapterSeq, src/evaluator.cpp:229-390
-std::string detect_adapter(const std::string& path, int trim_tail1) {
+std::string detect_adapter(const std::string& path, int trim_tail1, std::string* msgs) {
     const size_t kReadLimit = 256 * 1024, kBaseLimit = 151 * kReadLimit;
     FqReader r(path, false);
     std::vector<std::string> reads;
     size_t bases = 0;
-    std::string n, s, d, q;
-    while (reads.size() < kReadLimit && bases < kBaseLimit && r.read(n, s, d, q)) {
-        bases += s.size();
-        reads.push_back(s);
+    ByteBuf text;
+    Rec rec;
+    while (reads.size() < kReadLimit && bases < kBaseLimit) {
+        text.clear();
+        if (!r.read(text, rec)) {
+            if (!r.error().empty()) {
+                if (msgs) *msgs += r.error();
+                else std::cerr << r.error();
+            }
+            break;
+        }
+        bases += rec.len;
+        reads.emplace_back(text.data() + rec.off + rec.name_len, rec.len);
     }
     if (reads.size() < 10000) return "";
     const int shift_tail = std::max(1, trim_tail1);

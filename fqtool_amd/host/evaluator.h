@@ -8,7 +8,9 @@ namespace fqhost {
 
 // longest of the first 1000 reads
 int evaluate_read_len(const std::string& path);
-// detected adapter of one mate file ("" when none), trim_tail1 = -t as the reference passes it
-std::string detect_adapter(const std::string& path, int trim_tail1);
+// detected adapter of one mate file ("" when none), trim_tail1 = -t as the reference passes it.
+// A read error message goes to *msgs when given (so two concurrent detections can report in
+// the reference's order), else straight to stderr.
+std::string detect_adapter(const std::string& path, int trim_tail1, std::string* msgs = nullptr);
 
 }  // namespace fqhost

@@ -2,9 +2,13 @@
 #include "fastq.h"
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <iostream>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 
 namespace fqhost {
@@ -15,12 +19,29 @@ constexpr int kBufSize = 1 << 20;  // src/fqreader.cpp:10
 bool ends_with(const std::string& s, const std::string& suf) {
     return s.size() >= suf.size() && s.compare(s.size() - suf.size(), suf.size(), suf) == 0;
 }
+
+// first '\r' or '\n' in [p, p + n), or p + n
+const char* line_end(const char* p, size_t n) {
+    const char* nl = static_cast<const char*>(std::memchr(p, '\n', n));
+    const size_t upto = nl ? (size_t)(nl - p) : n;
+    const char* cr = static_cast<const char*>(std::memchr(p, '\r', upto));
+    return cr ? cr : p + upto;
+}
 }  // namespace
+
+void ByteBuf::reserve(size_t n) {
+    if (n <= cap_) return;
+    std::unique_ptr<char[]> q(new char[n]);
+    if (size_) std::memcpy(q.get(), p_.get(), size_);
+    p_ = std::move(q);
+    cap_ = n;
+}
 
 FqReader::FqReader(const std::string& path, bool phred64) : phred64_(phred64), buf_(kBufSize) {
     if (ends_with(path, ".gz")) {
         gz_ = gzopen(path.c_str(), "r");
         if (!gz_) throw std::runtime_error("Failed to open file: " + path);
+        gzbuffer(gz_, 1 << 20);
         gzrewind(gz_);
     } else {
         fp_ = path == "/dev/stdin" ? stdin : std::fopen(path.c_str(), "rb");
@@ -49,68 +70,253 @@ void FqReader::fill() {  // FqReader::readToBuf, src/fqreader.cpp:30-44
     used_ = 0;
 }
 
-bool FqReader::at_eof() const { return eof_; }
-
-// FqReader::getLine, src/fqreader.cpp:90-150
-bool FqReader::get_line(std::string& out) {
-    int start = used_, end = start;
-    while (end < len_ && buf_[end] != '\r' && buf_[end] != '\n') ++end;
+// FqReader::getLine, src/fqreader.cpp:90-150: appends the next line to `out`.  A line ends at
+// '\r' or '\n'; a '\n' right after the '\r' is consumed too unless the '\r' is the buffer's
+// second-to-last byte or later (the reference's `end < len-1` test).
+void FqReader::get_line(ByteBuf& out) {
+    const int start = used_;
+    const char* b = buf_.data();
+    int end = start < len_ ? (int)(line_end(b + start, (size_t)(len_ - start)) - b) : start;
     if (end < len_ || len_ < kBufSize) {
-        out.assign(buf_.data() + std::min(start, len_), (size_t)std::max(0, end - start));
+        const int s = std::min(start, len_);
+        const int k = std::max(0, end - start);
+        if (k) std::memcpy(out.extend((size_t)k), b + s, (size_t)k);
         ++end;
-        if (end < len_ - 1 && buf_[end] == '\n') ++end;
+        if (end < len_ - 1 && b[end] == '\n') ++end;
         used_ = end;
-        return true;
+        return;
     }
-    out.assign(buf_.data() + start, (size_t)(len_ - start));
+    if (len_ > start) std::memcpy(out.extend((size_t)(len_ - start)), b + start, (size_t)(len_ - start));
     for (;;) {
         fill();
-        start = 0;
-        end = 0;
-        while (end < len_ && buf_[end] != '\r' && buf_[end] != '\n') ++end;
+        b = buf_.data();
+        end = len_ > 0 ? (int)(line_end(b, (size_t)len_) - b) : 0;
         if (end < len_ || len_ < kBufSize) {
-            out.append(buf_.data() + start, (size_t)(end - start));
+            if (end) std::memcpy(out.extend((size_t)end), b, (size_t)end);
             ++end;
-            if (end < len_ - 1 && buf_[end] == '\n') ++end;
+            if (end < len_ - 1 && b[end] == '\n') ++end;
             used_ = end;
-            return true;
+            return;
         }
-        out.append(buf_.data() + start, (size_t)(len_ - start));
+        if (len_) std::memcpy(out.extend((size_t)len_), b, (size_t)len_);
     }
 }
 
 // FqReader::read, src/fqreader.cpp:160-195
-bool FqReader::read(std::string& name, std::string& seq, std::string& strand, std::string& qual) {
+bool FqReader::read(ByteBuf& text, Rec& r) {
+    err_.clear();
     if (used_ >= len_ && at_eof()) return false;
-    get_line(name);
-    while ((name.empty() && !(used_ >= len_ && at_eof())) || (!name.empty() && name[0] != '@')) get_line(name);
-    if (name.empty()) return false;
-    get_line(seq);
-    get_line(strand);
-    get_line(qual);
-    if (qual.size() != seq.size()) {
-        std::cerr << "Error: base sequnce and quality sequence have different length: \n"
-                  << name << "\n" << seq << "\n" << qual << "\n" << strand << "\n";
+    const size_t off = text.size();
+    get_line(text);
+    for (;;) {  // skip to a line that starts with '@' (src/fqreader.cpp:169-171)
+        const bool empty = text.size() == off;
+        if ((empty && !(used_ >= len_ && at_eof())) || (!empty && text.data()[off] != '@')) {
+            text.truncate(off);
+            get_line(text);
+        } else {
+            break;
+        }
+    }
+    if (text.size() == off) return false;
+    const size_t name_len = text.size() - off;
+    get_line(text);
+    const size_t seq_len = text.size() - off - name_len;
+    get_line(text);
+    const size_t strand_len = text.size() - off - name_len - seq_len;
+    get_line(text);
+    const size_t qual_len = text.size() - off - name_len - seq_len - strand_len;
+    char* p = text.data() + off;
+    if (qual_len != seq_len) {
+        const std::string name(p, name_len), seq(p + name_len, seq_len), strand(p + name_len + seq_len, strand_len),
+            qual(p + name_len + seq_len + strand_len, qual_len);
+        err_ = "Error: base sequnce and quality sequence have different length: \n" + name + "\n" + seq + "\n" + qual +
+               "\n" + strand + "\n";
+        text.truncate(off);
         return false;
     }
-    if (phred64_)  // Read::convertPhread64To33, src/read.h:71-75 (char arithmetic)
-        for (char& c : qual) c = (char)std::max(33, (int)c - (64 - 33));
+    if (phred64_) {  // Read::convertPhread64To33, src/read.h:71-75 (char arithmetic)
+        char* q = p + name_len + seq_len + strand_len;
+        for (size_t i = 0; i < qual_len; ++i) q[i] = (char)std::max(33, (int)q[i] - (64 - 33));
+    }
+    r.off = off;
+    r.name_len = (uint32_t)name_len;
+    r.strand_len = (uint32_t)strand_len;
+    r.len = (uint32_t)seq_len;
     return true;
+}
+
+bool FqReader::read(std::string& name, std::string& seq, std::string& strand, std::string& qual) {
+    scratch_.clear();
+    Rec r;
+    if (!read(scratch_, r)) {
+        if (!err_.empty()) std::cerr << err_;
+        return false;
+    }
+    const char* p = scratch_.data() + r.off;
+    name.assign(p, r.name_len);
+    seq.assign(p + r.name_len, r.len);
+    strand.assign(p + r.name_len + r.len, r.strand_len);
+    qual.assign(p + r.name_len + r.len + r.strand_len, r.len);
+    return true;
+}
+
+// ---- Pool ----
+struct Pool::Impl {
+    struct Job {
+        int n = 0;
+        const std::function<void(int)>* fn = nullptr;
+        std::atomic<int> next{0}, done{0};
+    };
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    std::deque<std::shared_ptr<Job>> jobs;
+    std::vector<std::thread> threads;
+    bool stop = false;
+
+    // runs indices of `j` until none are left; true when this call finished the job's last one
+    static bool work(Job& j) {
+        bool last = false;
+        for (int i; (i = j.next.fetch_add(1)) < j.n;) {
+            (*j.fn)(i);
+            if (j.done.fetch_add(1) + 1 == j.n) last = true;
+        }
+        return last;
+    }
+    void loop() {
+        std::unique_lock<std::mutex> l(m);
+        for (;;) {
+            cv.wait(l, [&] { return stop || !jobs.empty(); });
+            if (stop) return;
+            std::shared_ptr<Job> j = jobs.front();
+            if (j->next.load() >= j->n) {  // every index taken: drop it and look again
+                jobs.pop_front();
+                continue;
+            }
+            l.unlock();
+            const bool last = work(*j);
+            l.lock();
+            if (last) done_cv.notify_all();
+        }
+    }
+};
+
+Pool::Pool(int workers) : impl_(new Impl), workers_(std::max(0, workers)) {
+    for (int i = 0; i < workers_; ++i) impl_->threads.emplace_back([this] { impl_->loop(); });
+}
+
+Pool::~Pool() {
+    {
+        std::lock_guard<std::mutex> l(impl_->m);
+        impl_->stop = true;
+    }
+    impl_->cv.notify_all();
+    for (auto& t : impl_->threads) t.join();
+}
+
+void Pool::run(int n, const std::function<void(int)>& fn) {
+    if (n <= 0) return;
+    if (workers_ == 0 || n == 1) {
+        for (int i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    auto j = std::make_shared<Impl::Job>();
+    j->n = n;
+    j->fn = &fn;
+    {
+        std::lock_guard<std::mutex> l(impl_->m);
+        impl_->jobs.push_back(j);
+    }
+    impl_->cv.notify_all();
+    Impl::work(*j);
+    std::unique_lock<std::mutex> l(impl_->m);
+    impl_->done_cv.wait(l, [&] { return j->done.load() == n; });
+    for (auto it = impl_->jobs.begin(); it != impl_->jobs.end(); ++it)
+        if (*it == j) {
+            impl_->jobs.erase(it);
+            break;
+        }
+}
+
+// ---- Pack ----
+void Pack::clear() {
+    n = 0;
+    stride = 0;
+    for (int m = 0; m < 2; ++m) {
+        text[m].clear();
+        rec[m].clear();
+        seq[m].clear();
+        qual[m].clear();
+        len[m].clear();
+    }
 }
 
 fq_batch Pack::batch() const {
     fq_batch b;
     b.n = n;
     b.stride = stride;
-    b.seq1 = seq[0].data();
-    b.qual1 = qual[0].data();
+    b.seq1 = reinterpret_cast<const uint8_t*>(seq[0].data());
+    b.qual1 = reinterpret_cast<const uint8_t*>(qual[0].data());
     b.len1 = len[0].data();
-    b.seq2 = paired ? seq[1].data() : nullptr;
-    b.qual2 = paired ? qual[1].data() : nullptr;
+    b.seq2 = paired ? reinterpret_cast<const uint8_t*>(seq[1].data()) : nullptr;
+    b.qual2 = paired ? reinterpret_cast<const uint8_t*>(qual[1].data()) : nullptr;
     b.len2 = paired ? len[1].data() : nullptr;
     return b;
 }
 
+void pack_tiles(Pack& pk, Pool* pool) {
+    const int mates = pk.paired ? 2 : 1;
+    size_t maxlen = 0;
+    for (int m = 0; m < mates; ++m) {
+        pk.len[m].resize((size_t)pk.n);
+        for (int i = 0; i < pk.n; ++i) {
+            const uint32_t l = pk.rec[m][(size_t)i].len;
+            if (l > 65535) throw std::runtime_error("read longer than 65535 bases");
+            pk.len[m][(size_t)i] = (uint16_t)l;
+            maxlen = std::max<size_t>(maxlen, l);
+        }
+    }
+    pk.stride = (int)std::max<size_t>(16, (maxlen + 15) & ~(size_t)15);
+    const size_t bytes = fq_batch_bytes(pk.n, pk.stride);
+    const size_t tile_bytes = (size_t)FQ_TILE_READS * (size_t)pk.stride;
+    for (int m = 0; m < mates; ++m) {
+        pk.seq[m].resize_uninit(bytes);
+        pk.qual[m].resize_uninit(bytes);
+    }
+    for (int m = mates; m < 2; ++m) {
+        pk.seq[m].clear();
+        pk.qual[m].clear();
+        pk.len[m].clear();
+    }
+    const int tiles = (pk.n + FQ_TILE_READS - 1) / FQ_TILE_READS;
+    const int parts = pool ? std::min(tiles, pool->size() * 4) : 1;
+    auto work = [&](int part) {
+        const int t0 = (int)((int64_t)tiles * part / parts), t1 = (int)((int64_t)tiles * (part + 1) / parts);
+        for (int m = 0; m < mates; ++m) {
+            char* sp = pk.seq[m].data();
+            char* qp = pk.qual[m].data();
+            for (int t = t0; t < t1; ++t) {
+                std::memset(sp + (size_t)t * tile_bytes, 0, tile_bytes);
+                std::memset(qp + (size_t)t * tile_bytes, 0, tile_bytes);
+                const int i1 = std::min(pk.n, (t + 1) * FQ_TILE_READS);
+                for (int i = t * FQ_TILE_READS; i < i1; ++i) {
+                    const Rec& r = pk.rec[m][(size_t)i];
+                    const char* s = pk.text[m].data() + r.off + r.name_len;
+                    const char* q = s + r.len + r.strand_len;
+                    for (uint32_t j = 0; j < r.len; j += FQ_CHUNK) {
+                        const size_t k = std::min<size_t>(FQ_CHUNK, r.len - j);
+                        const size_t o = fq_batch_offset(pk.stride, i, (int32_t)j);
+                        std::memcpy(sp + o, s + j, k);
+                        std::memcpy(qp + o, q + j, k);
+                    }
+                }
+            }
+        }
+    };
+    if (pool) pool->run(parts, work);
+    else if (tiles) work(0);
+}
+
+// ---- PackReader ----
 PackReader::PackReader(const std::string& in1, const std::string& in2, bool interleaved, bool phred64)
     : r1_(in1, phred64), paired_(!in2.empty() || interleaved), interleaved_(interleaved) {
     if (!in2.empty() && !interleaved) {
@@ -121,91 +327,119 @@ PackReader::PackReader(const std::string& in1, const std::string& in2, bool inte
     }
 }
 
-bool PackReader::next(Pack& pk, size_t max_n) {
+namespace {
+size_t read_mate(FqReader& r, Pack& pk, int m, size_t max_n) {
+    Rec rc;
+    size_t k = 0;
+    while (k < max_n && r.read(pk.text[m], rc)) {
+        pk.rec[m].push_back(rc);
+        ++k;
+    }
+    return k;
+}
+}  // namespace
+
+bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     if (done_) return false;
-    const int mates = paired_ ? 2 : 1;
+    pk.clear();
     pk.paired = paired_;
-    pk.n = 0;
-    for (int m = 0; m < 2; ++m) {
-        pk.name[m].clear();
-        pk.strand[m].clear();
-        pk.seq_text[m].clear();
-        pk.qual_text[m].clear();
-    }
-    size_t maxlen = 0;
-    std::string nm, sq, sd, ql;
-    while ((size_t)pk.n < max_n) {
-        bool ok = true;
-        std::string names[2], seqv[2], strands[2], qualv[2];
-        for (int m = 0; m < mates && ok; ++m) {  // FqReaderPair::read, src/fqreader.cpp:254-267
-            FqReader* r = m == 0 ? &r1_ : r2_;
-            ok = r->read(names[m], seqv[m], strands[m], qualv[m]);
-        }
-        if (!ok) {
-            done_ = true;
-            break;
-        }
-        for (int m = 0; m < mates; ++m) {
-            maxlen = std::max(maxlen, seqv[m].size());
-            pk.name[m].push_back(std::move(names[m]));
-            pk.strand[m].push_back(std::move(strands[m]));
-            pk.seq_text[m].push_back(std::move(seqv[m]));
-            pk.qual_text[m].push_back(std::move(qualv[m]));
-        }
-        ++pk.n;
-    }
-    if (pk.n == 0) return false;
-    if (maxlen > 65535) throw std::runtime_error("read longer than 65535 bases");
-    pk.stride = (int)std::max<size_t>(16, (maxlen + 15) & ~(size_t)15);
-    for (int m = 0; m < mates; ++m) {
-        const size_t bytes = fq_batch_bytes(pk.n, pk.stride);
-        pk.seq[m].assign(bytes, 0);
-        pk.qual[m].assign(bytes, 0);
-        pk.len[m].resize((size_t)pk.n);
-        for (int i = 0; i < pk.n; ++i) {
-            const std::string& s = pk.seq_text[m][i];
-            const std::string& q = pk.qual_text[m][i];
-            // chunk-interleaved tiles: 16-byte pieces of the row, 512 bytes apart
-            for (size_t j = 0; j < s.size(); j += FQ_CHUNK) {
-                const size_t k = std::min<size_t>(FQ_CHUNK, s.size() - j);
-                const size_t o = fq_batch_offset(pk.stride, i, (int32_t)j);
-                std::memcpy(&pk.seq[m][o], s.data() + j, k);
-                std::memcpy(&pk.qual[m][o], q.data() + j, k);
-            }
-            pk.len[m][i] = (uint16_t)s.size();
-        }
-    }
+    size_t n = 0;
     if (!paired_) {
-        pk.seq[1].clear();
-        pk.qual[1].clear();
-        pk.len[1].clear();
+        n = read_mate(r1_, pk, 0, max_n);
+        if (n < max_n) {
+            done_ = true;
+            if (!r1_.error().empty()) std::cerr << r1_.error();
+        }
+    } else if (interleaved_) {  // FqReaderPair over one file: mate 1, then mate 2
+        Rec a, b;
+        while (n < max_n) {
+            if (!r1_.read(pk.text[0], a) || !r1_.read(pk.text[1], b)) {
+                done_ = true;
+                if (!r1_.error().empty()) std::cerr << r1_.error();
+                break;
+            }
+            pk.rec[0].push_back(a);
+            pk.rec[1].push_back(b);
+            ++n;
+        }
+    } else {
+        // One thread per mate.  FqReaderPair::read (src/fqreader.cpp:254-267) reads mate 1, then
+        // mate 2, and stops at the first that fails: the pair count is the shorter run, and only
+        // the mate the sequential reader would have failed on reports its error.
+        size_t n2 = 0;
+        std::thread t([&] { n2 = read_mate(*r2_, pk, 1, max_n); });
+        const size_t n1 = read_mate(r1_, pk, 0, max_n);
+        t.join();
+        n = std::min(n1, n2);
+        if (n < max_n) {
+            done_ = true;
+            const std::string& e = n1 <= n2 ? r1_.error() : r2_->error();
+            if (!e.empty()) std::cerr << e;
+        }
+        pk.rec[0].resize(n);
+        pk.rec[1].resize(n);
     }
+    if (n == 0) return false;
+    pk.n = (int)n;
+    pack_tiles(pk, pool);
     pk.seq_no = packs_++;
-    reads_ += (uint64_t)pk.n * mates;
+    reads_ += (uint64_t)pk.n * (paired_ ? 2 : 1);
     return true;
 }
 
-Writer::Writer(const std::string& path, int level) {
-    if (ends_with(path, ".gz")) {  // src/writer.cpp:36-47
-        gz_ = gzopen(path.c_str(), "w");
-        if (!gz_) throw std::runtime_error("cannot open " + path);
-        gzsetparams(gz_, level, Z_DEFAULT_STRATEGY);
-        gzbuffer(gz_, 1024 * 1024);
-    } else {
-        fp_ = std::fopen(path.c_str(), "wb");
-        if (!fp_) throw std::runtime_error("cannot open " + path);
-    }
+// ---- Writer ----
+Writer::Writer(const std::string& path, int level) : gzip_(ends_with(path, ".gz")), level_(level) {
+    fp_ = std::fopen(path.c_str(), "wb");
+    if (!fp_) throw std::runtime_error("cannot open " + path);
 }
 
+namespace {
+// one complete gzip member holding `s` (src/writer.cpp:36-47 writes through gzwrite at level -z)
+std::string gzip_member(const std::string& s, int level) {
+    z_stream z;
+    std::memset(&z, 0, sizeof z);
+    if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+        throw std::runtime_error("deflateInit2 failed");
+    std::string out;
+    out.resize(deflateBound(&z, (uLong)s.size()) + 64);
+    z.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(s.data()));
+    z.avail_in = (uInt)s.size();
+    z.next_out = reinterpret_cast<Bytef*>(&out[0]);
+    z.avail_out = (uInt)out.size();
+    const int rc = deflate(&z, Z_FINISH);
+    deflateEnd(&z);
+    if (rc != Z_STREAM_END) throw std::runtime_error("deflate failed");
+    out.resize(z.total_out);
+    return out;
+}
+}  // namespace
+
 Writer::~Writer() {
-    if (gz_) gzclose(gz_);
+    if (gzip_ && !any_member_) {  // an empty .gz output is still one (empty) gzip member
+        const std::string e = gzip_member(std::string(), level_);
+        std::fwrite(e.data(), 1, e.size(), fp_);
+    }
     if (fp_) std::fclose(fp_);
 }
 
-void Writer::write(const std::string& s) {
-    if (s.empty()) return;
-    if (gz_) gzwrite(gz_, s.data(), (unsigned)s.size());
-    else std::fwrite(s.data(), 1, s.size(), fp_);
+void Writer::write(const std::vector<std::string>& blocks, Pool* pool) {
+    if (!gzip_) {
+        for (const auto& s : blocks)
+            if (!s.empty()) std::fwrite(s.data(), 1, s.size(), fp_);
+        return;
+    }
+    std::vector<std::string> z(blocks.size());
+    auto work = [&](int i) {
+        if (!blocks[(size_t)i].empty()) z[(size_t)i] = gzip_member(blocks[(size_t)i], level_);
+    };
+    if (pool) pool->run((int)blocks.size(), work);
+    else
+        for (int i = 0; i < (int)blocks.size(); ++i) work(i);
+    for (const auto& s : z)
+        if (!s.empty()) {
+            std::fwrite(s.data(), 1, s.size(), fp_);
+            any_member_ = true;
+        }
 }
 
 }  // namespace fqhost

@@ -43,19 +43,21 @@ char comp(char c) {
     }
 }
 
-// A read as the loop body sees it after its in-place edits.
+// A read as the loop body sees it after its in-place edits (fields point into the pack's text).
 struct View {
-    const std::string* name;
-    const std::string* strand;
+    const char* name;
+    size_t name_len;
+    const char* strand;
+    size_t strand_len;
     const char* seq;
     const char* qual;
     int len;
 };
 
 View view(const Pack& pk, int m, int i, const fq_read_result* r) {
-    const char* s = pk.seq_text[m][(size_t)i].data();
-    const char* q = pk.qual_text[m][(size_t)i].data();
-    View v{&pk.name[m][(size_t)i], &pk.strand[m][(size_t)i], s, q, (int)pk.len[m][(size_t)i]};
+    const Rec& rc = pk.rec[m][(size_t)i];
+    View v{pk.name(m, (size_t)i), rc.name_len, pk.strand(m, (size_t)i), rc.strand_len,
+           pk.seq_text(m, (size_t)i), pk.qual_text(m, (size_t)i), (int)rc.len};
     if (r && !(r->flags & FQ_RF_NULL)) {  // trimmed in place; a NULL read keeps the original
         v.seq += r->start;
         v.qual += r->start;
@@ -66,7 +68,7 @@ View view(const Pack& pk, int m, int i, const fq_read_result* r) {
 
 // Read::toString / toStringWithTag, reference src/read.h:166-178
 void append_read(std::string& out, const View& v, const char* tag = nullptr) {
-    out += *v.name;
+    out.append(v.name, v.name_len);
     if (tag) {
         out += ' ';
         out += tag;
@@ -74,34 +76,41 @@ void append_read(std::string& out, const View& v, const char* tag = nullptr) {
     out += '\n';
     out.append(v.seq, (size_t)v.len);
     out += '\n';
-    out += *v.strand;
+    out.append(v.strand, v.strand_len);
     out += '\n';
     out.append(v.qual, (size_t)v.len);
     out += '\n';
 }
 
-}  // namespace
-
-std::string merged_name(const std::string& name, int len1, int len2) {
-    const std::string tag = "_merged_" + std::to_string(len1) + "_" + std::to_string(len2);
-    const size_t pos = name.find_first_of(' ');
-    if (pos == std::string::npos) return tag;
-    return name.substr(0, pos - 1) + tag + name.substr(pos);
+// text bytes of mate m's records [i0, i1) plus their line breaks: their untrimmed output size
+size_t span_bytes(const Pack& pk, int m, int i0, int i1) {
+    if (i1 <= i0) return 0;
+    const Rec& a = pk.rec[m][(size_t)i0];
+    const Rec& b = pk.rec[m][(size_t)i1 - 1];
+    return (size_t)(b.off - a.off) + b.name_len + 2 * (size_t)b.len + b.strand_len + 4 * (size_t)(i1 - i0);
 }
 
-void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out) {
+// the loop bodies' appends for reads (pairs) [i0, i1), into block k of each destination
+void format_range(const Options& o, const Pack& pk, const fq_read_result* res, int i0, int i1, size_t k,
+                  PackOutput& out) {
     const bool has_unpaired_left = !o.unpaired1.empty();
     const bool has_failed = !o.failed_out.empty();
+    std::string& o1 = out.out1[k];
+    std::string& o2 = out.out2[k];
+    std::string& u1 = out.unpaired1[k];
+    std::string& u2 = out.unpaired2[k];
+    std::string& fl = out.failed[k];
+    std::string& mg = out.merged[k];
     if (!pk.paired) {  // src/seprocessor.cpp:337-350
-        for (int i = 0; i < pk.n; ++i) {
+        for (int i = i0; i < i1; ++i) {
             const fq_read_result& r = res[i];
             const View v = view(pk, 0, i, &r);
-            if (!(r.flags & FQ_RF_NULL) && r.code == FQ_PASS_FILTER) append_read(out.out1, v);
-            else if (has_failed) append_read(out.failed, v, failed_type(r.code));
+            if (!(r.flags & FQ_RF_NULL) && r.code == FQ_PASS_FILTER) append_read(o1, v);
+            else if (has_failed) append_read(fl, v, failed_type(r.code));
         }
         return;
     }
-    for (int i = 0; i < pk.n; ++i) {  // src/peprocessor.cpp:351-429
+    for (int i = i0; i < i1; ++i) {  // src/peprocessor.cpp:351-429
         const fq_read_result& a = res[2 * (size_t)i];
         const fq_read_result& b = res[2 * (size_t)i + 1];
         const bool nn1 = !(a.flags & FQ_RF_NULL), nn2 = !(b.flags & FQ_RF_NULL);
@@ -117,51 +126,81 @@ void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, Pa
                         seq += comp(v2.seq[src]);
                         qual += v2.qual[src];
                     }
-                    const std::string name = merged_name(*v1.name, m1, m2);
-                    View mv{&name, v1.strand, seq.data(), qual.data(), (int)seq.size()};
-                    append_read(out.merged, mv);
+                    const std::string name = merged_name(std::string(v1.name, v1.name_len), m1, m2);
+                    const View mv{name.data(), name.size(), v1.strand, v1.strand_len, seq.data(), qual.data(),
+                                  (int)seq.size()};
+                    append_read(mg, mv);
                 }
                 merge_processed = true;
             } else if (!o.discard_unmerged) {
-                if (a.code == FQ_PASS_FILTER) append_read(out.merged, v1);
-                if (b.code == FQ_PASS_FILTER) append_read(out.merged, v2);
+                if (a.code == FQ_PASS_FILTER) append_read(mg, v1);
+                if (b.code == FQ_PASS_FILTER) append_read(mg, v2);
                 merge_processed = true;
             }
         }
         if (merge_processed) continue;
         const bool p1 = nn1 && a.code == FQ_PASS_FILTER, p2 = nn2 && b.code == FQ_PASS_FILTER;
         if (p1 && p2) {
-            append_read(out.out1, v1);
-            append_read(out.out2, v2);
+            append_read(o1, v1);
+            append_read(o2, v2);
         } else if (p1) {
             if (has_unpaired_left) {
-                append_read(out.unpaired1, v1);
-                if (has_failed) append_read(out.failed, v2, failed_type(b.code));
+                append_read(u1, v1);
+                if (has_failed) append_read(fl, v2, failed_type(b.code));
             } else if (has_failed) {
-                append_read(out.failed, v1, "paired_read_is_failing");
-                append_read(out.failed, v2, failed_type(b.code));
+                append_read(fl, v1, "paired_read_is_failing");
+                append_read(fl, v2, failed_type(b.code));
             }
         } else if (p2) {
             if (has_unpaired_left) {  // the reference checks the LEFT writer here (src/peprocessor.cpp:417)
-                append_read(out.unpaired2, v2);
-                if (has_failed) append_read(out.failed, v1, failed_type(b.code));  // sic: result2 (:420)
+                append_read(u2, v2);
+                if (has_failed) append_read(fl, v1, failed_type(b.code));  // sic: result2 (:420)
             } else if (has_failed) {
-                append_read(out.failed, v1, failed_type(a.code));
-                append_read(out.failed, v2, "paired_read_is_failing");
+                append_read(fl, v1, failed_type(a.code));
+                append_read(fl, v2, "paired_read_is_failing");
             }
         }
     }
 }
 
+}  // namespace
+
+std::string merged_name(const std::string& name, int len1, int len2) {
+    const std::string tag = "_merged_" + std::to_string(len1) + "_" + std::to_string(len2);
+    const size_t pos = name.find_first_of(' ');
+    if (pos == std::string::npos) return tag;
+    return name.substr(0, pos - 1) + tag + name.substr(pos);
+}
+
+void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out, Pool* pool) {
+    const int parts = pool ? std::max(1, std::min(pool->size() * 2, (pk.n + 8191) / 8192)) : 1;
+    for (auto* v : {&out.out1, &out.out2, &out.unpaired1, &out.unpaired2, &out.failed, &out.merged}) {
+        v->clear();
+        v->resize((size_t)parts);
+    }
+    auto work = [&](int k) {
+        const int i0 = (int)((int64_t)pk.n * k / parts), i1 = (int)((int64_t)pk.n * (k + 1) / parts);
+        out.out1[(size_t)k].reserve(span_bytes(pk, 0, i0, i1));
+        if (pk.paired) {
+            if (o.merge) out.merged[(size_t)k].reserve(span_bytes(pk, 0, i0, i1) + span_bytes(pk, 1, i0, i1));
+            else out.out2[(size_t)k].reserve(span_bytes(pk, 1, i0, i1));
+        }
+        format_range(o, pk, res, i0, i1, (size_t)k, out);
+    };
+    if (pool) pool->run(parts, work);
+    else work(0);
+}
+
 namespace {
 
 template <class T>
-class Queue {  // bounded FIFO between pipeline threads
+class Queue {  // bounded FIFO between pipeline threads; push/pop return at once after close()
    public:
     explicit Queue(size_t cap) : cap_(cap) {}
     void push(T v) {
         std::unique_lock<std::mutex> l(m_);
-        not_full_.wait(l, [&] { return q_.size() < cap_; });
+        not_full_.wait(l, [&] { return q_.size() < cap_ || closed_; });
+        if (closed_) return;
         q_.push_back(std::move(v));
         not_empty_.notify_one();
     }
@@ -178,6 +217,7 @@ class Queue {  // bounded FIFO between pipeline threads
         std::lock_guard<std::mutex> l(m_);
         closed_ = true;
         not_empty_.notify_all();
+        not_full_.notify_all();
     }
 
    private:
@@ -190,38 +230,43 @@ class Queue {  // bounded FIFO between pipeline threads
 
 }  // namespace
 
-// WriterThread (src/writerthread.cpp): one thread per output file, strings written in order
+// WriterThread (src/writerthread.cpp): one thread per output file, blocks written in order
 class AsyncWriter {
    public:
-    AsyncWriter(const std::string& path, int level) : w_(path, level), q_(16), t_([this] { loop(); }) {}
+    AsyncWriter(const std::string& path, int level, Pool* pool)
+        : w_(path, level), pool_(pool), q_(4), t_([this] { loop(); }) {}
     ~AsyncWriter() {
         q_.close();
         t_.join();
     }
-    void write(std::string s) {
-        if (!s.empty()) q_.push(std::move(s));
+    void write(std::vector<std::string> blocks) {
+        bool any = false;
+        for (const auto& s : blocks) any = any || !s.empty();
+        if (any) q_.push(std::move(blocks));
     }
 
    private:
     void loop() {
-        std::string s;
-        while (q_.pop(s)) w_.write(s);
+        std::vector<std::string> b;
+        while (q_.pop(b)) w_.write(b, pool_);
     }
     Writer w_;
-    Queue<std::string> q_;
+    Pool* pool_;
+    Queue<std::vector<std::string>> q_;
     std::thread t_;
 };
 
-OutputSet::OutputSet(const Options& o) : paired_(o.paired()) {
+OutputSet::OutputSet(const Options& o, Pool* pool) : paired_(o.paired()) {
+    const int z = o.compression;
     if (paired_) {
-        if (!o.unpaired1.empty()) wu1_.reset(new AsyncWriter(o.unpaired1, o.compression));
-        if (!o.unpaired2.empty() && o.unpaired2 != o.unpaired1) wu2_.reset(new AsyncWriter(o.unpaired2, o.compression));
-        if (o.merge && !o.merge_out.empty()) wm_.reset(new AsyncWriter(o.merge_out, o.compression));
+        if (!o.unpaired1.empty()) wu1_.reset(new AsyncWriter(o.unpaired1, z, pool));
+        if (!o.unpaired2.empty() && o.unpaired2 != o.unpaired1) wu2_.reset(new AsyncWriter(o.unpaired2, z, pool));
+        if (o.merge && !o.merge_out.empty()) wm_.reset(new AsyncWriter(o.merge_out, z, pool));
     }
-    if (!o.failed_out.empty()) wf_.reset(new AsyncWriter(o.failed_out, o.compression));
+    if (!o.failed_out.empty()) wf_.reset(new AsyncWriter(o.failed_out, z, pool));
     if (!o.out1.empty()) {
-        w1_.reset(new AsyncWriter(o.out1, o.compression));
-        if (paired_ && !o.out2.empty()) w2_.reset(new AsyncWriter(o.out2, o.compression));
+        w1_.reset(new AsyncWriter(o.out1, z, pool));
+        if (paired_ && !o.out2.empty()) w2_.reset(new AsyncWriter(o.out2, z, pool));
     }
 }
 
@@ -290,6 +335,10 @@ void log(const std::string& s) {
     std::cerr << d << s << std::endl;
 }
 
+double since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+}
+
 }  // namespace
 
 Options prepare_options(int argc, char** argv) {
@@ -304,9 +353,30 @@ Options prepare_options(int argc, char** argv) {
     if (!o.in1.empty()) o.est_seq_len1 = evaluate_read_len(o.in1);
     if (!o.in2.empty()) o.est_seq_len2 = evaluate_read_len(o.in2);
     if (o.detect_pe_adapter) {
-        // an interleaved input has no read2 file: opening "" fails as in the reference
-        o.detected_adapter1 = detect_adapter(o.in1, o.tail1);
-        o.detected_adapter2 = detect_adapter(o.in2, o.tail1);
+        // the two mates' detections run concurrently; their read errors are printed in the
+        // reference's order (read 1's first; read 2's only when read 1's detection succeeded).
+        // An interleaved input has no read2 file: opening "" fails as in the reference.
+        std::string a1, a2, msg1, msg2;
+        std::exception_ptr e1, e2;
+        std::thread t([&] {
+            try {
+                a2 = detect_adapter(o.in2, o.tail1, &msg2);
+            } catch (...) {
+                e2 = std::current_exception();
+            }
+        });
+        try {
+            a1 = detect_adapter(o.in1, o.tail1, &msg1);
+        } catch (...) {
+            e1 = std::current_exception();
+        }
+        t.join();
+        std::cerr << msg1;
+        if (e1) std::rethrow_exception(e1);
+        std::cerr << msg2;
+        if (e2) std::rethrow_exception(e2);
+        o.detected_adapter1 = a1;
+        o.detected_adapter2 = a2;
     }
     return o;
 }
@@ -324,24 +394,26 @@ int run_tool(int argc, char** argv) {
         std::cerr << "ERROR: " << e.what() << std::endl;
         return 255;
     }
+    const double prepass_s = since(t0);
     try {
         const bool paired = o.paired();
         const size_t pack_n = std::max<size_t>(o.max_reads_in_pack, 262144);
         int est = std::max(o.est_seq_len1, paired ? o.est_seq_len2 : 0);
         Engine eng;
         make_engine(eng, o, std::max(16, round16(o.merge ? 2 * est : est)), (int)pack_n, round16(std::max(est, 16)));
-        OutputSet outs(o);
-        // reader thread -> engine + formatting (this thread) -> writer threads
-        Queue<std::unique_ptr<Pack>> packs(2);
+        // -w host threads (the reference's worker count) pack tiles, format and compress
+        Pool pool(std::max(0, o.threads - 1));
+        OutputSet outs(o, &pool);
+        // reader thread -> engine + formatting (this thread) -> writer threads; four packs are
+        // recycled so their arenas and planes keep their capacity
+        Queue<std::unique_ptr<Pack>> packs(2), spare(4);
+        for (int i = 0; i < 4; ++i) spare.push(std::unique_ptr<Pack>(new Pack()));
         std::exception_ptr reader_err;
         std::thread reader([&] {
             try {
                 PackReader pr(o.in1, o.in2, o.interleaved, o.phred64);
-                for (;;) {
-                    std::unique_ptr<Pack> pk(new Pack());
-                    if (!pr.next(*pk, pack_n)) break;
-                    packs.push(std::move(pk));
-                }
+                std::unique_ptr<Pack> pk;
+                while (spare.pop(pk) && pr.next(*pk, pack_n, &pool)) packs.push(std::move(pk));
             } catch (...) {
                 reader_err = std::current_exception();
             }
@@ -350,32 +422,42 @@ int run_tool(int argc, char** argv) {
         HostAcc acc(o.insert_size_max);
         AdapterCounts ac;
         std::vector<fq_read_result> res;
-        std::unique_ptr<Pack> pk;
         uint64_t reads = 0;
-        double engine_s = 0;
-        while (packs.pop(pk)) {
-            int max1 = 0, max2 = 0;
-            for (uint16_t l : pk->len[0]) max1 = std::max(max1, (int)l);
-            if (paired)
-                for (uint16_t l : pk->len[1]) max2 = std::max(max2, (int)l);
-            const int need = o.merge ? max1 + max2 : std::max(max1, max2);
-            if (need > eng.max_cycles || pk->stride > eng.max_stride || pk->n > eng.max_batch) {
-                drain(eng, acc);  // keep what the old engine accumulated, then grow it
-                make_engine(eng, o, std::max(eng.max_cycles, round16(need)), std::max(eng.max_batch, pk->n),
-                            std::max(eng.max_stride, pk->stride));
+        double engine_s = 0, format_s = 0;
+        try {
+            std::unique_ptr<Pack> pk;
+            while (packs.pop(pk)) {
+                int max1 = 0, max2 = 0;
+                for (uint16_t l : pk->len[0]) max1 = std::max(max1, (int)l);
+                if (paired)
+                    for (uint16_t l : pk->len[1]) max2 = std::max(max2, (int)l);
+                const int need = o.merge ? max1 + max2 : std::max(max1, max2);
+                if (need > eng.max_cycles || pk->stride > eng.max_stride || pk->n > eng.max_batch) {
+                    drain(eng, acc);  // keep what the old engine accumulated, then grow it
+                    make_engine(eng, o, std::max(eng.max_cycles, round16(need)), std::max(eng.max_batch, pk->n),
+                                std::max(eng.max_stride, pk->stride));
+                }
+                res.resize((size_t)pk->n * (paired ? 2 : 1));
+                const fq_batch b = pk->batch();
+                const auto e0 = std::chrono::steady_clock::now();
+                if (fq_engine_process(eng.e, &b, res.data()) != FQ_OK)
+                    throw std::runtime_error(std::string("fq_engine_process: ") + fq_engine_last_error(eng.e));
+                engine_s += since(e0);
+                const auto f0 = std::chrono::steady_clock::now();
+                const fq_params p = o.to_params(eng.max_cycles);
+                if (o.adapter_trimming) ac.add(*pk, res.data(), p);
+                PackOutput out;
+                format_pack(o, *pk, res.data(), out, &pool);
+                format_s += since(f0);
+                outs.write(std::move(out));
+                reads += (uint64_t)pk->n * (paired ? 2 : 1);
+                spare.push(std::move(pk));
             }
-            res.resize((size_t)pk->n * (paired ? 2 : 1));
-            const fq_batch b = pk->batch();
-            const auto e0 = std::chrono::steady_clock::now();
-            if (fq_engine_process(eng.e, &b, res.data()) != FQ_OK)
-                throw std::runtime_error(std::string("fq_engine_process: ") + fq_engine_last_error(eng.e));
-            engine_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - e0).count();
-            const fq_params p = o.to_params(eng.max_cycles);
-            if (o.adapter_trimming) ac.add(*pk, res.data(), p);
-            PackOutput out;
-            format_pack(o, *pk, res.data(), out);
-            outs.write(std::move(out));
-            reads += (uint64_t)pk->n * (paired ? 2 : 1);
+        } catch (...) {
+            packs.close();
+            spare.close();
+            reader.join();
+            throw;
         }
         reader.join();
         if (reader_err) std::rethrow_exception(reader_err);
@@ -384,9 +466,9 @@ int run_tool(int argc, char** argv) {
         const Json rep = build_report(o, acc, ac);
         std::ofstream js(o.json_file, std::ios::binary);
         js << rep.dump(4);
-        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        log("fqtool-amd: " + std::to_string(reads) + " reads, wall " + std::to_string(wall) + " s, engine " +
-            std::to_string(engine_s) + " s; JSON report " + o.json_file + " (no HTML report in this build)");
+        log("fqtool-amd: " + std::to_string(reads) + " reads, wall " + std::to_string(since(t0)) + " s, engine " +
+            std::to_string(engine_s) + " s; pre-pass " + std::to_string(prepass_s) + " s, format " +
+            std::to_string(format_s) + " s; JSON report " + o.json_file + " (no HTML report in this build)");
     } catch (const std::exception& e) {
         std::cerr << "ERROR: " << e.what() << std::endl;
         return 255;

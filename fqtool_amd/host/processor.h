@@ -17,9 +17,10 @@
 
 namespace fqhost {
 
-// Output text of one pack, per destination (src/peprocessor.cpp:262-269)
+// Output text of one pack, per destination (src/peprocessor.cpp:262-269), as consecutive blocks
+// (one per formatting range; a gzip output writes each block as one member)
 struct PackOutput {
-    std::string out1, out2, unpaired1, unpaired2, failed, merged;
+    std::vector<std::string> out1, out2, unpaired1, unpaired2, failed, merged;
 };
 
 class AsyncWriter;
@@ -29,7 +30,7 @@ class AsyncWriter;
 // src/peprocessor.cpp:39-61, :457-492; src/seprocessor.cpp).  Each file has its own writer thread.
 class OutputSet {
    public:
-    explicit OutputSet(const Options& o);
+    explicit OutputSet(const Options& o, Pool* pool = nullptr);  // pool: gzip compression
     ~OutputSet();
     void write(PackOutput&& out);
     void close();  // flushes and closes every file
@@ -41,7 +42,8 @@ class OutputSet {
 
 // Builds the output text of one processed pack from the engine's per-read records, exactly as
 // the loop body of processPairEnd / processSingleEnd appends to its strings.
-void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out);
+// With a pool, ranges of the pack are formatted in parallel into consecutive blocks.
+void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out, Pool* pool = nullptr);
 
 // OverlapAnalysis::merge name rule (src/overlapanalysis.cpp:93-101)
 std::string merged_name(const std::string& name, int len1, int len2);

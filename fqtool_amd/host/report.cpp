@@ -37,7 +37,7 @@ void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_para
                 const uint8_t* ad = m ? p.adapter2 : p.adapter1;
                 s.assign(reinterpret_cast<const char*>(ad) + r.ad_pos, r.ad_len);
             } else {
-                s.assign(pk.seq_text[m][(size_t)i], r.ad_pos, r.ad_len);
+                s.assign(pk.seq_text(m, (size_t)i) + r.ad_pos, r.ad_len);
             }
             ++(m ? r2 : r1)[s];
         }

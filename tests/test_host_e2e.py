@@ -29,6 +29,17 @@ def test_host_pipeline_with_oracle_engine(case, host, oracle, tmp_path):
     E.check_outputs(case, str(tmp_path), report)
 
 
+@pytest.mark.parametrize("case", E.ok_cases())
+def test_host_pipeline_threaded(case, host, oracle, tmp_path):
+    """Same with -w 4 and small packs: tile packing, output formatting (blocks) and gzip members
+    run on the host pool; outputs and JSON must not change."""
+    argv = E.argv_for("fqtool", case, str(tmp_path))
+    assert argv[1:3] == ["-w", "1"]
+    argv[2] = "4"
+    report = E.run_session_with_oracle(host, oracle, argv, max_n=700)
+    E.check_outputs(case, str(tmp_path), report)
+
+
 @pytest.mark.parametrize("case", E.err_cases())
 def test_cli_errors_match_reference(case, tmp_path):
     if not os.path.exists(abi.FQTOOL_BIN):

@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""End-to-end (FASTQ file -> FASTQ files + JSON) timing of the fqtool-amd binary on the GPU box.
+
+Not the headline metric (bench.py is: device-resident batches).  This measures the whole tool:
+reader/parse, pinned H2D, engine, D2H, formatting and writers, on plain FASTQ in the page
+cache, next to the reference binary (oracle/_ref/fqtool_ref) on the same files and options,
+and checks that both produce byte-identical FASTQ and JSON (Software block masked).
+
+    python tools/e2e_bench.py [--pairs 2000000] [--workers 16] [--no-ref]
+Prints one JSON line per run plus a parity verdict.
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402  (write_fastq_pair, SEED, READ_LEN, STRIDE)
+
+OPTS = {
+    "C3": ["-q", "-a", "--detect_pe_adapter", "-g"],
+    "C5": ["-q", "-a", "-g", "-x", "--enable_cut_right"],
+    "C4": ["-q", "-a", "-g", "--enable_cut_right", "-m"],
+}
+
+
+def gen_fastq(pairs, d):
+    import torch
+
+    from fqtool_amd import abi
+
+    lib = abi.load_engine()
+    dev = torch.device("cuda:0")
+    bufs = [torch.empty(abi.batch_bytes(pairs, bench.STRIDE), dtype=torch.uint8, device=dev) for _ in range(4)]
+    lens = [torch.empty(pairs, dtype=torch.int16, device=dev) for _ in range(2)]
+    b = abi.FqBatch()
+    b.n, b.stride = pairs, bench.STRIDE
+    b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
+    b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
+    first = 10 ** 12
+    assert lib.fq_synth_fill_device(ctypes.byref(b), bench.SEED, first, bench.READ_LEN, None) == 0
+    torch.cuda.synchronize()
+    arr = [abi.untile_rows(t.cpu().numpy(), pairs, bench.STRIDE)[:, :bench.READ_LEN] for t in bufs]
+    del bufs
+    torch.cuda.empty_cache()
+    return bench.write_fastq_pair(arr[0], arr[1], arr[2], arr[3], first, d)
+
+
+def digest(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 22), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def same_records(a, b):
+    """Order-insensitive FASTQ comparison (the reference writes packs in completion order at -w > 1)."""
+    def sorted_digest(p):
+        cmd = f"paste - - - - < '{p}' | LC_ALL=C sort -S 2G | sha256sum"
+        return subprocess.run(["bash", "-c", cmd], stdout=subprocess.PIPE, check=True, text=True).stdout.split()[0]
+    return sorted_digest(a) == sorted_digest(b)
+
+
+def masked_json(path):
+    j = json.load(open(path))
+    j.pop("Software", None)
+    return j
+
+
+def run(tool, r1, r2, d, tag, cfg, workers):
+    o = {k: os.path.join(d, f"{tag}_{k}") for k in ("o1.fq", "o2.fq", "m.fq", "r.json", "r.html")}
+    cmd = [tool, "-i", r1, "-I", r2, "-o", o["o1.fq"], "-O", o["o2.fq"], *OPTS[cfg], "-w", str(workers),
+           "-J", o["r.json"], "-H", o["r.html"]]
+    if cfg == "C4":
+        cmd += ["--merge_output", o["m.fq"]]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    wall = time.perf_counter() - t0
+    if p.returncode != 0:
+        raise SystemExit(f"{tag} failed rc={p.returncode}: {p.stderr[-2000:]}")
+    m = re.search(r"wall ([0-9.]+) s, engine ([0-9.]+) s(.*)", p.stderr)
+    return wall, (m.groups() if m else None), o
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=2_000_000)
+    ap.add_argument("--workers", type=int, default=16)
+    ap.add_argument("--config", default="C3", choices=sorted(OPTS))
+    ap.add_argument("--no-ref", action="store_true")
+    args = ap.parse_args()
+    tmp = tempfile.mkdtemp(prefix="fqe2e_")
+    try:
+        t0 = time.perf_counter()
+        r1, r2 = gen_fastq(args.pairs, tmp)
+        gb = (os.path.getsize(r1) + os.path.getsize(r2)) / 1e9
+        print(f"[e2e] wrote {args.pairs} pairs ({gb:.2f} GB FASTQ) in {time.perf_counter() - t0:.1f}s", flush=True)
+        reads = 2 * args.pairs
+        ours = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
+        wall, inner, o_ours = run(ours, r1, r2, tmp, "amd", args.config, args.workers)
+        line = {"tool": "fqtool-amd", "config": args.config, "pairs": args.pairs, "fastq_GB": round(gb, 3),
+                "wall_s": round(wall, 3), "Mreads_s": round(reads / wall / 1e6, 3),
+                "fastq_GB_s": round(gb / wall, 3), "workers": args.workers, "tool_log": inner}
+        print(json.dumps(line), flush=True)
+        ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
+        if not args.no_ref and os.path.exists(ref):
+            w = min(16, args.workers)
+            wall_r, _, o_ref = run(ref, r1, r2, tmp, "ref", args.config, w)
+            print(json.dumps({"tool": "reference", "config": args.config, "pairs": args.pairs, "wall_s": round(wall_r, 3),
+                              "Mreads_s": round(reads / wall_r / 1e6, 3), "workers": w}), flush=True)
+            same = {}
+            for k in ("o1.fq", "o2.fq", "m.fq"):
+                if os.path.exists(o_ref[k]) or os.path.exists(o_ours[k]):
+                    if not (os.path.exists(o_ours[k]) and os.path.exists(o_ref[k])):
+                        same[k] = False
+                    elif digest(o_ours[k]) == digest(o_ref[k]):
+                        same[k] = "identical"
+                    else:
+                        same[k] = "same records, pack order differs" if same_records(o_ours[k], o_ref[k]) else False
+            jr, jo = masked_json(o_ref["r.json"]), masked_json(o_ours["r.json"])
+            # the reference counts InsertSize on worker thread 0 only; compare it at -w 1 only
+            if w > 1:
+                jr.pop("InsertSize", None)
+                jo.pop("InsertSize", None)
+            same["json"] = jr == jo
+            print(json.dumps({"parity": same, "speedup_vs_reference": round(wall_r / wall, 2)}), flush=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
