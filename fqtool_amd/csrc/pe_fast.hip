@@ -627,7 +627,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     const uint32_t kk = (sw[j] >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
                     const uint32_t canon = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, kk);
-                    exo |= FULL ? (canon ^ sw[j]) : ((canon ^ sw[j]) & bm);
+                    // sum of |canon - byte| (one v_sad_u8): zero iff every byte is canonical, and
+                    // at most 40 dwords x 4 x 255 per tile, so it never wraps
+                    exo = FULL ? __builtin_amdgcn_sad_u8(canon, sw[j], exo)
+                               : __builtin_amdgcn_sad_u8(canon & bm, sw[j] & bm, exo);
                     const uint32_t qm = FULL ? qw[j] : (qw[j] & bm);
                     qhi |= qm;
                     q20 += __popc((qm + 0x4A4A4A4Au) & (0x80808080u & bm));  // q > '5'
