@@ -9,9 +9,12 @@ i.e. every pair's trim/filter result record and the Stats x4 / FilterResult / in
 accumulators; with N ranks the accumulator block is then summed over RCCL (the only exchange
 the path has).  Scaling is weak: each rank owns `--pairs` pairs (its own index range).
 
-Launch:  python bench.py [--gpus N --steps K --warmup W]
+Launch:  python bench.py [--gpus N --steps K --warmup W] [--config C2|C3|C4|C5]
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
-Rank 0 prints ONE JSON line.
+Without a launcher, --gpus N > 1 spawns the N rank processes itself (before any GPU call); under
+a launcher WORLD_SIZE must equal N or the run stops.  Rank 0 prints ONE JSON line.  After the
+timed region each rank checks a stratified sample of its shard against the CPU restatement
+(`parity_sample`: the oracle as checker, never timed) and the run fails if any rank differs.
 """
 import argparse
 import ctypes
@@ -152,109 +155,204 @@ def cpu_baseline(lib, abi, torch, pairs):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=100_000_000, help="pairs per GPU (BASELINE: 100 M)")
-    ap.add_argument("--cpu-pairs", type=int, default=1_000_000, help="CPU-baseline sample size (pairs)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS),
-                    help="workload (BASELINE.json configs); the headline metric is C3")
-    args = ap.parse_args()
+class HipRunner:
+    """One rank of the product path: libfqengine.so (HIP kernels for gfx950) on one GPU, its
+    shard of the synthetic workload resident in HBM (generated in place)."""
 
-    import torch
+    backend = "nccl"
+
+    def __init__(self, args, local):
+        import torch
+
+        from fqtool_amd import abi
+
+        self.torch, self.abi, self.args = torch, abi, args
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.local = local
+        self.lib = abi.load_engine()
+        self.p = config_params(abi, args.config)
+        self.paired = bool(self.p.paired)
+        h = ctypes.c_void_p()
+        if self.lib.fq_engine_create(ctypes.byref(self.p), local, 0, 0, ctypes.byref(h)) != 0:
+            raise SystemExit("fq_engine_create: " + self.lib.fq_engine_last_error(None).decode())
+        self.h = h
+        self.events = []
+
+    def alloc(self, first, n):
+        torch, abi = self.torch, self.abi
+        self.first, self.n = first, n
+        np_ = 4 if self.paired else 2
+        log(f"cuda:{self.local}: allocating {np_ * abi.batch_bytes(n, STRIDE) / 1e9:.1f} GB of reads for {n} "
+            f"{'pairs' if self.paired else 'reads'}")
+        self.planes = [torch.empty(abi.batch_bytes(n, STRIDE), dtype=torch.uint8, device=self.dev) for _ in range(np_)]
+        self.lens = [torch.empty(n, dtype=torch.int16, device=self.dev) for _ in range(np_ // 2)]
+        self.results = torch.empty(n * (2 if self.paired else 1) * 16, dtype=torch.uint8, device=self.dev)
+        self.acc = torch.zeros(self.lib.fq_engine_acc_words(self.h), dtype=torch.int64, device=self.dev)
+        assert self.lib.fq_engine_set_acc_buffer(self.h, self.acc.data_ptr()) == 0
+        b = abi.FqBatch()
+        b.n, b.stride = n, STRIDE
+        b.seq1, b.qual1, b.len1 = self.planes[0].data_ptr(), self.planes[1].data_ptr(), self.lens[0].data_ptr()
+        if self.paired:
+            b.seq2, b.qual2, b.len2 = self.planes[2].data_ptr(), self.planes[3].data_ptr(), self.lens[1].data_ptr()
+        self.batch = b
+        self.stream = torch.cuda.current_stream(self.dev)
+        t0 = time.time()
+        assert self.lib.fq_synth_fill_device(ctypes.byref(b), SEED, first, READ_LEN,
+                                             ctypes.c_void_p(self.stream.cuda_stream)) == 0
+        torch.cuda.synchronize(self.dev)
+        log(f"cuda:{self.local}: synthetic shard generated in {time.time() - t0:.2f}s")
+
+    def step(self, timed):
+        """One pass of the hot path over the whole resident shard: every record + accumulators.
+        HIP events on the launch stream bracket the engine launch (kernel time for roofline)."""
+        self.acc.zero_()
+        ev = None
+        if timed:
+            ev = (self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True))
+            ev[0].record(self.stream)
+        rc = self.lib.fq_engine_process_device(self.h, ctypes.byref(self.batch), self.results.data_ptr(),
+                                               ctypes.c_void_p(self.stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(self.lib.fq_engine_last_error(self.h).decode())
+        if ev:
+            ev[1].record(self.stream)
+            self.events.append(ev)
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def elapsed_tensor(self, x):
+        return self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+
+    def kernel_ms(self):
+        ms = [a.elapsed_time(b) for a, b in self.events]
+        return sum(ms) / len(ms) if ms else None
+
+    def finish(self):
+        if self.lib.fq_engine_sync(self.h) != 0:
+            raise RuntimeError(self.lib.fq_engine_last_error(self.h).decode())
+
+    def acc_host(self):
+        return self.acc.cpu().numpy().view("uint64")
+
+    def parity_sample(self, target):
+        """CHECKER leg (after the timed region): a stratified tile sample of this rank's shard,
+        the full run's records and a re-run's accumulator vs the CPU restatement (oracle/)."""
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from oracle_lib import load_oracle
+        from sample_parity import check_sample
+
+        return check_sample(self.lib, load_oracle(), self.torch, self.p, self.planes, self.lens, self.results,
+                            self.n, STRIDE, target, device_index=self.local, seed=self.first + 1)
+
+    def cpu_baseline(self, pairs):
+        del self.planes, self.lens, self.results
+        self.torch.cuda.empty_cache()
+        return cpu_baseline(self.lib, self.abi, self.torch, pairs)
+
+    def close(self):
+        self.lib.fq_engine_destroy(self.h)
+
+
+def make_runner(spec, args, local):
+    if spec == "hip":
+        return HipRunner(args, local)
+    # CPU rehearsal of the rank orchestration (tests/test_bench_cpu.py): "module:Class" on sys.path
+    import importlib
+
+    mod, cls = spec.split(":")
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    return getattr(importlib.import_module(mod), cls)(args, local)
+
+
+def free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_rank(args):
+    """One rank: shard, warm up, time exactly `steps` passes between barriers + device syncs,
+    max over ranks, RCCL sum of the accumulator block, parity sample, rank 0 prints the line."""
+    import hashlib
+
     import torch.distributed as dist
 
-    from fqtool_amd import abi
     from fqtool_amd.dist import reduce_accumulator, shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    runner = make_runner(args.runner, args, local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    lib = abi.load_engine()
-    p = config_params(abi, args.config)
-    paired = bool(p.paired)
-    h = ctypes.c_void_p()
-    if lib.fq_engine_create(ctypes.byref(p), local, 0, 0, ctypes.byref(h)) != 0:
-        raise SystemExit("fq_engine_create: " + lib.fq_engine_last_error(None).decode())
-
+        kw = {"device_id": runner.dev} if runner.backend == "nccl" else {}
+        dist.init_process_group(runner.backend, **kw)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     first, n = shard(rank, world, args.pairs)
-    log(f"rank {rank}/{world}: allocating {4 * n * STRIDE / 1e9:.1f} GB of reads for {n} pairs")
-    bufs = [torch.empty(abi.batch_bytes(n, STRIDE), dtype=torch.uint8, device=dev) for _ in range(4)]
-    lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
-    results = torch.empty(n * 2 * 16, dtype=torch.uint8, device=dev)
-    acc = torch.zeros(lib.fq_engine_acc_words(h), dtype=torch.int64, device=dev)
-    assert lib.fq_engine_set_acc_buffer(h, acc.data_ptr()) == 0
-    b = abi.FqBatch()
-    b.n, b.stride = n, STRIDE
-    b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
-    b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
-    stream = torch.cuda.current_stream(dev)
-    sb = abi.FqBatch()  # single-end view (C2): read 1 planes only
-    sb.n, sb.stride, sb.seq1, sb.qual1, sb.len1 = b.n, b.stride, b.seq1, b.qual1, b.len1
-    t0 = time.time()
-    assert lib.fq_synth_fill_device(ctypes.byref(b), SEED, first, READ_LEN, ctypes.c_void_p(stream.cuda_stream)) == 0
-    torch.cuda.synchronize(dev)
-    log(f"synthetic data generated in {time.time() - t0:.2f}s")
+    runner.alloc(first, n)
 
-    def step(ev=None):
-        acc.zero_()
-        if ev:
-            ev[0].record(stream)
-        rc = lib.fq_engine_process_device(h, ctypes.byref(b if paired else sb), results.data_ptr(),
-                                          ctypes.c_void_p(stream.cuda_stream))
-        if rc != 0:
-            raise RuntimeError(lib.fq_engine_last_error(h).decode())
-        if ev:
-            ev[1].record(stream)
-        reduce_accumulator(acc)  # Stats/FilterResult/insert-size sum over RCCL (xGMI) when world > 1
+    def step(timed):
+        runner.step(timed)
+        reduce_accumulator(runner.acc)  # Stats/FilterResult/insert-size sum over RCCL (xGMI) when world > 1
 
     for i in range(args.warmup):
-        step()
-        torch.cuda.synchronize(dev)
-        log(f"warmup {i + 1}/{args.warmup}")
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        step(False)
+        runner.sync()
+        log(f"rank {rank}: warmup {i + 1}/{args.warmup}")
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    runner.sync()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(events[i])
-    torch.cuda.synchronize(dev)
+    for _ in range(args.steps):
+        step(True)
+    runner.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = runner.elapsed_tensor(elapsed)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = [e0.elapsed_time(e1) for e0, e1 in events]
-    kavg = sum(kernel_ms) / len(kernel_ms)
-    if lib.fq_engine_sync(h) != 0:
-        raise RuntimeError(lib.fq_engine_last_error(h).decode())
+    kavg = runner.kernel_ms()
+    runner.finish()
+    log(f"rank {rank}: {args.steps} steps in {elapsed:.3f}s")
 
-    acc_host = acc.cpu().numpy().view("uint64")
+    abi = runner.abi
+    p = runner.p
+    paired = runner.paired
+    acc_host = runner.acc_host()
     total_pairs = n * world
     reads = (2 if paired else 1) * total_pairs
-    # sanity: every pair (read) was counted by the pre-filter stats and by FilterResult
+    # size-independent invariants of the reduced block: every pair (read) counted once by the
+    # pre-filter stats and once by FilterResult
     st0 = abi.acc_stats_offset(p.insert_size_max, p.max_cycles, 0)
     assert int(acc_host[st0 + abi.FQ_ST_READS]) == total_pairs, "accumulator lost pairs"
-    assert int(acc_host[abi.FQ_ACC_FILTER:abi.FQ_ACC_FILTER + 32].sum()) == reads
+    assert int(acc_host[abi.FQ_ACC_FILTER:abi.FQ_ACC_FILTER + 32].sum()) == reads, "FilterResult lost reads"
+    acc_digest = hashlib.sha256(acc_host.tobytes()).hexdigest()
+
+    sample = None
+    if args.sample_pairs > 0:
+        t1 = time.time()
+        sample = runner.parity_sample(args.sample_pairs)
+        if sample is not None:
+            log(f"rank {rank}: parity sample {sample} ({time.time() - t1:.1f}s)")
+            if world > 1:  # every rank checks its own shard; all must agree
+                ok = runner.elapsed_tensor(1.0 if sample["ok"] else 0.0)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                sample["all_ranks_ok"] = bool(ok.item() == 1.0)
+                sample["ranks"] = world
 
     value = reads * args.steps / elapsed / 1e6
     traffic, traffic_src = pmc_traffic(args.config, args.pairs) if world == 1 else (None, None)
     bytes_per_pair = (2 if paired else 1) * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result per read
-    achieved = n * bytes_per_pair / (kavg / 1e3) / 1e9
+    achieved = n * bytes_per_pair / (kavg / 1e3) / 1e9 if kavg else None
     out = {
         "metric": "Mreads/s (150 bp PE, q+adapter+polyG)" if args.config == "C3" else f"Mreads/s ({args.config})",
         "value": round(value, 2),
@@ -268,26 +366,75 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded counter-based generator in HBM, SURVEY.md 8(d))",
-        "config": {"workload": WORKLOADS[args.config], ("pairs_per_gpu" if paired else "reads_per_gpu"): n, "read_len": READ_LEN, "row_stride": STRIDE,
+        "config": {"workload": WORKLOADS[args.config], ("pairs_per_gpu" if paired else "reads_per_gpu"): n,
+                   "read_len": READ_LEN, "row_stride": STRIDE,
                    "parallelism": f"dp{world} (pairs sharded, RCCL sum of the accumulator block)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes per launch (PMC)", "traffic_src": traffic_src,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": traffic, "traffic_unit": "bytes per launch (PMC)", "traffic_src": traffic_src,
                      "algorithmic_bytes": n * bytes_per_pair,
-                     "kernel_ms_avg": round(kavg, 3),
+                     "kernel_ms_avg": round(kavg, 3) if kavg else None,
                      ("bytes_per_pair" if paired else "bytes_per_read"): bytes_per_pair},
         "cpu_baseline": None,
+        "acc_sha256": acc_digest,
+        "parity_sample": sample,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C3":
-        del bufs, lens, results
-        torch.cuda.empty_cache()
         log(f"CPU baseline on {args.cpu_pairs} pairs ...")
-        out["cpu_baseline"] = cpu_baseline(lib, abi, torch, args.cpu_pairs)
-    lib.fq_engine_destroy(h)
+        out["cpu_baseline"] = runner.cpu_baseline(args.cpu_pairs)
+    runner.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if sample is not None and not sample.get("all_ranks_ok", sample["ok"]):
+        raise SystemExit("bench: parity sample FAILED (the engine's records/accumulator differ from the oracle)")
+
+
+def _spawned_rank(i, args, port):
+    os.environ.update(RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run_rank(args)
+
+
+def launch(args):
+    """`--gpus N` without a launcher: start N rank processes here (spawn, before this process
+    touches any GPU), one per GPU. Under torchrun WORLD_SIZE must equal N."""
+    if "WORLD_SIZE" in os.environ or args.gpus == 1:
+        run_rank(args)
+        return
+    if args.runner == "hip":
+        import torch
+
+        ndev = torch.cuda.device_count()  # counts devices without initialising HIP in this process
+        if ndev < args.gpus:
+            raise SystemExit(f"bench: --gpus {args.gpus} but only {ndev} GPUs are visible")
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_spawned_rank, args=(args, free_port()), nprocs=args.gpus, join=True, start_method="spawn")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=None,
+                    help="pairs (SE: reads) per GPU; default 100 M (BASELINE configs 1-3), 125 M for C5 "
+                         "(config 4's 1 B pairs over 8 GPUs)")
+    ap.add_argument("--cpu-pairs", type=int, default=1_000_000, help="CPU-baseline sample size (pairs)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sample-pairs", type=int, default=1_000_000,
+                    help="per-rank parity sample checked against the oracle after the timed region (0: off)")
+    ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS),
+                    help="workload (BASELINE.json configs); the headline metric is C3")
+    ap.add_argument("--runner", default="hip", help=argparse.SUPPRESS)  # tests: CPU rehearsal of the ranks
+    args = ap.parse_args()
+    if args.pairs is None:
+        args.pairs = 125_000_000 if args.config == "C5" else 100_000_000
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    launch(args)
 
 
 if __name__ == "__main__":

@@ -17,7 +17,7 @@ static inline int qv(const uint8_t* q, int i) { return (int)(signed char)q[i]; }
 
 /* The batch planes hold rows in chunk-interleaved tiles (include/fqengine.h); the restatement
  * below works on contiguous reads, gathered here one at a time. */
-static uint8_t g_row[4][65536];
+static _Thread_local uint8_t g_row[4][65536]; /* per thread: the checker runs chunks in parallel */
 static const uint8_t* gather(int k, const uint8_t* plane, int stride, int i, int len) {
     fq_batch_get_row(plane, stride, i, g_row[k], len);
     return g_row[k];
@@ -416,7 +416,7 @@ static int process_pe(const fq_params* p, const fq_batch* b, fq_read_result* res
     uint64_t* pre2 = acc + fq_acc_stats_offset(p->insert_size_max, p->max_cycles, 1);
     uint64_t* post1 = acc + fq_acc_stats_offset(p->insert_size_max, p->max_cycles, 2);
     uint64_t* post2 = acc + fq_acc_stats_offset(p->insert_size_max, p->max_cycles, 3);
-    static uint8_t ms[131072], mq[131072];
+    static _Thread_local uint8_t ms[131072], mq[131072];
     for (int i = 0; i < b->n; ++i) {
         int l1 = b->len1[i], l2 = b->len2[i];
         const uint8_t* s1 = gather(0, b->seq1, b->stride, i, l1);
