@@ -30,6 +30,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+PCIE_PEAK_GBS = 64.0  # PCIe 5.0 x16, one direction (host <-> MI355X)
 READ_LEN = 150
 STRIDE = 160
 SEED = 20261015
@@ -246,6 +247,81 @@ class HipRunner:
         return check_sample(self.lib, load_oracle(), self.torch, self.p, self.planes, self.lens, self.results,
                             self.n, STRIDE, target, device_index=self.local, seed=self.first + 1)
 
+    def engine_leg(self, pack_pairs, packs=4, rounds=4):
+        """The host-pack path (what the fqtool binary drives): page-locked host packs of
+        `pack_pairs` pairs go through fq_engine_submit/poll -- H2D on a copy stream, kernels,
+        D2H of the 16-byte records -- with up to 3 packs in flight, so copies of pack k+1
+        overlap the kernels of pack k.  Rate includes PCIe both ways; parse/format excluded."""
+        import numpy as np
+
+        abi, lib, torch = self.abi, self.lib, self.torch
+        pp = min(pack_pairs, self.n) // abi.TILE_READS * abi.TILE_READS
+        packs = max(1, min(packs, self.n // pp))
+        h = ctypes.c_void_p()
+        if lib.fq_engine_create(ctypes.byref(self.p), self.local, pp, STRIDE, ctypes.byref(h)) != 0:
+            raise RuntimeError(lib.fq_engine_last_error(None).decode())
+        rpp = 2 if self.paired else 1
+        plane_bytes = abi.batch_bytes(pp, STRIDE)
+        host = []
+        try:
+            for k in range(packs):
+                bufs = []
+                for nbytes in [plane_bytes] * len(self.planes) + [pp * 2] * len(self.lens) + [pp * rpp * 16]:
+                    ptr = ctypes.c_void_p()
+                    if lib.fq_host_alloc(nbytes, ctypes.byref(ptr)) != 0:
+                        raise RuntimeError("fq_host_alloc failed")
+                    host.append(ptr)
+                    bufs.append((ptr, nbytes))
+                lo = k * pp  # pack k = pairs [k*pp, (k+1)*pp) of the resident shard (tile aligned)
+                srcs = [pl[lo * STRIDE: lo * STRIDE + plane_bytes] for pl in self.planes] + \
+                       [l[lo: lo + pp] for l in self.lens]
+                for (ptr, nbytes), t in zip(bufs, srcs):
+                    a = t.cpu().numpy()
+                    ctypes.memmove(ptr.value, a.ctypes.data, nbytes)
+                b = abi.FqBatch()
+                b.n, b.stride = pp, STRIDE
+                b.seq1, b.qual1 = bufs[0][0].value, bufs[1][0].value
+                if self.paired:
+                    b.seq2, b.qual2 = bufs[2][0].value, bufs[3][0].value
+                    b.len1, b.len2 = bufs[4][0].value, bufs[5][0].value
+                else:
+                    b.len1 = bufs[2][0].value
+                host.append((b, bufs[-1][0]))
+
+            batches = [x for x in host if isinstance(x, tuple)]
+
+            def run(n_rounds):
+                seq = ctypes.c_uint64()
+                for r in range(n_rounds):
+                    for k, (b, res) in enumerate(batches):
+                        if lib.fq_engine_pending(h) >= min(3, len(batches)):
+                            if lib.fq_engine_poll(h, 1, ctypes.byref(seq)) != 1:
+                                raise RuntimeError(lib.fq_engine_last_error(h).decode())
+                        if lib.fq_engine_submit(h, ctypes.byref(b), res, r * len(batches) + k) != 0:
+                            raise RuntimeError(lib.fq_engine_last_error(h).decode())
+                while lib.fq_engine_pending(h) > 0:
+                    if lib.fq_engine_poll(h, 1, ctypes.byref(seq)) != 1:
+                        raise RuntimeError(lib.fq_engine_last_error(h).decode())
+
+            run(1)
+            t0 = time.perf_counter()
+            run(rounds)
+            dt = time.perf_counter() - t0
+            pairs = pp * len(batches) * rounds
+            h2d = pairs * (len(self.planes) * STRIDE + len(self.lens) * 2)
+            d2h = pairs * rpp * 16
+            return {"value": round(rpp * pairs / dt / 1e6, 2), "unit": "Mreads/s",
+                    "pack_pairs" if self.paired else "pack_reads": pp, "packs": pairs // pp,
+                    "h2d_GBps": round(h2d / dt / 1e9, 2), "d2h_GBps": round(d2h / dt / 1e9, 2),
+                    "pcie_peak_GBps": PCIE_PEAK_GBS,
+                    "path": "page-locked host packs: fq_engine_submit (H2D on a copy stream) -> kernels -> "
+                            "D2H of the records, <= 3 packs in flight; FASTQ parse/format not included"}
+        finally:
+            lib.fq_engine_destroy(h)
+            for x in host:
+                if not isinstance(x, tuple):
+                    lib.fq_host_free(x)
+
     def cpu_baseline(self, pairs):
         del self.planes, self.lens, self.results
         self.torch.cuda.empty_cache()
@@ -349,6 +425,16 @@ def run_rank(args):
                 sample["all_ranks_ok"] = bool(ok.item() == 1.0)
                 sample["ranks"] = world
 
+    engine = None
+    if args.engine_pairs > 0 and hasattr(runner, "engine_leg"):
+        log(f"rank {rank}: engine leg (pinned host packs of {args.engine_pairs}) ...")
+        engine = runner.engine_leg(args.engine_pairs)
+        log(f"rank {rank}: engine leg {engine}")
+        if world > 1:
+            t = runner.elapsed_tensor(engine["value"])
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            engine["value_all_ranks"] = round(float(t.item()), 2)
+
     value = reads * args.steps / elapsed / 1e6
     traffic, traffic_src = pmc_traffic(args.config, args.pairs) if world == 1 else (None, None)
     bytes_per_pair = (2 if paired else 1) * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result per read
@@ -376,6 +462,8 @@ def run_rank(args):
                      "kernel_ms_avg": round(kavg, 3) if kavg else None,
                      ("bytes_per_pair" if paired else "bytes_per_read"): bytes_per_pair},
         "cpu_baseline": None,
+        "engine_mreads_s": engine["value"] if engine else None,
+        "engine": engine,
         "acc_sha256": acc_digest,
         "parity_sample": sample,
     }
@@ -426,6 +514,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sample-pairs", type=int, default=1_000_000,
                     help="per-rank parity sample checked against the oracle after the timed region (0: off)")
+    ap.add_argument("--engine-pairs", type=int, default=1_048_576,
+                    help="pairs per host pack of the PCIe-inclusive engine leg (0: off)")
     ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS),
                     help="workload (BASELINE.json configs); the headline metric is C3")
     ap.add_argument("--runner", default="hip", help=argparse.SUPPRESS)  # tests: CPU rehearsal of the ranks

@@ -203,6 +203,11 @@ def load_engine(path=ENGINE_LIB):
     lib.fq_synth_fill_device.argtypes = [ctypes.POINTER(FqBatch), u64, u64, i32, vp]
     lib.fq_engine_last_kernel_ms.argtypes = [vp]
     lib.fq_engine_last_kernel_ms.restype = ctypes.c_double
+    lib.fq_engine_submit.argtypes = [vp, ctypes.POINTER(FqBatch), vp, u64]
+    lib.fq_engine_poll.argtypes = [vp, ctypes.c_int, ctypes.POINTER(u64)]
+    lib.fq_engine_pending.argtypes = [vp]
+    lib.fq_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
+    lib.fq_host_free.argtypes = [vp]
     return lib
 
 
@@ -210,7 +215,8 @@ ENGINE_SYMBOLS = [
     "fq_engine_create", "fq_engine_destroy", "fq_engine_process", "fq_engine_process_device",
     "fq_engine_acc_words", "fq_engine_acc_device_ptr", "fq_engine_read_acc", "fq_engine_reset_acc",
     "fq_engine_sync", "fq_engine_set_acc_buffer", "fq_engine_last_error", "fq_engine_device_info", "fq_synth_fill_device",
-    "fq_engine_last_kernel_ms",
+    "fq_engine_last_kernel_ms", "fq_engine_submit", "fq_engine_poll", "fq_engine_pending", "fq_host_alloc",
+    "fq_host_free",
 ]
 
 

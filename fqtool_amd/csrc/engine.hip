@@ -6,9 +6,40 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <string>
 
 #include "engine_internal.h"
+
+// Tile list the fast kernel hands to the general kernel (one per concurrently running launch).
+struct Scratch {
+    int* slow_tiles = nullptr;
+    int* slow_count = nullptr;
+    size_t slow_cap = 0;
+};
+
+// One in-flight pack of the asynchronous pipeline (fq_engine_submit / fq_engine_poll): its own
+// device copy of the batch, result records and hand-off list, and the events that order
+//   H2D (stream in) -> kernels (compute stream) -> D2H of the records (stream out).
+struct Slot {
+    uint8_t* d_rows = nullptr;  // 4 planes of fq_batch_bytes(max_batch, max_stride)
+    uint16_t* d_lens = nullptr;  // 2 x max_batch
+    fq_read_result* d_res = nullptr;
+    Scratch scratch;
+    hipEvent_t ev_in = nullptr, ev_kern = nullptr, ev_done = nullptr;
+    int* h_err = nullptr;  // pinned: the device error flag as of this pack's kernels
+    bool busy = false;      // events recorded and not yet waited for
+};
+
+// A submitted pack, in submission order, until fq_engine_poll reports it.
+struct Pending {
+    uint64_t seq_no;
+    int slot;
+    bool done;  // its slot's events completed (the slot may already serve a later pack)
+    int err;
+};
+
+static const int kSlots = 3;  // H2D(k+1) || kernels(k) || D2H(k-1)
 
 struct fq_engine {
     fq_params p;
@@ -21,15 +52,13 @@ struct fq_engine {
     unsigned long long* own_acc = nullptr;  // the engine's own buffer
     size_t acc_words = 0;
     int* err = nullptr;
-    // staging for the host-memory path
-    uint8_t* d_rows = nullptr;  // 4 planes of fq_batch_bytes(max_batch, max_stride)
-    uint16_t* d_lens = nullptr;  // 2 x max_batch
-    fq_read_result* d_res = nullptr;
+    // host-memory path: pipeline slots and their streams
+    Slot slots[kSlots];
+    std::deque<Pending> pending;
+    hipStream_t s_in = nullptr, s_out = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool fast = false;          // pe_fast kernel usable for these params
-    int* slow_tiles = nullptr;  // tile list handed from the fast to the general kernel
-    int* slow_count = nullptr;
-    size_t slow_cap = 0;
+    bool fast = false;  // pe_fast kernel usable for these params
+    Scratch scratch;    // hand-off list of fq_engine_process_device
     bool timed = false;
     std::string last_error;
 };
@@ -66,6 +95,51 @@ static int validate_params(const fq_params* p, std::string& why) {
     return FQ_OK;
 }
 
+static int ensure_scratch(fq_engine* e, Scratch& sc, size_t ntiles, bool sync_device) {
+    if (!sc.slow_count) HIP_TRY(e, hipMalloc(&sc.slow_count, sizeof(int)));
+    if (ntiles <= sc.slow_cap) return FQ_OK;
+    // the old list may still be read by a launch in flight
+    if (sync_device) HIP_TRY(e, hipDeviceSynchronize());
+    if (sc.slow_tiles) HIP_TRY(e, hipFree(sc.slow_tiles));
+    sc.slow_tiles = nullptr;
+    sc.slow_cap = 0;
+    HIP_TRY(e, hipMalloc(&sc.slow_tiles, ntiles * sizeof(int)));
+    sc.slow_cap = ntiles;
+    return FQ_OK;
+}
+
+static void free_scratch(Scratch& sc) {
+    if (sc.slow_tiles) (void)hipFree(sc.slow_tiles);
+    if (sc.slow_count) (void)hipFree(sc.slow_count);
+    sc = Scratch();
+}
+
+static void free_slot(Slot& s) {
+    if (s.d_rows) (void)hipFree(s.d_rows);
+    if (s.d_lens) (void)hipFree(s.d_lens);
+    if (s.d_res) (void)hipFree(s.d_res);
+    if (s.h_err) (void)hipHostFree(s.h_err);
+    if (s.ev_in) (void)hipEventDestroy(s.ev_in);
+    if (s.ev_kern) (void)hipEventDestroy(s.ev_kern);
+    if (s.ev_done) (void)hipEventDestroy(s.ev_done);
+    free_scratch(s.scratch);
+    s = Slot();
+}
+
+static int alloc_slot(fq_engine* e, Slot& s) {
+    if (s.d_rows) return FQ_OK;
+    const size_t rows = (size_t)4 * fq_batch_bytes(e->max_batch, e->max_stride);
+    HIP_TRY(e, hipMalloc(&s.d_rows, rows));
+    HIP_TRY(e, hipMalloc(&s.d_lens, (size_t)2 * e->max_batch * sizeof(uint16_t)));
+    HIP_TRY(e, hipMalloc(&s.d_res, (size_t)2 * e->max_batch * sizeof(fq_read_result)));
+    HIP_TRY(e, hipHostMalloc((void**)&s.h_err, sizeof(int), hipHostMallocDefault));
+    *s.h_err = 0;
+    HIP_TRY(e, hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
+    HIP_TRY(e, hipEventCreateWithFlags(&s.ev_kern, hipEventDisableTiming));
+    HIP_TRY(e, hipEventCreateWithFlags(&s.ev_done, hipEventDisableTiming));
+    return FQ_OK;
+}
+
 extern "C" {
 
 int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int32_t max_stride, fq_engine** out) {
@@ -98,21 +172,16 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     };
     hipError_t he;
     if ((he = hipSetDevice(device)) != hipSuccess) return bail(hip_fail(e, he, "hipSetDevice"));
-    if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess)
-        return bail(hip_fail(e, he, "hipStreamCreate"));
+    for (hipStream_t* s : {&e->stream, &e->s_in, &e->s_out})
+        if ((he = hipStreamCreateWithFlags(s, hipStreamNonBlocking)) != hipSuccess)
+            return bail(hip_fail(e, he, "hipStreamCreate"));
     if ((he = hipMalloc(&e->own_acc, e->acc_words * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc acc"));
     e->acc = e->own_acc;
     if ((he = hipMalloc(&e->err, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc err"));
     if ((he = hipMemset(e->acc, 0, e->acc_words * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
     if ((he = hipMemset(e->err, 0, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
-    if (max_batch > 0 && max_stride > 0) {
-        const size_t rows = (size_t)4 * fq_batch_bytes(max_batch, max_stride);
-        if ((he = hipMalloc(&e->d_rows, rows)) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc rows"));
-        if ((he = hipMalloc(&e->d_lens, (size_t)2 * max_batch * sizeof(uint16_t))) != hipSuccess)
-            return bail(hip_fail(e, he, "hipMalloc lens"));
-        if ((he = hipMalloc(&e->d_res, (size_t)2 * max_batch * sizeof(fq_read_result))) != hipSuccess)
-            return bail(hip_fail(e, he, "hipMalloc results"));
-    }
+    // the first pipeline slot up front, so an engine that cannot hold one pack fails here
+    if (max_batch > 0 && max_stride > 0 && alloc_slot(e, e->slots[0]) != FQ_OK) return bail(FQ_E_HIP);
     if ((he = hipEventCreate(&e->ev0)) != hipSuccess) return bail(hip_fail(e, he, "hipEventCreate"));
     if ((he = hipEventCreate(&e->ev1)) != hipSuccess) return bail(hip_fail(e, he, "hipEventCreate"));
     if (fq_pack_kernel_lds_bytes(e->p) > 160 * 1024)
@@ -122,7 +191,6 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     e->fast = fq_pe_fast_supported(e->p) && !(force_general && force_general[0] == '1');
     if (e->fast) {
         if ((he = fq_pe_fast_prepare()) != hipSuccess) return bail(hip_fail(e, he, "hipFuncSetAttribute fast"));
-        if ((he = hipMalloc(&e->slow_count, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc"));
     }
     *out = e;
     return FQ_OK;
@@ -131,17 +199,15 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
 int fq_engine_destroy(fq_engine* e) {
     if (!e) return FQ_OK;
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    (void)hipDeviceSynchronize();
     if (e->own_acc) (void)hipFree(e->own_acc);
     if (e->err) (void)hipFree(e->err);
-    if (e->d_rows) (void)hipFree(e->d_rows);
-    if (e->d_lens) (void)hipFree(e->d_lens);
-    if (e->d_res) (void)hipFree(e->d_res);
-    if (e->slow_tiles) (void)hipFree(e->slow_tiles);
-    if (e->slow_count) (void)hipFree(e->slow_count);
+    for (Slot& s : e->slots) free_slot(s);
+    free_scratch(e->scratch);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
-    if (e->stream) (void)hipStreamDestroy(e->stream);
+    for (hipStream_t s : {e->stream, e->s_in, e->s_out})
+        if (s) (void)hipStreamDestroy(s);
     delete e;
     return FQ_OK;
 }
@@ -156,30 +222,27 @@ static int grid_for(const fq_engine* e, int n) {
     return need < cap ? (need > 0 ? need : 1) : cap;
 }
 
-static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStream_t s) {
+// Enqueues the kernels of one batch on stream s.  `sc` is the hand-off list of this launch; it
+// must not be shared with a launch that can run concurrently (different stream).
+static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStream_t s, Scratch& sc, bool timed,
+                  bool sync_device_on_grow) {
     if (db.n <= 0) return FQ_OK;
     if (e->fast) {
         const size_t ntiles = ((size_t)db.n + 31) / 32 + 1;  // single-end 64-read tiles enter as two
-        if (ntiles > e->slow_cap) {
-            HIP_TRY(e, hipStreamSynchronize(s));
-            if (e->slow_tiles) HIP_TRY(e, hipFree(e->slow_tiles));
-            e->slow_tiles = nullptr;
-            e->slow_cap = 0;
-            HIP_TRY(e, hipMalloc(&e->slow_tiles, ntiles * sizeof(int)));
-            e->slow_cap = ntiles;
-        }
-        HIP_TRY(e, hipMemsetAsync(e->slow_count, 0, sizeof(int), s));
-        HIP_TRY(e, hipEventRecord(e->ev0, s));
-        HIP_TRY(e, fq_launch_pe_fast(e->p, db, dres, e->acc, e->slow_tiles, e->slow_count, e->cus, s));
-        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, e->cus, s, e->slow_tiles, e->slow_count));
+        int rc = ensure_scratch(e, sc, ntiles, sync_device_on_grow);
+        if (rc != FQ_OK) return rc;
+        HIP_TRY(e, hipMemsetAsync(sc.slow_count, 0, sizeof(int), s));
+        if (timed) HIP_TRY(e, hipEventRecord(e->ev0, s));
+        HIP_TRY(e, fq_launch_pe_fast(e->p, db, dres, e->acc, sc.slow_tiles, sc.slow_count, e->cus, s));
+        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, e->cus, s, sc.slow_tiles, sc.slow_count));
+    } else {
+        if (timed) HIP_TRY(e, hipEventRecord(e->ev0, s));
+        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, grid_for(e, db.n), s));
+    }
+    if (timed) {
         HIP_TRY(e, hipEventRecord(e->ev1, s));
         e->timed = true;
-        return FQ_OK;
     }
-    HIP_TRY(e, hipEventRecord(e->ev0, s));
-    HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, grid_for(e, db.n), s));
-    HIP_TRY(e, hipEventRecord(e->ev1, s));
-    e->timed = true;
     return FQ_OK;
 }
 
@@ -193,8 +256,21 @@ static int check_err(fq_engine* e) {
     return FQ_OK;
 }
 
-int fq_engine_process(fq_engine* e, const fq_batch* hb, fq_read_result* results) {
-    if (!e || !hb || !results) return FQ_E_INVALID;
+// Waits for slot k's pack (if any) and records its completion in the pending list.
+static int retire_slot(fq_engine* e, int k) {
+    Slot& s = e->slots[k];
+    if (!s.busy) return FQ_OK;
+    HIP_TRY(e, hipEventSynchronize(s.ev_done));
+    s.busy = false;
+    for (Pending& q : e->pending)
+        if (q.slot == k && !q.done) {
+            q.done = true;
+            q.err = *s.h_err;
+        }
+    return FQ_OK;
+}
+
+static int validate_host_batch(fq_engine* e, const fq_batch* hb) {
     const bool pe = e->p.paired;
     if (hb->n < 0 || hb->n > e->max_batch || hb->stride <= 0 || hb->stride > e->max_stride || (hb->stride & 15))
         return fail(e, FQ_E_INVALID, "batch exceeds the engine's max_batch/max_stride (or stride % 16 != 0)");
@@ -205,33 +281,101 @@ int fq_engine_process(fq_engine* e, const fq_batch* hb, fq_read_result* results)
             (pe && (hb->len2[i] > e->p.max_cycles || hb->len2[i] > hb->stride)))
             return fail(e, FQ_E_TOO_LONG, "read longer than max_cycles / stride");
     }
+    return FQ_OK;
+}
+
+int fq_engine_submit(fq_engine* e, const fq_batch* hb, fq_read_result* results, uint64_t seq_no) {
+    if (!e || !hb || !results) return FQ_E_INVALID;
+    int rc = validate_host_batch(e, hb);
+    if (rc != FQ_OK) return rc;
+    if (hb->n == 0) {  // nothing to move: complete at once, in order
+        e->pending.push_back(Pending{seq_no, -1, true, 0});
+        return FQ_OK;
+    }
     HIP_TRY(e, hipSetDevice(e->device));
+    // the slot after the newest pack's (round robin), once its previous pack has drained
+    int k = 0;
+    for (auto it = e->pending.rbegin(); it != e->pending.rend(); ++it)
+        if (it->slot >= 0) {
+            k = (it->slot + 1) % kSlots;
+            break;
+        }
+    if ((rc = retire_slot(e, k)) != FQ_OK) return rc;
+    Slot& s = e->slots[k];
+    if ((rc = alloc_slot(e, s)) != FQ_OK) return rc;
+    const bool pe = e->p.paired;
     const size_t rowbytes = fq_batch_bytes(hb->n, hb->stride);
     const size_t plane = fq_batch_bytes(e->max_batch, e->max_stride);
     fq_batch db;
     db.n = hb->n;
     db.stride = hb->stride;
-    db.seq1 = e->d_rows;
-    db.qual1 = e->d_rows + plane;
-    db.len1 = e->d_lens;
-    db.seq2 = pe ? e->d_rows + 2 * plane : nullptr;
-    db.qual2 = pe ? e->d_rows + 3 * plane : nullptr;
-    db.len2 = pe ? e->d_lens + e->max_batch : nullptr;
-    hipStream_t s = e->stream;
-    HIP_TRY(e, hipMemcpyAsync((void*)db.seq1, hb->seq1, rowbytes, hipMemcpyHostToDevice, s));
-    HIP_TRY(e, hipMemcpyAsync((void*)db.qual1, hb->qual1, rowbytes, hipMemcpyHostToDevice, s));
-    HIP_TRY(e, hipMemcpyAsync((void*)db.len1, hb->len1, (size_t)hb->n * 2, hipMemcpyHostToDevice, s));
+    db.seq1 = s.d_rows;
+    db.qual1 = s.d_rows + plane;
+    db.len1 = s.d_lens;
+    db.seq2 = pe ? s.d_rows + 2 * plane : nullptr;
+    db.qual2 = pe ? s.d_rows + 3 * plane : nullptr;
+    db.len2 = pe ? s.d_lens + e->max_batch : nullptr;
+    // H2D on the copy-in stream (overlaps the previous pack's kernels when the host batch is pinned)
+    HIP_TRY(e, hipMemcpyAsync((void*)db.seq1, hb->seq1, rowbytes, hipMemcpyHostToDevice, e->s_in));
+    HIP_TRY(e, hipMemcpyAsync((void*)db.qual1, hb->qual1, rowbytes, hipMemcpyHostToDevice, e->s_in));
+    HIP_TRY(e, hipMemcpyAsync((void*)db.len1, hb->len1, (size_t)hb->n * 2, hipMemcpyHostToDevice, e->s_in));
     if (pe) {
-        HIP_TRY(e, hipMemcpyAsync((void*)db.seq2, hb->seq2, rowbytes, hipMemcpyHostToDevice, s));
-        HIP_TRY(e, hipMemcpyAsync((void*)db.qual2, hb->qual2, rowbytes, hipMemcpyHostToDevice, s));
-        HIP_TRY(e, hipMemcpyAsync((void*)db.len2, hb->len2, (size_t)hb->n * 2, hipMemcpyHostToDevice, s));
+        HIP_TRY(e, hipMemcpyAsync((void*)db.seq2, hb->seq2, rowbytes, hipMemcpyHostToDevice, e->s_in));
+        HIP_TRY(e, hipMemcpyAsync((void*)db.qual2, hb->qual2, rowbytes, hipMemcpyHostToDevice, e->s_in));
+        HIP_TRY(e, hipMemcpyAsync((void*)db.len2, hb->len2, (size_t)hb->n * 2, hipMemcpyHostToDevice, e->s_in));
     }
-    int rc = launch(e, db, e->d_res, s);
-    if (rc != FQ_OK) return rc;
+    HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
+    // kernels on the compute stream (one accumulator: the packs' kernels run in order)
+    HIP_TRY(e, hipStreamWaitEvent(e->stream, s.ev_in, 0));
+    if ((rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false)) != FQ_OK) return rc;
+    HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
+    // D2H of the records (and of the error flag) on the copy-out stream
+    HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
     const size_t nres = (size_t)hb->n * (pe ? 2 : 1);
-    HIP_TRY(e, hipMemcpyAsync(results, e->d_res, nres * sizeof(fq_read_result), hipMemcpyDeviceToHost, s));
-    HIP_TRY(e, hipStreamSynchronize(s));
-    return check_err(e);
+    if (nres)
+        HIP_TRY(e, hipMemcpyAsync(results, s.d_res, nres * sizeof(fq_read_result), hipMemcpyDeviceToHost, e->s_out));
+    HIP_TRY(e, hipMemcpyAsync(s.h_err, e->err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
+    HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
+    s.busy = true;
+    e->pending.push_back(Pending{seq_no, k, false, 0});
+    return FQ_OK;
+}
+
+int fq_engine_poll(fq_engine* e, int wait, uint64_t* seq_no) {
+    if (!e) return FQ_E_INVALID;
+    if (e->pending.empty()) return 0;
+    HIP_TRY(e, hipSetDevice(e->device));
+    Pending& q = e->pending.front();
+    if (!q.done) {
+        Slot& s = e->slots[q.slot];
+        if (!wait) {
+            const hipError_t st = hipEventQuery(s.ev_done);
+            if (st == hipErrorNotReady) return 0;
+            if (st != hipSuccess) return hip_fail(e, st, "hipEventQuery");
+        }
+        int rc = retire_slot(e, q.slot);
+        if (rc != FQ_OK) return rc;
+    }
+    const Pending done = q;
+    e->pending.pop_front();
+    if (seq_no) *seq_no = done.seq_no;
+    if (done.err) {
+        HIP_TRY(e, hipMemsetAsync(e->err, 0, sizeof(int), e->stream));
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        return fail(e, FQ_E_TOO_LONG, "a read is longer than max_cycles or the row stride");
+    }
+    return 1;
+}
+
+int fq_engine_pending(const fq_engine* e) { return e ? (int)e->pending.size() : FQ_E_INVALID; }
+
+int fq_engine_process(fq_engine* e, const fq_batch* hb, fq_read_result* results) {
+    if (!e || !hb || !results) return FQ_E_INVALID;
+    if (!e->pending.empty()) return fail(e, FQ_E_INVALID, "fq_engine_process with submitted packs not yet polled");
+    int rc = fq_engine_submit(e, hb, results, 0);
+    if (rc != FQ_OK) return rc;
+    rc = fq_engine_poll(e, 1, nullptr);
+    return rc == 1 ? FQ_OK : rc;
 }
 
 int fq_engine_process_device(fq_engine* e, const fq_batch* db, fq_read_result* dres, void* stream) {
@@ -240,7 +384,8 @@ int fq_engine_process_device(fq_engine* e, const fq_batch* db, fq_read_result* d
         (e->p.paired && (!db->seq2 || !db->qual2 || !db->len2)))
         return fail(e, FQ_E_INVALID, "bad device batch");
     HIP_TRY(e, hipSetDevice(e->device));
-    return launch(e, *db, dres, (hipStream_t)stream);  // NULL is the HIP default stream
+    // NULL is the HIP default stream
+    return launch(e, *db, dres, (hipStream_t)stream, e->scratch, true, true);
 }
 
 size_t fq_engine_acc_words(const fq_engine* e) { return e ? e->acc_words : 0; }
@@ -287,6 +432,24 @@ int fq_engine_device_info(const fq_engine* e, int* device, char* arch, size_t ar
     if (device) *device = e->device;
     if (arch && arch_len) std::snprintf(arch, arch_len, "%s", e->arch);
     return FQ_OK;
+}
+
+int fq_host_alloc(size_t bytes, void** out) {
+    if (!out) return FQ_E_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return FQ_E_NO_DEVICE;
+    // portable: any device's DMA engines may read it (packs are dealt over several GPUs)
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) {
+        *out = nullptr;
+        return FQ_E_NOMEM;
+    }
+    return FQ_OK;
+}
+
+int fq_host_free(void* p) {
+    if (!p) return FQ_OK;
+    return hipHostFree(p) == hipSuccess ? FQ_OK : FQ_E_HIP;
 }
 
 int fq_synth_fill_device(const fq_batch* db, uint64_t seed, uint64_t first_index, int32_t read_len, void* stream) {

@@ -172,7 +172,12 @@ int fqh_session_add_acc(fqh_session* s, const uint64_t* acc, int max_cycles) {
 
 // closes the output files and writes the JSON report (-J); returns the report text
 char* fqh_session_finish(fqh_session* s) {
-    s->outs->close();
+    try {
+        s->outs->close();
+    } catch (const std::exception& e) {
+        s->err = e.what();
+        return nullptr;
+    }
     const std::string t = build_report(s->o, s->acc, s->ac).dump(4);
     {
         std::ofstream js(s->o.json_file, std::ios::binary);

@@ -2,10 +2,12 @@
 #include "fastq.h"
 
 #include <algorithm>
+#include <cerrno>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <exception>
 #include <iostream>
 #include <memory>
 #include <mutex>
@@ -29,12 +31,51 @@ const char* line_end(const char* p, size_t n) {
 }
 }  // namespace
 
+ByteBuf& ByteBuf::operator=(ByteBuf&& o) noexcept {
+    if (this != &o) {
+        release();
+        p_ = o.p_;
+        size_ = o.size_;
+        cap_ = o.cap_;
+        want_pinned_ = o.want_pinned_;
+        is_pinned_ = o.is_pinned_;
+        o.p_ = nullptr;
+        o.size_ = o.cap_ = 0;
+        o.is_pinned_ = false;
+    }
+    return *this;
+}
+
+void ByteBuf::release() {
+    if (!p_) return;
+    if (is_pinned_) fq_host_free(p_);
+    else delete[] p_;
+    p_ = nullptr;
+    cap_ = size_ = 0;
+    is_pinned_ = false;
+}
+
 void ByteBuf::reserve(size_t n) {
     if (n <= cap_) return;
-    std::unique_ptr<char[]> q(new char[n]);
-    if (size_) std::memcpy(q.get(), p_.get(), size_);
-    p_ = std::move(q);
+    char* q = nullptr;
+    bool pinned = false;
+    if (want_pinned_) {
+        void* v = nullptr;
+        if (fq_host_alloc(n, &v) == FQ_OK) {
+            q = static_cast<char*>(v);
+            pinned = true;
+        } else {
+            want_pinned_ = false;  // no device (CPU tests): ordinary memory from now on
+        }
+    }
+    if (!q) q = new char[n];
+    if (size_) std::memcpy(q, p_, size_);
+    const size_t keep = size_;
+    release();
+    p_ = q;
+    size_ = keep;
     cap_ = n;
+    is_pinned_ = pinned;
 }
 
 FqReader::FqReader(const std::string& path, bool phred64) : phred64_(phred64), buf_(kBufSize) {
@@ -166,6 +207,8 @@ struct Pool::Impl {
         int n = 0;
         const std::function<void(int)>* fn = nullptr;
         std::atomic<int> next{0}, done{0};
+        std::mutex em;
+        std::exception_ptr err;  // the first exception of any index, rethrown by run()
     };
     std::mutex m;
     std::condition_variable cv, done_cv;
@@ -177,7 +220,12 @@ struct Pool::Impl {
     static bool work(Job& j) {
         bool last = false;
         for (int i; (i = j.next.fetch_add(1)) < j.n;) {
-            (*j.fn)(i);
+            try {
+                (*j.fn)(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> g(j.em);
+                if (!j.err) j.err = std::current_exception();
+            }
             if (j.done.fetch_add(1) + 1 == j.n) last = true;
         }
         return last;
@@ -235,6 +283,7 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
             impl_->jobs.erase(it);
             break;
         }
+    if (j->err) std::rethrow_exception(j->err);
 }
 
 // ---- Pack ----
@@ -353,9 +402,14 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     } else if (interleaved_) {  // FqReaderPair over one file: mate 1, then mate 2
         Rec a, b;
         while (n < max_n) {
-            if (!r1_.read(pk.text[0], a) || !r1_.read(pk.text[1], b)) {
+            // FqReaderPair::read (src/fqreader.cpp:254-267) reads mate 2 even when mate 1 failed
+            const bool ok_a = r1_.read(pk.text[0], a);
+            const std::string err_a = ok_a ? std::string() : r1_.error();
+            const bool ok_b = r1_.read(pk.text[1], b);
+            if (!ok_a || !ok_b) {
                 done_ = true;
-                if (!r1_.error().empty()) std::cerr << r1_.error();
+                std::cerr << err_a;
+                if (!ok_b) std::cerr << r1_.error();
                 break;
             }
             pk.rec[0].push_back(a);
@@ -364,8 +418,9 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
         }
     } else {
         // One thread per mate.  FqReaderPair::read (src/fqreader.cpp:254-267) reads mate 1, then
-        // mate 2, and stops at the first that fails: the pair count is the shorter run, and only
-        // the mate the sequential reader would have failed on reports its error.
+        // mate 2 (always both), and stops once either failed: the pair count is the shorter run,
+        // and a mate reports its error only if its failure is at that index (both do, read 1
+        // first, when they fail at the same index).
         size_t n2 = 0;
         std::thread t([&] { n2 = read_mate(*r2_, pk, 1, max_n); });
         const size_t n1 = read_mate(r1_, pk, 0, max_n);
@@ -373,8 +428,8 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
         n = std::min(n1, n2);
         if (n < max_n) {
             done_ = true;
-            const std::string& e = n1 <= n2 ? r1_.error() : r2_->error();
-            if (!e.empty()) std::cerr << e;
+            if (n1 <= n2) std::cerr << r1_.error();
+            if (n2 <= n1) std::cerr << r2_->error();
         }
         pk.rec[0].resize(n);
         pk.rec[1].resize(n);
@@ -414,18 +469,37 @@ std::string gzip_member(const std::string& s, int level) {
 }
 }  // namespace
 
+namespace {
+void put(FILE* fp, const std::string& s) {
+    if (!s.empty() && std::fwrite(s.data(), 1, s.size(), fp) != s.size())
+        throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
+}
+}  // namespace
+
 Writer::~Writer() {
-    if (gzip_ && !any_member_) {  // an empty .gz output is still one (empty) gzip member
-        const std::string e = gzip_member(std::string(), level_);
-        std::fwrite(e.data(), 1, e.size(), fp_);
+    try {
+        close();
+    } catch (...) {  // a destructor cannot report; close() explicitly to see write errors
     }
-    if (fp_) std::fclose(fp_);
+}
+
+void Writer::close() {
+    if (!fp_) return;
+    FILE* fp = fp_;
+    fp_ = nullptr;
+    try {
+        if (gzip_ && !any_member_) put(fp, gzip_member(std::string(), level_));  // an empty .gz is one empty member
+    } catch (...) {
+        std::fclose(fp);
+        throw;
+    }
+    if (std::fclose(fp) != 0) throw std::runtime_error(std::string("closing output failed: ") + std::strerror(errno));
 }
 
 void Writer::write(const std::vector<std::string>& blocks, Pool* pool) {
+    if (!fp_) throw std::runtime_error("write to a closed output");
     if (!gzip_) {
-        for (const auto& s : blocks)
-            if (!s.empty()) std::fwrite(s.data(), 1, s.size(), fp_);
+        for (const auto& s : blocks) put(fp_, s);
         return;
     }
     std::vector<std::string> z(blocks.size());
@@ -437,7 +511,7 @@ void Writer::write(const std::vector<std::string>& blocks, Pool* pool) {
         for (int i = 0; i < (int)blocks.size(); ++i) work(i);
     for (const auto& s : z)
         if (!s.empty()) {
-            std::fwrite(s.data(), 1, s.size(), fp_);
+            put(fp_, s);
             any_member_ = true;
         }
 }

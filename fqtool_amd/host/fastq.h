@@ -28,11 +28,19 @@
 namespace fqhost {
 
 // Growable byte buffer that keeps its capacity when cleared (packs are recycled) and does not
-// zero what it allocates.
+// zero what it allocates.  A pinned buffer takes page-locked memory from the engine
+// (fq_host_alloc: the H2D/D2H DMA then overlaps the kernels); without a HIP device it silently
+// uses ordinary memory, which the engine also accepts (synchronous copies).
 class ByteBuf {
    public:
-    char* data() { return p_.get(); }
-    const char* data() const { return p_.get(); }
+    explicit ByteBuf(bool pinned = false) : want_pinned_(pinned) {}
+    ~ByteBuf() { release(); }
+    ByteBuf(const ByteBuf&) = delete;
+    ByteBuf& operator=(const ByteBuf&) = delete;
+    ByteBuf(ByteBuf&& o) noexcept { *this = std::move(o); }
+    ByteBuf& operator=(ByteBuf&& o) noexcept;
+    char* data() { return p_; }
+    const char* data() const { return p_; }
     size_t size() const { return size_; }
     void clear() { size_ = 0; }
     void resize_uninit(size_t n) {
@@ -42,15 +50,37 @@ class ByteBuf {
     void reserve(size_t n);
     char* extend(size_t n) {  // appends n uninitialised bytes, returns their start
         if (size_ + n > cap_) reserve(std::max(size_ + n, cap_ + cap_ / 2 + 4096));
-        char* r = p_.get() + size_;
+        char* r = p_ + size_;
         size_ += n;
         return r;
     }
     void truncate(size_t n) { size_ = n; }
+    bool pinned() const { return is_pinned_; }
 
    private:
-    std::unique_ptr<char[]> p_;
+    void release();
+    char* p_ = nullptr;
     size_t size_ = 0, cap_ = 0;
+    bool want_pinned_ = false, is_pinned_ = false;
+};
+
+// Array of T over a ByteBuf (read lengths, result records): pinned like its buffer.
+template <class T>
+class PodBuf {
+   public:
+    explicit PodBuf(bool pinned = false) : b_(pinned) {}
+    void resize(size_t n) { b_.resize_uninit(n * sizeof(T)); }
+    void clear() { b_.clear(); }
+    size_t size() const { return b_.size() / sizeof(T); }
+    T* data() { return reinterpret_cast<T*>(b_.data()); }
+    const T* data() const { return reinterpret_cast<const T*>(b_.data()); }
+    T& operator[](size_t i) { return data()[i]; }
+    const T& operator[](size_t i) const { return data()[i]; }
+    const T* begin() const { return data(); }
+    const T* end() const { return data() + size(); }
+
+   private:
+    ByteBuf b_;
 };
 
 // One record's fields in a mate's text arena: name at off, then seq (len bytes), strand, qual.
@@ -103,15 +133,22 @@ class Pool {
     int workers_;
 };
 
-// One pack of reads (pairs when paired): record text + the engine's batch planes.
+// One pack of reads (pairs when paired): record text + the engine's batch planes + the engine's
+// per-read records.  A pinned pack keeps planes, lengths and records in page-locked memory.
 struct Pack {
+    explicit Pack(bool pinned = false)
+        : seq{ByteBuf(pinned), ByteBuf(pinned)},
+          qual{ByteBuf(pinned), ByteBuf(pinned)},
+          len{PodBuf<uint16_t>(pinned), PodBuf<uint16_t>(pinned)},
+          res(pinned) {}
     int n = 0;
     int stride = 0;
     bool paired = false;
     ByteBuf text[2];
     std::vector<Rec> rec[2];
     ByteBuf seq[2], qual[2];  // batch planes
-    std::vector<uint16_t> len[2];
+    PodBuf<uint16_t> len[2];
+    PodBuf<fq_read_result> res;  // engine records: n (SE) or 2n (PE)
     uint64_t seq_no = 0;
 
     const char* name(int m, size_t i) const { return text[m].data() + rec[m][i].off; }
@@ -120,6 +157,10 @@ struct Pack {
     const char* qual_text(int m, size_t i) const { return strand(m, i) + rec[m][i].strand_len; }
     void clear();
     fq_batch batch() const;
+    fq_read_result* results() {  // sized for this pack
+        res.resize((size_t)n * (paired ? 2 : 1));
+        return res.data();
+    }
 };
 
 // Fills the pack's lengths, stride and tile planes from its record text (pool-parallel over
@@ -158,6 +199,7 @@ class Writer {
     Writer& operator=(const Writer&) = delete;
     void write(const std::vector<std::string>& blocks, Pool* pool = nullptr);
     void write(const std::string& s) { write(std::vector<std::string>{s}); }
+    void close();  // flushes; throws on a short write or a failed close (full disk)
 
    private:
     FILE* fp_ = nullptr;

@@ -201,6 +201,11 @@ Table make_table(Options& o) {
     range(t.add({"--max_packs_in_mem"}, Kind::SizeT, &o.max_packs_in_mem, "max packs in memory"), 1, 1000000);
     // ---- engine
     t.add({"--device"}, Kind::Int, &o.device, "[fqtool-amd] HIP device of the engine (default 0)");
+    range(t.add({"--pack_pairs"}, Kind::SizeT, &o.pack_pairs,
+                "[fqtool-amd] reads/pairs per engine pack (default max(--max_item_in_pack, 262144))"),
+          1, 16777216);
+    t.add({"--devices"}, Kind::Str, &o.devices,
+          "[fqtool-amd] comma-separated HIP devices the packs are dealt over, e.g. 0,1,2,3 (default: --device)");
     return t;
 }
 
@@ -437,6 +442,21 @@ void Options::validate() const {
     if (polyg && (polyg_min_len < 1 && paired())) throw CliError("polyG one-mismatch period must be >= 1", 2);
     if (polyg && !paired() && polyg_one_per < 1) throw CliError("polyG one-mismatch period must be >= 1", 2);
     if (polyx && polyx_one_per < 1) throw CliError("polyX one-mismatch period must be >= 1", 2);
+}
+
+std::vector<int> Options::device_list() const {
+    if (devices.empty()) return {device};
+    std::vector<int> out;
+    size_t i = 0;
+    while (i <= devices.size()) {
+        const size_t j = std::min(devices.find(',', i), devices.size());
+        long long v = 0;
+        if (!cast_signed(devices.substr(i, j - i), v) || v < 0 || v > 1023)
+            throw std::runtime_error("--devices must be a comma-separated list of device ids, got '" + devices + "'");
+        out.push_back((int)v);
+        i = j + 1;
+    }
+    return out;
 }
 
 fq_params Options::to_params(int max_cycles) const {

@@ -62,8 +62,12 @@ struct Options {
     int low_qual_base_limit = 40;
     int est_seq_len1 = 151, est_seq_len2 = 151;
     std::string command, cwd, version = "0.0.0";
-    // engine device
+    // engine devices: --device, or the --devices list (one engine per entry; packs are dealt
+    // round-robin over them; an id may repeat)
     int device = 0;
+    std::string devices;
+    size_t pack_pairs = 0;  // 0: max(max_reads_in_pack, 262144)
+    std::vector<int> device_list() const;
 
     bool paired() const { return !in2.empty() || interleaved; }
     // Options::update (src/options.cpp:24-58) minus the parts that need the evaluator

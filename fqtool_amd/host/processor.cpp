@@ -230,29 +230,54 @@ class Queue {  // bounded FIFO between pipeline threads; push/pop return at once
 
 }  // namespace
 
-// WriterThread (src/writerthread.cpp): one thread per output file, blocks written in order
+// WriterThread (src/writerthread.cpp): one thread per output file, blocks written in order.
+// A write error (full disk, deflate failure) stops the thread and is rethrown by close().
 class AsyncWriter {
    public:
     AsyncWriter(const std::string& path, int level, Pool* pool)
         : w_(path, level), pool_(pool), q_(4), t_([this] { loop(); }) {}
     ~AsyncWriter() {
-        q_.close();
-        t_.join();
+        try {
+            close();
+        } catch (...) {
+        }
     }
     void write(std::vector<std::string> blocks) {
+        if (err_) std::rethrow_exception(err_);
         bool any = false;
         for (const auto& s : blocks) any = any || !s.empty();
         if (any) q_.push(std::move(blocks));
+    }
+    void close() {
+        if (closed_) return;
+        closed_ = true;
+        q_.close();
+        t_.join();
+        if (!err_) {
+            try {
+                w_.close();
+            } catch (...) {
+                err_ = std::current_exception();
+            }
+        }
+        if (err_) std::rethrow_exception(err_);
     }
 
    private:
     void loop() {
         std::vector<std::string> b;
-        while (q_.pop(b)) w_.write(b, pool_);
+        try {
+            while (q_.pop(b)) w_.write(b, pool_);
+        } catch (...) {
+            err_ = std::current_exception();
+            q_.close();  // the producer's next push returns at once; write() rethrows
+        }
     }
     Writer w_;
     Pool* pool_;
     Queue<std::vector<std::string>> q_;
+    std::exception_ptr err_;
+    bool closed_ = false;
     std::thread t_;
 };
 
@@ -270,7 +295,12 @@ OutputSet::OutputSet(const Options& o, Pool* pool) : paired_(o.paired()) {
     }
 }
 
-OutputSet::~OutputSet() { close(); }
+OutputSet::~OutputSet() {
+    try {
+        close();
+    } catch (...) {
+    }
+}
 
 void OutputSet::write(PackOutput&& out) {
     if (wm_) wm_->write(std::move(out.merged));
@@ -284,48 +314,60 @@ void OutputSet::write(PackOutput&& out) {
 }
 
 void OutputSet::close() {
-    w1_.reset();
-    w2_.reset();
-    wu1_.reset();
-    wu2_.reset();
-    wf_.reset();
-    wm_.reset();
+    std::exception_ptr first;
+    for (auto* w : {&w1_, &w2_, &wu1_, &wu2_, &wf_, &wm_}) {
+        if (!*w) continue;
+        try {
+            (*w)->close();
+        } catch (...) {
+            if (!first) first = std::current_exception();
+        }
+        w->reset();
+    }
+    if (first) std::rethrow_exception(first);
 }
 
 namespace {
 
-struct Engine {
-    fq_engine* e = nullptr;
-    int max_cycles = 0;
-    int max_batch = 0;
-    int max_stride = 0;
-    ~Engine() {
-        if (e) fq_engine_destroy(e);
+// One engine per entry of --devices (several may share a GPU).  All have the same geometry;
+// a pack with longer reads (or more of them) re-creates them larger after draining them.
+struct Engines {
+    std::vector<int> devices;
+    std::vector<fq_engine*> e;
+    int max_cycles = 0, max_batch = 0, max_stride = 0;
+    ~Engines() { destroy(); }
+    void destroy() {
+        for (fq_engine* x : e) fq_engine_destroy(x);
+        e.clear();
     }
 };
 
 int round16(int x) { return (x + 15) & ~15; }
 
-void make_engine(Engine& eng, const Options& o, int max_cycles, int max_batch, int max_stride) {
-    if (eng.e) {
-        fq_engine_destroy(eng.e);
-        eng.e = nullptr;
-    }
+void make_engines(Engines& en, const Options& o, int max_cycles, int max_batch, int max_stride) {
+    en.destroy();
     fq_params p = o.to_params(max_cycles);
-    const int rc = fq_engine_create(&p, o.device, max_batch, max_stride, &eng.e);
-    if (rc != FQ_OK) throw std::runtime_error(std::string("fq_engine_create: ") + fq_engine_last_error(nullptr));
-    eng.max_cycles = max_cycles;
-    eng.max_batch = max_batch;
-    eng.max_stride = max_stride;
+    for (int dev : en.devices) {
+        fq_engine* x = nullptr;
+        const int rc = fq_engine_create(&p, dev, max_batch, max_stride, &x);
+        if (rc != FQ_OK)
+            throw std::runtime_error("fq_engine_create (device " + std::to_string(dev) + "): " + fq_engine_last_error(nullptr));
+        en.e.push_back(x);
+    }
+    en.max_cycles = max_cycles;
+    en.max_batch = max_batch;
+    en.max_stride = max_stride;
 }
 
-void drain(Engine& eng, HostAcc& acc) {
-    if (!eng.e) return;
-    std::vector<uint64_t> buf(fq_engine_acc_words(eng.e));
-    if (fq_engine_read_acc(eng.e, buf.data(), buf.size()) != FQ_OK)
-        throw std::runtime_error(std::string("fq_engine_read_acc: ") + fq_engine_last_error(eng.e));
-    acc.add(buf.data(), eng.max_cycles);
-    fq_engine_reset_acc(eng.e);
+// the engines' accumulators summed into the host's (RCCL-free: they are in this process)
+void drain(Engines& en, HostAcc& acc) {
+    for (fq_engine* x : en.e) {
+        std::vector<uint64_t> buf(fq_engine_acc_words(x));
+        if (fq_engine_read_acc(x, buf.data(), buf.size()) != FQ_OK)
+            throw std::runtime_error(std::string("fq_engine_read_acc: ") + fq_engine_last_error(x));
+        acc.add(buf.data(), en.max_cycles);
+        fq_engine_reset_acc(x);
+    }
 }
 
 void log(const std::string& s) {
@@ -397,18 +439,23 @@ int run_tool(int argc, char** argv) {
     const double prepass_s = since(t0);
     try {
         const bool paired = o.paired();
-        const size_t pack_n = std::max<size_t>(o.max_reads_in_pack, 262144);
+        const size_t pack_n = o.pack_pairs ? o.pack_pairs : std::max<size_t>(o.max_reads_in_pack, 262144);
         int est = std::max(o.est_seq_len1, paired ? o.est_seq_len2 : 0);
-        Engine eng;
-        make_engine(eng, o, std::max(16, round16(o.merge ? 2 * est : est)), (int)pack_n, round16(std::max(est, 16)));
+        Engines eng;
+        eng.devices = o.device_list();
+        const int G = (int)eng.devices.size();
+        const int depth = G > 2 ? 2 : 3;  // packs in flight per engine (each holds a device slot)
+        make_engines(eng, o, std::max(16, round16(o.merge ? 2 * est : est)), (int)pack_n, round16(std::max(est, 16)));
         // -w host threads (the reference's worker count) pack tiles, format and compress
         Pool pool(std::max(0, o.threads - 1));
         OutputSet outs(o, &pool);
-        // reader thread -> engine + formatting (this thread) -> writer threads; four packs are
-        // recycled so their arenas and planes keep their capacity
-        Queue<std::unique_ptr<Pack>> packs(2), spare(4);
-        for (int i = 0; i < 4; ++i) spare.push(std::unique_ptr<Pack>(new Pack()));
-        std::exception_ptr reader_err;
+        // reader thread -> dispatcher (this thread: submit to engine seq_no mod G, poll in
+        // submission order) -> formatter thread (records -> output text, in input order) ->
+        // writer threads.  Packs (pinned planes and records) are recycled.
+        const int n_packs = G * depth + 4;
+        Queue<std::unique_ptr<Pack>> packs(2), done(2), spare((size_t)n_packs);
+        for (int i = 0; i < n_packs; ++i) spare.push(std::unique_ptr<Pack>(new Pack(true)));
+        std::exception_ptr reader_err, format_err;
         std::thread reader([&] {
             try {
                 PackReader pr(o.in1, o.in2, o.interleaved, o.phred64);
@@ -421,9 +468,46 @@ int run_tool(int argc, char** argv) {
         });
         HostAcc acc(o.insert_size_max);
         AdapterCounts ac;
-        std::vector<fq_read_result> res;
         uint64_t reads = 0;
         double engine_s = 0, format_s = 0;
+        std::thread formatter([&] {
+            try {
+                std::unique_ptr<Pack> pk;
+                while (done.pop(pk)) {
+                    const auto f0 = std::chrono::steady_clock::now();
+                    const fq_params p = o.to_params(eng.max_cycles);
+                    if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p);
+                    PackOutput out;
+                    format_pack(o, *pk, pk->res.data(), out, &pool);
+                    format_s += since(f0);
+                    outs.write(std::move(out));
+                    reads += (uint64_t)pk->n * (paired ? 2 : 1);
+                    spare.push(std::move(pk));
+                }
+            } catch (...) {
+                format_err = std::current_exception();
+                done.close();
+                spare.close();
+                packs.close();
+            }
+        });
+        struct InFlight {
+            std::unique_ptr<Pack> pk;
+            int g;
+        };
+        std::deque<InFlight> inflight;  // submission order == input order
+        auto complete_oldest = [&] {
+            InFlight f = std::move(inflight.front());
+            inflight.pop_front();
+            uint64_t seq = 0;
+            const auto e0 = std::chrono::steady_clock::now();
+            const int rc = fq_engine_poll(eng.e[(size_t)f.g], 1, &seq);
+            engine_s += since(e0);
+            if (rc != 1)
+                throw std::runtime_error(std::string("fq_engine_poll: ") + fq_engine_last_error(eng.e[(size_t)f.g]));
+            if (seq != f.pk->seq_no) throw std::runtime_error("engine completed packs out of order");
+            done.push(std::move(f.pk));
+        };
         try {
             std::unique_ptr<Pack> pk;
             while (packs.pop(pk)) {
@@ -433,42 +517,43 @@ int run_tool(int argc, char** argv) {
                     for (uint16_t l : pk->len[1]) max2 = std::max(max2, (int)l);
                 const int need = o.merge ? max1 + max2 : std::max(max1, max2);
                 if (need > eng.max_cycles || pk->stride > eng.max_stride || pk->n > eng.max_batch) {
-                    drain(eng, acc);  // keep what the old engine accumulated, then grow it
-                    make_engine(eng, o, std::max(eng.max_cycles, round16(need)), std::max(eng.max_batch, pk->n),
-                                std::max(eng.max_stride, pk->stride));
+                    while (!inflight.empty()) complete_oldest();
+                    drain(eng, acc);  // keep what the old engines accumulated, then grow them
+                    make_engines(eng, o, std::max(eng.max_cycles, round16(need)), std::max(eng.max_batch, pk->n),
+                                 std::max(eng.max_stride, pk->stride));
                 }
-                res.resize((size_t)pk->n * (paired ? 2 : 1));
+                if ((int)inflight.size() >= G * depth) complete_oldest();
+                const int g = (int)(pk->seq_no % (uint64_t)G);
                 const fq_batch b = pk->batch();
                 const auto e0 = std::chrono::steady_clock::now();
-                if (fq_engine_process(eng.e, &b, res.data()) != FQ_OK)
-                    throw std::runtime_error(std::string("fq_engine_process: ") + fq_engine_last_error(eng.e));
+                if (fq_engine_submit(eng.e[(size_t)g], &b, pk->results(), pk->seq_no) != FQ_OK)
+                    throw std::runtime_error(std::string("fq_engine_submit: ") + fq_engine_last_error(eng.e[(size_t)g]));
                 engine_s += since(e0);
-                const auto f0 = std::chrono::steady_clock::now();
-                const fq_params p = o.to_params(eng.max_cycles);
-                if (o.adapter_trimming) ac.add(*pk, res.data(), p);
-                PackOutput out;
-                format_pack(o, *pk, res.data(), out, &pool);
-                format_s += since(f0);
-                outs.write(std::move(out));
-                reads += (uint64_t)pk->n * (paired ? 2 : 1);
-                spare.push(std::move(pk));
+                inflight.push_back(InFlight{std::move(pk), g});
             }
+            while (!inflight.empty()) complete_oldest();
         } catch (...) {
             packs.close();
             spare.close();
+            done.close();
             reader.join();
+            formatter.join();
             throw;
         }
+        done.close();
+        formatter.join();
         reader.join();
+        if (format_err) std::rethrow_exception(format_err);
         if (reader_err) std::rethrow_exception(reader_err);
         drain(eng, acc);
         outs.close();
         const Json rep = build_report(o, acc, ac);
         std::ofstream js(o.json_file, std::ios::binary);
         js << rep.dump(4);
-        log("fqtool-amd: " + std::to_string(reads) + " reads, wall " + std::to_string(since(t0)) + " s, engine " +
-            std::to_string(engine_s) + " s; pre-pass " + std::to_string(prepass_s) + " s, format " +
-            std::to_string(format_s) + " s; JSON report " + o.json_file + " (no HTML report in this build)");
+        log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s), wall " +
+            std::to_string(since(t0)) + " s, engine submit/wait " + std::to_string(engine_s) + " s; pre-pass " +
+            std::to_string(prepass_s) + " s, format " + std::to_string(format_s) + " s; JSON report " + o.json_file +
+            " (no HTML report in this build)");
     } catch (const std::exception& e) {
         std::cerr << "ERROR: " << e.what() << std::endl;
         return 255;

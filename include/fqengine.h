@@ -257,9 +257,34 @@ int fq_engine_process(fq_engine* e, const fq_batch* host_batch, fq_read_result* 
 
 /* Device-resident pack (inputs already in HBM): enqueues the kernels on `stream`
  * (a hipStream_t; NULL = the HIP default stream) and returns without synchronising.
- * `device_results` may be NULL when the caller needs only the accumulators. */
+ * `device_results` may be NULL when the caller needs only the accumulators.
+ * The engine's hand-off tile list is shared by these calls: use one stream at a time per
+ * engine (concurrent streams need one engine each). */
 int fq_engine_process_device(fq_engine* e, const fq_batch* device_batch,
                              fq_read_result* device_results, void* stream);
+
+/* ---- asynchronous host-pack pipeline ---------------------------------------------------
+ * Replaces the reference's concurrent workers over disjoint packs (consumePack on -w threads,
+ * src/peprocessor.cpp:546-566) with an in-order device pipeline per engine:
+ * fq_engine_submit enqueues one host pack -- H2D on a copy-in stream, the kernels on the compute
+ * stream, D2H of its records into `results` on a copy-out stream -- and returns without waiting.
+ * Up to 3 packs are in flight per engine (a further submit first waits for the oldest pack's
+ * device slot to drain).  The host batch arrays and `results` must stay valid and untouched
+ * until fq_engine_poll has reported `seq_no`.  With pinned host memory (fq_host_alloc) pack
+ * k+1's H2D overlaps pack k's kernels and pack k-1's D2H.
+ * fq_engine_poll reports packs in submission order: it returns 1 and sets *seq_no when the
+ * oldest pending pack is complete (its records are in its `results`), 0 when nothing is pending
+ * or (wait == 0) the oldest pack is still running, and a negative FQ_E_* code on failure.
+ * One thread submits and polls a given engine; fq_engine_process must not be mixed with
+ * packs still pending. */
+int fq_engine_submit(fq_engine* e, const fq_batch* host_batch, fq_read_result* results, uint64_t seq_no);
+int fq_engine_poll(fq_engine* e, int wait, uint64_t* seq_no);
+int fq_engine_pending(const fq_engine* e); /* packs submitted and not yet reported */
+
+/* Page-locked host memory for packs and records (hipHostMalloc, portable across devices).
+ * FQ_E_NO_DEVICE without a HIP device: callers then use ordinary memory. */
+int fq_host_alloc(size_t bytes, void** out);
+int fq_host_free(void* p);
 
 /* Accumulators */
 size_t fq_engine_acc_words(const fq_engine* e);

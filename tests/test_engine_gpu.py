@@ -197,3 +197,57 @@ def test_null_mate_after_full_pairs(eng_lib, oracle, mode):
     assert (res_o["flags"][1::2][32 * 4096:] & abi.FQ_RF_NULL).all()
     res_e, acc_e = run_engine(eng_lib, p, pk)
     assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+def test_async_submit_poll_pipeline(eng_lib, oracle):
+    """fq_engine_submit / fq_engine_poll: more packs than pipeline slots, pinned and pageable
+    host buffers, an empty pack and a ragged one; packs come back in submission order with the
+    oracle's records, and the accumulator is the sum over all packs (the reference's per-worker
+    accumulation over disjoint packs, src/peprocessor.cpp:546-566)."""
+    p = config("C3b", max_cycles=256)
+    sizes = [5000, 0, 4097, 31, 6000, 1, 5000]
+    packs = [synth_pack(oracle, n, True, first=100_000 * k) for k, n in enumerate(sizes)]
+    h = make_engine(eng_lib, p, max_batch=max(sizes), max_stride=160)
+    pinned = []
+    try:
+        outs, batches = [], []
+        for k, pk in enumerate(packs):
+            if k % 2 == 0:  # page-locked records
+                ptr = ctypes.c_void_p()
+                nbytes = max(1, pk.n * 2 * 16)
+                assert eng_lib.fq_host_alloc(nbytes, ctypes.byref(ptr)) == 0
+                pinned.append(ptr)
+                buf = (ctypes.c_uint8 * nbytes).from_address(ptr.value)
+                res = np.frombuffer(buf, dtype=np.dtype(abi.RESULT_DTYPE_FIELDS), count=pk.n * 2)
+            else:
+                res = pk.result_array()
+            outs.append(res)
+            batches.append(pk.batch())
+        got = []
+        for k, pk in enumerate(packs):
+            assert eng_lib.fq_engine_submit(h, ctypes.byref(batches[k]), outs[k].ctypes.data if outs[k].size else
+                                            ctypes.addressof(ctypes.c_uint8()), 1000 + k) == 0, \
+                eng_lib.fq_engine_last_error(h)
+            seq = ctypes.c_uint64()
+            if eng_lib.fq_engine_poll(h, 0, ctypes.byref(seq)) == 1:
+                got.append(seq.value)
+        res_dummy = packs[0].result_array()
+        assert eng_lib.fq_engine_process(h, ctypes.byref(batches[0]), res_dummy.ctypes.data) != 0  # packs pending
+        while eng_lib.fq_engine_pending(h) > 0:
+            seq = ctypes.c_uint64()
+            assert eng_lib.fq_engine_poll(h, 1, ctypes.byref(seq)) == 1
+            got.append(seq.value)
+        assert got == [1000 + k for k in range(len(packs))]
+        assert eng_lib.fq_engine_poll(h, 1, None) == 0
+        acc = np.zeros(eng_lib.fq_engine_acc_words(h), np.uint64)
+        assert eng_lib.fq_engine_read_acc(h, acc.ctypes.data, acc.size) == 0
+        want_acc = np.zeros_like(acc)
+        for k, pk in enumerate(packs):
+            res_o, acc_o = run_oracle(oracle, p, pk)
+            assert np.array_equal(outs[k], res_o), f"pack {k}"
+            want_acc += acc_o
+        assert np.array_equal(acc, want_acc)
+    finally:
+        eng_lib.fq_engine_destroy(h)
+        for ptr in pinned:
+            eng_lib.fq_host_free(ptr)

@@ -63,3 +63,19 @@ def test_fqtool_binary_matches_reference(case, tmp_path):
                        timeout=300)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     E.check_outputs(case, str(tmp_path))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", E.ok_cases())
+def test_fqtool_multi_engine_matches_reference(case, tmp_path):
+    """Packs dealt round-robin over three engines (virtual devices on one GPU, each with its
+    asynchronous pinned pipeline), small packs so every engine gets several, -w 4: the writer
+    reorders by pack sequence number and the accumulators are summed, so the FASTQ and JSON
+    must still equal the reference's -w 1 outputs."""
+    argv = E.argv_for(abi.FQTOOL_BIN, case, str(tmp_path))
+    argv[2] = "4"
+    argv += ["--devices", "0,0,0", "--pack_pairs", "777"]
+    p = subprocess.run(argv, capture_output=True, cwd=tmp_path, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    assert "on 3 engine(s)" in p.stderr.decode()
+    E.check_outputs(case, str(tmp_path))
