@@ -177,10 +177,33 @@ __device__ inline int window_scan(LdsQual qual, int s0, int send, int w, int T) 
     return send;
 }
 
+// cut_right's scan (src/filter.cpp:124-152) restricted to the windows that can be low: a window
+// whose mean is below T holds at least one base below T, so only windows overlapping a 16-position
+// chunk with such a base (bit c of low_chunks) are scanned, in order; the others are skipped.
+// The first low window in [s0, send) is the same as window_scan<false>'s (send if none).
+template <class QQ>
+__device__ inline int low_window_scan(QQ qual, int s0, int send, int w, int T, uint32_t low_chunks) {
+    int from = s0;
+    while (low_chunks) {
+        const int c = __builtin_ctz(low_chunks);
+        low_chunks &= low_chunks - 1;
+        const int a = max(from, 16 * c - w + 1), b = min(send, 16 * c + 16);  // windows overlapping chunk c
+        if (a < b) {
+            const int r = window_scan<false>(qual, a, b, w, T);
+            if (r < b) return r;
+        }
+        from = max(from, b);
+        if (from >= send) break;
+    }
+    return send;
+}
+
 // Filter::trimAndCut, reference src/filter.cpp:69-189. Returns false for NULL.
+// low_chunks: bit c set when chunk c (positions [16c, 16c+16)) may hold a quality below cut_right's
+// threshold (~0u: unknown, every window is scanned).
 template <class SQ, class QQ>
 __device__ inline bool trim_and_cut_t(const fq_params& p, SQ seq, QQ qual, int l, int front, int tail,
-                                      int& out_start, int& out_len) {
+                                      int& out_start, int& out_len, uint32_t low_chunks = ~0u) {
     const bool enF = p.cut_front, enR = p.cut_right, enT = p.cut_tail;
     if (front == 0 && tail == 0 && !enF && !enR && !enT) {
         out_start = 0;
@@ -206,7 +229,8 @@ __device__ inline bool trim_and_cut_t(const fq_params& p, SQ seq, QQ qual, int l
     if (enR) {
         const int w = p.cut_right_window, thr = 33 + p.cut_right_quality;
         if (l - front - tail - w <= 0) return false;
-        int s = window_scan<false>(qual, front, l - tail - w, w, thr);
+        int s = low_chunks == ~0u ? window_scan<false>(qual, front, l - tail - w, w, thr)
+                                  : low_window_scan(qual, front, l - tail - w, w, thr, low_chunks);
         if (s < l - tail - w) {
             while (s < l - 1 && qual(s) >= thr) ++s;
             rlen = s - front;

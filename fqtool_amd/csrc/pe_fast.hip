@@ -87,9 +87,12 @@ struct Layout {
     static constexpr int kWaves = MERGE ? 7 : 8;
     static constexpr int kThreads = 64 * kWaves;
     static constexpr int kWaveW = kCodeW + (LEAN ? 0 : 64 * kQS);
-    static constexpr int kHists = MERGE ? 5 : 4;  // [pre1, pre2, post1 (x2 with MERGE), post2]
+    // [pre1, pre2, post1 (x2 with MERGE), post2] (+ MERGE: read 2's merged parts, cycles 0..319,
+    // in removed mode, which uses blocks 0-3 as the kept/removed rows of the two mates)
+    static constexpr int kHists = MERGE ? 6 : 4;
+    static constexpr int kXtraW = MERGE ? kSlots * 32 : 0;  // one more cycle row: dummy positions up to 335
     static constexpr int kColsW = kWaves * kWaveW;
-    static constexpr int kLdsW = kColsW + kHists * kHistW + kSmallW + kScalW + kAdW;
+    static constexpr int kLdsW = kColsW + kHists * kHistW + kXtraW + kSmallW + kScalW + kAdW;
     static_assert(kLdsW * 4 * kBlocksPerCU <= 160 * 1024, "LDS budget");
     static_assert((kColsW & 1) == 0 && (kHistW & 1) == 0, "u64 cells must stay 8-byte aligned");
     static_assert(kThreads <= kBlock, "launch bound");
@@ -485,10 +488,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     uint32_t* col = lds + wave * LY::kWaveW;  // code / N columns: word field*64 + lane
     uint32_t* qrows = col + kCodeW;           // full variant: quality rows, row = lane
     uint32_t* hist = lds + LY::kColsW;        // [pre1, pre2, post1, post2] x kHistW (post1 x2 with MERGE)
-    unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + LY::kHists * kHistW);
+    unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + LY::kHists * kHistW + LY::kXtraW);
     unsigned long long* scal = small + kSmallW / 2;
     uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16 * kScalCopies);
-    for (int i = threadIdx.x; i < LY::kHists * kHistW + kSmallW + kScalW; i += kThreads) hist[i] = 0;
+    for (int i = threadIdx.x; i < LY::kHists * kHistW + LY::kXtraW + kSmallW + kScalW; i += kThreads) hist[i] = 0;
     for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kThreads)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
     __syncthreads();
@@ -507,11 +510,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     const int K = max(limit, 1);
     const int req = p.overlap_require;
     const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
+    // cut_right threshold 33 + q, in 0..93 (CLI range): the same SWAR below-threshold test
+    const bool lowr_ok = p.cut_right && 33 + p.cut_right_quality >= 1 && 33 + p.cut_right_quality <= 127;
+    const uint32_t limr = lowr_ok ? (uint32_t)(0x80 - (33 + p.cut_right_quality)) * 0x01010101u : 0u;
     // Without front trimming every kept window starts at 0, so each base lands in exactly one of
     // two disjoint blocks: "kept" (inside a passing read's window; the post block) or "removed"
     // (trimmed tails, failed pairs; the pre block), one LDS atomic per base.  At the flush
     // pre = kept + removed and post = kept.
-    const bool removed_mode = !MERGE && (LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front));
+    const bool removed_mode = LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front);
     const int g_per = max(p.polyg_one_mismatch_per, 1);
     const int g_inv = g_per > 256 ? 0 : (65536 + g_per - 1) / g_per;
 #ifdef FQ_PHASE_STAMPS
@@ -567,6 +573,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4) ||
                          (MERGE && L + xor32(L) > p.max_cycles);
         uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0, lowf = 0, tqf = 0, nbf = 0;  // whole-read sums
+        uint32_t lowr = 0;  // FULL with cut_right: bit k = chunk k holds a quality below its threshold
         // column word of chunk k: k for read 1, 9-k for read 2 (stepped, not precomputed, so the
         // ten addresses are not kept live across tiles)
         uint32_t* wp = col + lane_x + (rc ? (kChunks - 1) * 64 : 0);
@@ -608,7 +615,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 #endif
                 const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
                 const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
-                uint32_t cc = 0, nn4 = 0;
+                uint32_t cc = 0, nn4 = 0, lr = 0;
                 // bases of this chunk still in the read; opaque, or the masks of all ten chunks
                 // (functions of L alone) are computed up front and kept live across the loop
                 int Lk = L - 16 * k;
@@ -637,6 +644,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     q30 += __popc((qm + 0x40404040u) & (0x80808080u & bm));  // q > '?'
                     lowf += __popc(~(qm + limq) & (0x80808080u & bm));        // q < limit
                     if (!LEAN) tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);    // (LEAN excludes -e)
+                    if (!LEAN) lr |= ~(qm + limr) & (0x80808080u & bm);         // q < cut_right threshold
                     cc |= (kk & 0x03030303u) << (2 * j);
                     nn4 |= ((kk >> 2) & 0x01010101u) << (2 * j);
                 };
@@ -647,6 +655,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 #pragma unroll
                     for (int j = 0; j < 4; ++j) dword(j, std::false_type{});
                 }
+                if (!LEAN) lowr |= (lr != 0 ? 1u : 0u) << k;
                 // N flags are kept only for positions inside the read (later passes rely on it)
                 const uint32_t fck = tr4x4(cc), fwk = tr4x4(nn4) & (full ? 0x55555555u : posmask(Lk));
                 nbf += __popc(fwk);
@@ -701,7 +710,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             nn = valid;
             n = L;
         } else {
-            nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n);
+            nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n, lowr_ok ? lowr : ~0u);
         }
         // the shuffle must run in every lane: ds_bpermute from a lane that is switched off returns
         // whatever its register held before (e.g. the previous tile's value)
@@ -803,10 +812,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             return ov;
         };
         // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
+        Overlap ov1{0, 0, 0, 0};  // (merge) the first analysis and the windows it saw
+        int n1a = -1, n2a = -1;
+        bool ad_ov = false;
         if (PAIRED && both && !(abl & 1)) {
             const Overlap ov = pair_overlap();
             const int n_o = xor32(n);
             const int n1 = mate ? n_o : n, n2 = mate ? n : n_o;
+            if (MERGE) {
+                ov1 = ov;
+                n1a = n1;
+                n2a = n2;
+            }
             if (mate == 0) {  // PairEndProcessor::statInsertSize, src/peprocessor.cpp:510-523
                 int isize = p.insert_size_max;
                 if (ov.overlapped) isize = ov.offset > 0 ? n1 + n2 - ov.len : ov.len;
@@ -816,6 +833,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             if (p.adapter_trimming) {
                 const int ol = ov.len;  // AdapterTrimmer::trimByOverlapAnalysis, src/adaptertrimmer.cpp:14-27
                 if (ov.diff <= 5 && ov.overlapped && ov.offset < 0 && ol > n1 / 3) {
+                    ad_ov = true;
                     rr.flags |= FQ_RF_AD_OVERLAP;
                     rr.ad_pos = (uint16_t)(st + ol);
                     rr.ad_len = (uint16_t)(n - ol);
@@ -847,7 +865,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         bool merged = false;
         int m1 = 0, m2 = 0, mol = 0;
         if (MERGE && both) {
-            const Overlap ov2 = pair_overlap();
+            // OverlapAnalysis::analyze of the current windows (src/peprocessor.cpp:354).  Known
+            // without a scan (pair-uniform test): when neither window changed since the first
+            // analysis, the same result; when only trimByOverlapAnalysis cut both reads to the
+            // phase-2 overlap ol = len2 - k (offset -k), the trimmed pair compares exactly the same
+            // bases at offset 0, the first offset phase 1 tries, so {1, 0, ol, diff}.
+            const int n_o = xor32(n);
+            const int n1c = mate ? n_o : n, n2c = mate ? n : n_o;
+            const bool same = n1a >= 0 && n1c == n1a && n2c == n2a;
+            const bool derived = n1a >= 0 && ad_ov && n1c == ov1.len && n2c == ov1.len && ov1.len == n2a + ov1.offset;
+            Overlap ov2 = same ? ov1 : Overlap{1, 0, ov1.len, ov1.diff};
+            if (!same && !derived) ov2 = pair_overlap();  // pair-uniform branch (the mate lanes swap values)
             if (ov2.overlapped) {
                 merged = true;
                 mol = ov2.len;
@@ -984,7 +1012,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             // removed (pre = kept + removed at the flush), one LDS atomic per base.  Per chunk the
             // 16 slot numbers are built as nibbles (SWAR), rotated by r positions like the
             // qualities, so a base costs a nibble extract, an address and a byte extract.
-            const int wlen = post_on ? wn : 0;
+            // (merge: read 2's part of a merged read is not a prefix of read 2; it goes to read 1's
+            // post block at other cycles, below, and read 2's own bases only to its pre block)
+            const int wlen = post_on && !(MERGE && merged && mate) ? wn : 0;
             const int dsel = r >> 2, rr4 = 4 * (r & 7);
             const bool rswap = r >= 8;
             // LDS byte address of rotated position t's cell in slot 0 of chunk 0 (this mate's rows)
@@ -1059,6 +1089,67 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                         __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)a), kCount1 | (unsigned long long)qv,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
+                }
+            }
+        }
+        if (MERGE && removed_mode && valid && !(abl & 4) && merged && mate && post_on) {
+            // Read 2's part of the merged read, rc(r2)[ol, ol + m2) at merged cycles m1 .. m1+m2-1
+            // (OverlapAnalysis::merge src/overlapanalysis.cpp:74-104, then Stats::statRead of the
+            // merged read, src/peprocessor.cpp:361): read 2's column holds the reverse complement,
+            // so merged position j is column index 159 - pos_hi + j (codes already complemented);
+            // its quality is read 2's byte at forward position pos_hi - j.  Cells: cycle rows of
+            // the extra block, count << 40 | sum(q); N bases are counted as G and moved.
+            const uint32_t xb = (uint32_t)(LY::kColsW + 4 * kHistW) * 4u;
+            const int pos_hi = ws + wn - 1;
+            const int ci0 = kMaxLen - 1 - pos_hi;
+            uint32_t rb[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int c = m1 + t;
+                rb[t] = xb + (uint32_t)((((c >> 4) * kSlots) * 32 + 2 * (c & 15)) * 4);
+            }
+            for (int J = 0; 16 * J < wn; ++J) {
+                const uint32_t cw = field_window(col, kFC, lane_x, ci0 + 16 * J);
+                const uint32_t nw = field_window(col, kFN, lane_x, ci0 + 16 * J);
+                // qualities of forward positions [hi - 15, hi], hi = pos_hi - 16J, ascending in
+                // a0..a3, then reversed: qrev[k] byte b = merged t = 4k + b
+                const int lo = pos_hi - 16 * J - 15;
+                const int wl = lo >> 2, sh = lo & 3;  // (lo < 0 only for dummy positions)
+                uint32_t qw5[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) qw5[i] = qrow[min(max(wl + i, 0), kQS - 1)];
+                uint32_t qa[4], qrev[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) qa[i] = __builtin_amdgcn_alignbyte(qw5[i + 1], qw5[i], sh);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) qrev[i] = __builtin_amdgcn_perm(0u, qa[3 - i], 0x00010203u);
+                // slot nibbles: code, or the dummy slot beyond the part
+                const int rem = wn - 16 * J;
+                const unsigned long long dm = ~0ull << min(4 * max(rem, 0), 63);
+                uint32_t nlo = spread2to4(cw), nhi = spread2to4(cw >> 16);
+                const uint32_t dlo = (uint32_t)dm, dhi = rem >= 16 ? 0u : (uint32_t)(dm >> 32);
+                nlo = (nlo & ~dlo) | (dlo & 0x55555555u);  // 5 = kDummySlot
+                nhi = (nhi & ~dhi) | (dhi & 0x55555555u);
+                const uint32_t jb = (uint32_t)J * (uint32_t)(kSlots * 32 * 4);
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const uint32_t ks = __builtin_amdgcn_ubfe(t < 8 ? nlo : nhi, 4 * (t & 7), 4);
+                    const uint32_t qv = __builtin_amdgcn_ubfe(qrev[t >> 2], 8 * (t & 3), 8);
+                    const uint32_t a = rb[t] + jb + (ks << 7);
+                    __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)a), kCount1 | (unsigned long long)qv,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                uint32_t nv = nw & posmask(rem);
+                while (nv) {  // N (code 3): from the G slot (3) to the N slot (4)
+                    const int t = (__ffs(nv) - 1) >> 1;
+                    nv &= nv - 1;
+                    const unsigned long long v =
+                        kCount1 | (unsigned long long)__builtin_amdgcn_ubfe(qrev[t >> 2], 8 * (t & 3), 8);
+                    const uint32_t a = rb[t] + jb;
+                    __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + 4u * 128u)), v, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + 3u * 128u)), 0ull - v,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
@@ -1202,6 +1293,21 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 atomicAdd(&dst[cls], (unsigned long long)cnt);
                 atomicAdd(&dst[8 + cls], (unsigned long long)qs);
             }
+        }
+    }
+    if (MERGE && removed_mode) {  // read 2's merged parts: post1 (acc block 2) at cycles < 320
+        const int ncyc = min(2 * kMaxLen, p.max_cycles);
+        const uint32_t* hx = hist + 4 * kHistW;
+        for (int i = threadIdx.x; i < ncyc * 5; i += kThreads) {
+            const int c = i / 5, slot = i - c * 5;
+            const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hx + cell(c, slot));
+            const long long cnt = (long long)(v >> 40);
+            const long long qs = (long long)(v & kQMask) - 33ll * cnt;
+            if (cnt == 0 && qs == 0) continue;
+            const int cls = slot_class(slot);
+            unsigned long long* dst = acc + st_base + 2 * st_words + FQ_ST_CYCLES + (size_t)c * FQ_ST_PER_CYCLE;
+            atomicAdd(&dst[cls], (unsigned long long)cnt);
+            atomicAdd(&dst[8 + cls], (unsigned long long)qs);
         }
     }
     for (int k = 0; k < 4 && !removed_mode; ++k) {

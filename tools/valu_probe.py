@@ -19,8 +19,10 @@ res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
 torch.cuda.synchronize()
 bits = {"full": 0, "no_overlap": 1, "no_filter": 2, "no_stats": 4, "no_polyg": 8, "stage_only": 15,
         "no_ov_exact": 64, "no_ov_scan": 128}
+import bench
+CFG = os.environ.get("CONFIG", "C3")
 for name in os.environ.get("VARIANTS", "full,no_overlap,no_filter,no_stats,no_polyg,stage_only").split(","):
-    p = abi.default_params(True, 256); p.qual_filter_enabled = 1; p.adapter_trimming = 1; p.polyg_enabled = 1
+    p = bench.config_params(abi, CFG)
     p.reserved[0] = bits[name]
     h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
     lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_engine_sync(h)
