@@ -83,77 +83,143 @@ def c3_params(abi, max_cycles=256):
     return config_params(abi, "C3", max_cycles)
 
 
-def write_fastq_pair(seq1, qual1, seq2, qual2, first_index, d):
-    """Format pairs as FASTQ files (for the reference CPU baseline run)."""
-    paths = []
-    for mate, (s, q) in enumerate(((seq1, qual1), (seq2, qual2)), start=1):
-        path = os.path.join(d, f"r{mate}.fq")
-        with open(path, "wb") as f:
-            chunks = []
-            for i in range(s.shape[0]):
-                idx = first_index + i
-                chunks.append(b"@SYN:1:1101:%d:%d %d:N:0:ACGTACGT\n%s\n+\n%s\n"
-                              % (idx % 100000, idx // 100000, mate, s[i].tobytes(), q[i].tobytes()))
-                if len(chunks) >= 65536:
-                    f.write(b"".join(chunks))
-                    chunks = []
-            f.write(b"".join(chunks))
-        paths.append(path)
+def write_fastq_fast(planes, n, first_index, d, tag=""):
+    """Format n pairs (tiled device planes: seq1, qual1, seq2, qual2) as two FASTQ files of
+    fixed-width records, vectorised (numpy), chunk by chunk:
+    @SYN:1:1101:<idx % 100000, 5 digits>:<idx // 100000, 7 digits> <mate>:N:0:ACGTACGT"""
+    import numpy as np
+
+    from fqtool_amd import abi
+
+    L = READ_LEN
+    head = b"@SYN:1:1101:"
+    name_len = len(head) + 5 + 1 + 7 + len(b" 1:N:0:ACGTACGT")
+    rec_len = name_len + 1 + L + 3 + L + 1
+    paths = [os.path.join(d, f"{tag}r{m}.fq") for m in (1, 2)]
+    files = [open(p_, "wb") for p_ in paths]
+    try:
+        step = 1 << 20  # pairs per chunk (multiple of the tile size)
+        for lo in range(0, n, step):
+            hi = min(n, lo + step)
+            k = hi - lo
+            idx = np.arange(first_index + lo, first_index + hi, dtype=np.int64)
+            digits = []
+            for v, w in ((idx % 100000, 5), (idx // 100000, 7)):
+                digits.append(np.stack([(v // 10 ** (w - 1 - j)) % 10 + 48 for j in range(w)], 1).astype(np.uint8))
+            for m in range(2):
+                rec = np.empty((k, rec_len), np.uint8)
+                o = 0
+                rec[:, o:o + len(head)] = np.frombuffer(head, np.uint8)
+                o += len(head)
+                rec[:, o:o + 5] = digits[0]
+                o += 5
+                rec[:, o] = ord(":")
+                o += 1
+                rec[:, o:o + 7] = digits[1]
+                o += 7
+                tail = b" %d:N:0:ACGTACGT\n" % (m + 1)
+                rec[:, o:o + len(tail)] = np.frombuffer(tail, np.uint8)
+                o += len(tail)
+                sl = slice(lo * STRIDE, lo * STRIDE + abi.batch_bytes(k, STRIDE))
+                seq = abi.untile_rows(planes[2 * m][sl].cpu().numpy(), k, STRIDE)[:, :L]
+                qual = abi.untile_rows(planes[2 * m + 1][sl].cpu().numpy(), k, STRIDE)[:, :L]
+                rec[:, o:o + L] = seq
+                o += L
+                rec[:, o:o + 3] = np.frombuffer(b"\n+\n", np.uint8)
+                o += 3
+                rec[:, o:o + L] = qual
+                o += L
+                rec[:, o] = 10
+                files[m].write(rec)  # (buffer protocol: no extra copy)
+    finally:
+        for f in files:
+            f.close()
     return paths
 
 
-def cpu_baseline(lib, abi, torch, pairs):
-    """Time the reference CPU path on a bounded sample of the same workload on this host."""
-    import numpy as np
-
-    ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
+def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
+    """Rank 0 at N=1, after the timed region: both host-side legs on FASTQ files of the same
+    synthetic workload (fixed-width records, page cache):
+      e2e          -- the fqtool-amd binary end to end (parse, pinned packs, engine on cuda:0,
+                      formatting, writers, JSON) on `e2e_pairs` pairs, outputs to /dev/null;
+      cpu_baseline -- the reference binary (oracle/_ref/fqtool_ref, -w <= 16) on the first
+                      `cpu_pairs` pairs (or, without it, the C restatement single-threaded)."""
+    n = max(cpu_pairs, e2e_pairs)
+    tmp = tempfile.mkdtemp(prefix="fqbench_")
+    rec_bytes = 2 * (40 + 2 * READ_LEN + 5)
+    free = shutil.disk_usage(tmp).free
+    if (e2e_pairs + cpu_pairs) * rec_bytes * 1.2 > free:  # keep to the space the box has
+        e2e_pairs = max(0, min(e2e_pairs, int(free / 1.2 / rec_bytes) - cpu_pairs))
+        n = max(cpu_pairs, e2e_pairs)
     dev = torch.device("cuda:0")
-    bufs = [torch.empty(abi.batch_bytes(pairs, STRIDE), dtype=torch.uint8, device=dev) for _ in range(4)]
-    lens = [torch.empty(pairs, dtype=torch.int16, device=dev) for _ in range(2)]
+    bufs = [torch.empty(abi.batch_bytes(n, STRIDE), dtype=torch.uint8, device=dev) for _ in range(4)]
+    lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
     b = abi.FqBatch()
-    b.n, b.stride = pairs, STRIDE
+    b.n, b.stride = n, STRIDE
     b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
     b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
     first = 10 ** 12  # a disjoint index range
     assert lib.fq_synth_fill_device(ctypes.byref(b), SEED, first, READ_LEN, None) == 0
     torch.cuda.synchronize()
-    arr = [abi.untile_rows(t.cpu().numpy(), pairs, STRIDE)[:, :READ_LEN] for t in bufs]
-    del bufs
-    tmp = tempfile.mkdtemp(prefix="fqbench_")
+    out = {"e2e": None, "cpu_baseline": None}
     try:
-        r1, r2 = write_fastq_pair(arr[0], arr[1], arr[2], arr[3], first, tmp)
+        t0 = time.perf_counter()
+        small = write_fastq_fast(bufs, cpu_pairs, first, tmp, "cpu_")
+        big = write_fastq_fast(bufs, e2e_pairs, first, tmp, "e2e_") if e2e_pairs else None
+        del bufs, lens
+        torch.cuda.empty_cache()
+        log(f"FASTQ written in {time.perf_counter() - t0:.1f}s ({cpu_pairs} + {e2e_pairs} pairs)")
+        opts = ["-q", "-a", "--detect_pe_adapter", "-g"]
+        if big:
+            tool = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
+            cmd = [tool, "-i", big[0], "-I", big[1], "-o", "/dev/null", "-O", "/dev/null", *opts, "-w", str(workers),
+                   "-J", os.path.join(tmp, "amd.json"), "-H", os.path.join(tmp, "amd.html")]
+            t0 = time.perf_counter()
+            p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+            dt = time.perf_counter() - t0
+            if p.returncode != 0:
+                raise RuntimeError("fqtool failed: " + p.stderr[-2000:])
+            tool_log = [l for l in p.stderr.splitlines() if "fqtool-amd:" in l]
+            gb = (os.path.getsize(big[0]) + os.path.getsize(big[1])) / 1e9
+            out["e2e"] = {"value": round(2 * e2e_pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": e2e_pairs,
+                          "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
+                          "path": "fqtool binary: FASTQ (page cache) -> parse -> pinned packs -> engine (cuda:0) -> "
+                                  "format -> /dev/null + JSON, C3 options",
+                          "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
+        ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
         if os.path.exists(ref):
-            workers = min(16, os.cpu_count() or 1)
-            cmd = [ref, "-i", r1, "-I", r2, "-o", os.path.join(tmp, "o1.fq"), "-O", os.path.join(tmp, "o2.fq"),
-                   "-q", "-a", "--detect_pe_adapter", "-g", "-w", str(workers),
+            w = min(16, workers)
+            cmd = [ref, "-i", small[0], "-I", small[1], "-o", "/dev/null", "-O", "/dev/null", *opts, "-w", str(w),
                    "-J", os.path.join(tmp, "r.json"), "-H", os.path.join(tmp, "r.html")]
             t0 = time.perf_counter()
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
             dt = time.perf_counter() - t0
-            return {"value": round(2 * pairs / dt / 1e6, 4), "unit": "Mreads/s", "cores": workers,
-                    "kind": "reference",
-                    "sample": f"{pairs} pairs ({2 * pairs} reads) of the same synthetic workload as FASTQ on "
-                              f"local disk, oracle/_ref/fqtool_ref -w {workers} (+1 reader, 2 writer threads), "
-                              f"wall {dt:.2f}s incl. its adapter-detection pre-pass"}
-        # no reference build: time the C restatement (single thread) on the packed sample
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        from oracle_lib import load_oracle
-        from batch_util import Pack, run_oracle
+            out["cpu_baseline"] = {
+                "value": round(2 * cpu_pairs / dt / 1e6, 4), "unit": "Mreads/s", "cores": w, "kind": "reference",
+                "sample": f"{cpu_pairs} pairs ({2 * cpu_pairs} reads) of the same synthetic workload as FASTQ in the "
+                          f"page cache, oracle/_ref/fqtool_ref -w {w} (+1 reader, 2 writer threads), wall {dt:.2f}s "
+                          f"incl. its adapter-detection pre-pass"}
+        else:  # no reference build: the C restatement (single thread) on the packed sample
+            import numpy as np
 
-        oracle = load_oracle()
-        pk = Pack(pairs, STRIDE, True)
-        pk.seq1[:, :READ_LEN], pk.qual1[:, :READ_LEN] = arr[0], arr[1]
-        pk.seq2[:, :READ_LEN], pk.qual2[:, :READ_LEN] = arr[2], arr[3]
-        pk.len1[:] = READ_LEN
-        pk.len2[:] = READ_LEN
-        p = c3_params(abi)
-        t0 = time.perf_counter()
-        run_oracle(oracle, p, pk)
-        dt = time.perf_counter() - t0
-        return {"value": round(2 * pairs / dt / 1e6, 4), "unit": "Mreads/s", "cores": 1, "kind": "port",
-                "sample": f"{pairs} pairs, oracle/fq_oracle.c single thread, in-memory packs"}
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            from oracle_lib import load_oracle
+            from batch_util import Pack, run_oracle
+
+            oracle = load_oracle()
+            pk = Pack(cpu_pairs, STRIDE, True)
+            b = pk.batch()
+            oracle.orc_synth_fill(ctypes.byref(b), SEED, first, READ_LEN)
+            pk.load_batch()
+            t0 = time.perf_counter()
+            run_oracle(oracle, c3_params(abi), pk)
+            dt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": round(2 * cpu_pairs / dt / 1e6, 4), "unit": "Mreads/s", "cores": 1,
+                                   "kind": "port",
+                                   "sample": f"{cpu_pairs} pairs, oracle/fq_oracle.c single thread, in-memory packs"}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+    return out
 
 
 class HipRunner:
@@ -322,10 +388,10 @@ class HipRunner:
                 if not isinstance(x, tuple):
                     lib.fq_host_free(x)
 
-    def cpu_baseline(self, pairs):
+    def host_legs(self, cpu_pairs, e2e_pairs, workers):
         del self.planes, self.lens, self.results
         self.torch.cuda.empty_cache()
-        return cpu_baseline(self.lib, self.abi, self.torch, pairs)
+        return host_legs(self.lib, self.abi, self.torch, cpu_pairs, e2e_pairs, workers)
 
     def close(self):
         self.lib.fq_engine_destroy(self.h)
@@ -464,12 +530,16 @@ def run_rank(args):
         "cpu_baseline": None,
         "engine_mreads_s": engine["value"] if engine else None,
         "engine": engine,
+        "e2e": None,
         "acc_sha256": acc_digest,
         "parity_sample": sample,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C3":
-        log(f"CPU baseline on {args.cpu_pairs} pairs ...")
-        out["cpu_baseline"] = runner.cpu_baseline(args.cpu_pairs)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C3" and hasattr(runner, "host_legs"):
+        log(f"host legs: e2e on {args.e2e_pairs} pairs, CPU baseline on {args.cpu_pairs} pairs ...")
+        legs = runner.host_legs(args.cpu_pairs, args.e2e_pairs, min(16, os.cpu_count() or 1))
+        out["cpu_baseline"] = legs["cpu_baseline"]
+        out["e2e"] = legs["e2e"]
+        log(f"e2e {legs['e2e']}")
     runner.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -511,7 +581,8 @@ def main():
                     help="pairs (SE: reads) per GPU; default 100 M (BASELINE configs 1-3), 125 M for C5 "
                          "(config 4's 1 B pairs over 8 GPUs)")
     ap.add_argument("--cpu-pairs", type=int, default=1_000_000, help="CPU-baseline sample size (pairs)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip both host legs (e2e and CPU baseline)")
+    ap.add_argument("--e2e-pairs", type=int, default=10_000_000, help="pairs of the end-to-end tool leg (0: off)")
     ap.add_argument("--sample-pairs", type=int, default=1_000_000,
                     help="per-rank parity sample checked against the oracle after the timed region (0: off)")
     ap.add_argument("--engine-pairs", type=int, default=1_048_576,

@@ -244,6 +244,8 @@ def load_host(path=HOST_LIB):
     lib.fqh_session_finish.argtypes = [vp]
     lib.fqh_session_finish.restype = vp
     lib.fqh_session_close.argtypes = [vp]
+    lib.fqh_debug_records.argtypes = [ctypes.c_char_p, ci, ci, ci, ci]
+    lib.fqh_debug_records.restype = vp
     return lib
 
 
@@ -258,5 +260,5 @@ HOST_SYMBOLS = [
     "fqh_run", "fqh_json_double", "fqh_merged_name", "fqh_evaluate_read_len", "fqh_detect_adapter",
     "fqh_report_json", "fqh_free", "fqh_session_open", "fqh_session_error", "fqh_session_params",
     "fqh_session_next", "fqh_session_consume", "fqh_session_add_acc", "fqh_session_finish",
-    "fqh_session_close",
+    "fqh_session_close", "fqh_debug_records",
 ]

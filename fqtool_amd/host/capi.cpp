@@ -190,4 +190,47 @@ char* fqh_session_finish(fqh_session* s) {
 
 void fqh_session_close(fqh_session* s) { delete s; }
 
+char* fqh_debug_records(const char* path, int bulk, int buf_size, int pack_n, int phred64) {
+    std::string out;
+    auto put = [&](const char* a, size_t la, const char* b, size_t lb, const char* c, size_t lc, const char* d,
+                   size_t ld) {
+        out.append(a, la).append("\t").append(b, lb).append("\t").append(c, lc).append("\t").append(d, ld).append("\n");
+    };
+    try {
+        if (bulk) {
+            FqBulkReader r(path, phred64 != 0, buf_size);
+            ByteBuf text;
+            Rec rc;
+            for (bool more = true; more;) {
+                r.begin(text);
+                int k = 0;
+                while (k < pack_n && (more = r.read(rc))) {
+                    const char* t = text.data();
+                    put(t + rc.off, rc.name_len, t + rc.seq_off(), rc.len, t + rc.strand_off(), rc.strand_len,
+                        t + rc.qual_off(), rc.len);
+                    ++k;
+                }
+                r.end();
+            }
+            out += r.error();
+        } else {
+            FqReader r(path, phred64 != 0, buf_size);
+            ByteBuf text;
+            Rec rc;
+            while (r.read(text, rc)) {
+                const char* t = text.data();
+                put(t + rc.off, rc.name_len, t + rc.seq_off(), rc.len, t + rc.strand_off(), rc.strand_len,
+                    t + rc.qual_off(), rc.len);
+                text.clear();
+            }
+            out += r.error();
+        }
+    } catch (const std::exception& e) {
+        out += std::string("EXCEPTION: ") + e.what();
+    }
+    char* res = (char*)std::malloc(out.size() + 1);
+    std::memcpy(res, out.c_str(), out.size() + 1);
+    return res;
+}
+
 }  // extern "C"

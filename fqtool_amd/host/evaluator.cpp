@@ -161,7 +161,7 @@ std::string detect_adapter(const std::string& path, int trim_tail1, std::string*
             break;
         }
         bases += rec.len;
-        reads.emplace_back(text.data() + rec.off + rec.name_len, rec.len);
+        reads.emplace_back(text.data() + rec.seq_off(), rec.len);
     }
     if (reads.size() < 10000) return "";
     const int shift_tail = std::max(1, trim_tail1);

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -78,7 +79,8 @@ void ByteBuf::reserve(size_t n) {
     is_pinned_ = pinned;
 }
 
-FqReader::FqReader(const std::string& path, bool phred64) : phred64_(phred64), buf_(kBufSize) {
+FqReader::FqReader(const std::string& path, bool phred64, int buf_size)
+    : phred64_(phred64), buf_size_(buf_size), buf_((size_t)buf_size) {
     if (ends_with(path, ".gz")) {
         gz_ = gzopen(path.c_str(), "r");
         if (!gz_) throw std::runtime_error("Failed to open file: " + path);
@@ -98,15 +100,15 @@ FqReader::~FqReader() {
 
 void FqReader::fill() {  // FqReader::readToBuf, src/fqreader.cpp:30-44
     if (gz_) {
-        len_ = gzread(gz_, buf_.data(), kBufSize);
+        len_ = gzread(gz_, buf_.data(), (unsigned)buf_size_);
         if (len_ < 0) {
             std::cerr << "Error to read gzip file" << std::endl;
             len_ = 0;
         }
-        eof_ = gzeof(gz_) != 0 || len_ < kBufSize;
+        eof_ = gzeof(gz_) != 0 || len_ < buf_size_;
     } else {
-        len_ = (int)std::fread(buf_.data(), 1, kBufSize, fp_);
-        eof_ = std::feof(fp_) != 0 || len_ < kBufSize;
+        len_ = (int)std::fread(buf_.data(), 1, (size_t)buf_size_, fp_);
+        eof_ = std::feof(fp_) != 0 || len_ < buf_size_;
     }
     used_ = 0;
 }
@@ -118,7 +120,7 @@ void FqReader::get_line(ByteBuf& out) {
     const int start = used_;
     const char* b = buf_.data();
     int end = start < len_ ? (int)(line_end(b + start, (size_t)(len_ - start)) - b) : start;
-    if (end < len_ || len_ < kBufSize) {
+    if (end < len_ || len_ < buf_size_) {
         const int s = std::min(start, len_);
         const int k = std::max(0, end - start);
         if (k) std::memcpy(out.extend((size_t)k), b + s, (size_t)k);
@@ -132,7 +134,7 @@ void FqReader::get_line(ByteBuf& out) {
         fill();
         b = buf_.data();
         end = len_ > 0 ? (int)(line_end(b, (size_t)len_) - b) : 0;
-        if (end < len_ || len_ < kBufSize) {
+        if (end < len_ || len_ < buf_size_) {
             if (end) std::memcpy(out.extend((size_t)end), b, (size_t)end);
             ++end;
             if (end < len_ - 1 && b[end] == '\n') ++end;
@@ -183,6 +185,7 @@ bool FqReader::read(ByteBuf& text, Rec& r) {
     r.name_len = (uint32_t)name_len;
     r.strand_len = (uint32_t)strand_len;
     r.len = (uint32_t)seq_len;
+    r.gap[0] = r.gap[1] = r.gap[2] = 0;
     return true;
 }
 
@@ -193,11 +196,157 @@ bool FqReader::read(std::string& name, std::string& seq, std::string& strand, st
         if (!err_.empty()) std::cerr << err_;
         return false;
     }
-    const char* p = scratch_.data() + r.off;
-    name.assign(p, r.name_len);
-    seq.assign(p + r.name_len, r.len);
-    strand.assign(p + r.name_len + r.len, r.strand_len);
-    qual.assign(p + r.name_len + r.len + r.strand_len, r.len);
+    const char* p = scratch_.data();
+    name.assign(p + r.off, r.name_len);
+    seq.assign(p + r.seq_off(), r.len);
+    strand.assign(p + r.strand_off(), r.strand_len);
+    qual.assign(p + r.qual_off(), r.len);
+    return true;
+}
+
+// ---- FqBulkReader ----
+FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
+    : phred64_(phred64), bsize_((uint64_t)buf_size) {
+    if (ends_with(path, ".gz")) {
+        gz_ = gzopen(path.c_str(), "r");
+        if (!gz_) throw std::runtime_error("Failed to open file: " + path);
+        gzbuffer(gz_, 1 << 20);
+        gzrewind(gz_);
+    } else {
+        fp_ = path == "/dev/stdin" ? stdin : std::fopen(path.c_str(), "rb");
+        if (!fp_) throw std::runtime_error("Failed to open file: " + path);
+    }
+}
+
+FqBulkReader::~FqBulkReader() {
+    if (gz_) gzclose(gz_);
+    if (fp_ && fp_ != stdin) std::fclose(fp_);
+}
+
+void FqBulkReader::begin(ByteBuf& text) {
+    text_ = &text;
+    text.clear();
+    base_ = carry_off_;
+    if (!carry_.empty()) std::memcpy(text.extend(carry_.size()), carry_.data(), carry_.size());
+    carry_.clear();
+    pos_ = 0;
+}
+
+void FqBulkReader::end() {
+    if (!text_) return;
+    const size_t n = text_->size();
+    if (pos_ < n) carry_.assign(text_->data() + pos_, n - pos_);
+    else carry_.clear();
+    carry_off_ = base_ + pos_;
+    text_ = nullptr;
+}
+
+// Reads up to the next buffer boundary past at least 4 MiB more (or to the end of the stream), so
+// every reference buffer that holds an arena byte is complete in the arena.
+void FqBulkReader::read_more() {
+    const uint64_t want_end = (total_ + (4u << 20) + bsize_ - 1) / bsize_ * bsize_;
+    size_t want = (size_t)(want_end - total_);
+    char* dst = text_->extend(want);
+    size_t got = 0;
+    if (gz_) {
+        while (got < want) {
+            const unsigned ask = (unsigned)std::min<size_t>(want - got, 1u << 30);
+            const int r = gzread(gz_, dst + got, ask);
+            if (r < 0) {
+                std::cerr << "Error to read gzip file" << std::endl;
+                break;
+            }
+            got += (size_t)r;
+            if ((unsigned)r < ask) break;
+        }
+    } else {
+        got = std::fread(dst, 1, want, fp_);
+    }
+    text_->truncate(text_->size() - (want - got));
+    total_ += got;
+    if (got < want) eof_ = true;
+}
+
+// getLine's rule (src/fqreader.cpp:139-140): a '\n' right after a terminator at buffer index e is
+// folded into it iff e + 1 < len - 1, len = that buffer's length (all but the stream's last
+// buffer are full).
+bool FqBulkReader::skip_ok(uint64_t g) const {
+    const uint64_t k = g / bsize_, e = g - k * bsize_;
+    const uint64_t len = (eof_ && total_ < (k + 1) * bsize_) ? total_ - k * bsize_ : bsize_;
+    return e + 2 < len;
+}
+
+// the line at arena offset x: [x, e), next line at `next`; reads more of the stream as needed.
+// Past the end of the stream every line is empty (the reference's getLine at EOF).
+bool FqBulkReader::line(size_t x, size_t& e, size_t& next) {
+    for (;;) {
+        const size_t n = text_->size();
+        if (x < n) {
+            const char* d = text_->data();
+            const size_t t = (size_t)(line_end(d + x, n - x) - d);
+            if (t < n) {
+                e = t;
+                next = t + 1;
+                if (next < n && d[next] == '\n' && skip_ok(base_ + t)) ++next;
+                return true;
+            }
+        }
+        if (eof_) {  // the last line has no terminator, or we are past the end: empty lines
+            e = std::max(x, n);
+            next = e + 1;
+            return true;
+        }
+        read_more();
+    }
+}
+
+bool FqBulkReader::read(Rec& r) {  // FqReader::read, src/fqreader.cpp:160-195
+    err_.clear();
+    if (at_end(pos_)) return false;
+    size_t x = pos_, e = 0, nx = 0;
+    line(x, e, nx);
+    for (;;) {  // skip to a line that starts with '@' (src/fqreader.cpp:169-171)
+        const bool empty = e == x;
+        if ((empty && !at_end(nx)) || (!empty && text_->data()[x] != '@')) {
+            x = nx;
+            line(x, e, nx);
+        } else {
+            break;
+        }
+    }
+    if (e == x) {
+        pos_ = nx;
+        return false;
+    }
+    const size_t name_off = x, name_len = e - x;
+    size_t ls[3], le[3], ln[3];
+    size_t y = nx;
+    for (int k = 0; k < 3; ++k) {
+        line(y, le[k], ln[k]);
+        ls[k] = y;
+        y = ln[k];
+    }
+    pos_ = y;
+    const size_t seq_len = le[0] - ls[0], strand_len = le[1] - ls[1], qual_len = le[2] - ls[2];
+    char* d = text_->data();
+    if (qual_len != seq_len) {
+        const char* z = "";
+        auto str = [&](size_t a, size_t b) { return a < text_->size() ? std::string(d + a, std::min(b, text_->size()) - a) : std::string(z); };
+        err_ = "Error: base sequnce and quality sequence have different length: \n" + str(name_off, e) + "\n" +
+               str(ls[0], le[0]) + "\n" + str(ls[2], le[2]) + "\n" + str(ls[1], le[1]) + "\n";
+        return false;
+    }
+    if (phred64_) {  // Read::convertPhread64To33, src/read.h:71-75 (char arithmetic)
+        char* q = d + ls[2];
+        for (size_t i = 0; i < qual_len; ++i) q[i] = (char)std::max(33, (int)q[i] - (64 - 33));
+    }
+    r.off = name_off;
+    r.name_len = (uint32_t)name_len;
+    r.len = (uint32_t)seq_len;
+    r.strand_len = (uint32_t)strand_len;
+    r.gap[0] = (uint8_t)(ls[0] - e);
+    r.gap[1] = (uint8_t)(ls[1] - le[0]);
+    r.gap[2] = (uint8_t)(ls[2] - le[1]);
     return true;
 }
 
@@ -290,6 +439,7 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
 void Pack::clear() {
     n = 0;
     stride = 0;
+    shared_text = false;
     for (int m = 0; m < 2; ++m) {
         text[m].clear();
         rec[m].clear();
@@ -349,8 +499,8 @@ void pack_tiles(Pack& pk, Pool* pool) {
                 const int i1 = std::min(pk.n, (t + 1) * FQ_TILE_READS);
                 for (int i = t * FQ_TILE_READS; i < i1; ++i) {
                     const Rec& r = pk.rec[m][(size_t)i];
-                    const char* s = pk.text[m].data() + r.off + r.name_len;
-                    const char* q = s + r.len + r.strand_len;
+                    const char* s = pk.arena(m) + r.seq_off();
+                    const char* q = pk.arena(m) + r.qual_off();
                     for (uint32_t j = 0; j < r.len; j += FQ_CHUNK) {
                         const size_t k = std::min<size_t>(FQ_CHUNK, r.len - j);
                         const size_t o = fq_batch_offset(pk.stride, i, (int32_t)j);
@@ -366,32 +516,32 @@ void pack_tiles(Pack& pk, Pool* pool) {
 }
 
 // ---- PackReader ----
-PackReader::PackReader(const std::string& in1, const std::string& in2, bool interleaved, bool phred64)
-    : r1_(in1, phred64), paired_(!in2.empty() || interleaved), interleaved_(interleaved) {
-    if (!in2.empty() && !interleaved) {
-        r2_own_.reset(new FqReader(in2, phred64));
-        r2_ = r2_own_.get();
-    } else if (interleaved) {
-        r2_ = &r1_;
-    }
+PackReader::PackReader(const std::string& in1, const std::string& in2, bool interleaved, bool phred64, int buf_size)
+    : r1_(in1, phred64, buf_size), paired_(!in2.empty() || interleaved), interleaved_(interleaved) {
+    if (!in2.empty() && !interleaved) r2_.reset(new FqBulkReader(in2, phred64, buf_size));
 }
 
 namespace {
-size_t read_mate(FqReader& r, Pack& pk, int m, size_t max_n) {
+size_t read_mate(FqBulkReader& r, Pack& pk, int m, size_t max_n) {
+    r.begin(pk.text[m]);
     Rec rc;
     size_t k = 0;
-    while (k < max_n && r.read(pk.text[m], rc)) {
+    pk.rec[m].reserve(max_n);
+    while (k < max_n && r.read(rc)) {
         pk.rec[m].push_back(rc);
         ++k;
     }
+    r.end();
     return k;
 }
 }  // namespace
 
 bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     if (done_) return false;
+    const auto t0 = std::chrono::steady_clock::now();
     pk.clear();
     pk.paired = paired_;
+    pk.shared_text = false;
     size_t n = 0;
     if (!paired_) {
         n = read_mate(r1_, pk, 0, max_n);
@@ -400,12 +550,14 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
             if (!r1_.error().empty()) std::cerr << r1_.error();
         }
     } else if (interleaved_) {  // FqReaderPair over one file: mate 1, then mate 2
+        pk.shared_text = true;
+        r1_.begin(pk.text[0]);
         Rec a, b;
         while (n < max_n) {
             // FqReaderPair::read (src/fqreader.cpp:254-267) reads mate 2 even when mate 1 failed
-            const bool ok_a = r1_.read(pk.text[0], a);
+            const bool ok_a = r1_.read(a);
             const std::string err_a = ok_a ? std::string() : r1_.error();
-            const bool ok_b = r1_.read(pk.text[1], b);
+            const bool ok_b = r1_.read(b);
             if (!ok_a || !ok_b) {
                 done_ = true;
                 std::cerr << err_a;
@@ -416,6 +568,7 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
             pk.rec[1].push_back(b);
             ++n;
         }
+        r1_.end();
     } else {
         // One thread per mate.  FqReaderPair::read (src/fqreader.cpp:254-267) reads mate 1, then
         // mate 2 (always both), and stops once either failed: the pair count is the shorter run,
@@ -436,7 +589,10 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     }
     if (n == 0) return false;
     pk.n = (int)n;
+    const auto t1 = std::chrono::steady_clock::now();
     pack_tiles(pk, pool);
+    parse_s += std::chrono::duration<double>(t1 - t0).count();
+    tiles_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     pk.seq_no = packs_++;
     reads_ += (uint64_t)pk.n * (paired_ ? 2 : 1);
     return true;

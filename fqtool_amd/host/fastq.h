@@ -83,15 +83,23 @@ class PodBuf {
     ByteBuf b_;
 };
 
-// One record's fields in a mate's text arena: name at off, then seq (len bytes), strand, qual.
+// One record's fields in a mate's text arena: name at off, then seq (len bytes), strand, qual,
+// each field followed by gap[k] bytes of line terminator (0 when the fields were copied back to
+// back; 1 or 2 -- "\r\n", or an empty line the reference's getLine folds into the terminator --
+// when the arena holds the file's own bytes).
 struct Rec {
     uint64_t off;
     uint32_t name_len, strand_len, len;
+    uint8_t gap[3];
+    size_t seq_off() const { return off + name_len + gap[0]; }
+    size_t strand_off() const { return seq_off() + len + gap[1]; }
+    size_t qual_off() const { return strand_off() + strand_len + gap[2]; }
 };
 
 class FqReader {
    public:
-    FqReader(const std::string& path, bool phred64);
+    // buf_size: the reference's read buffer (1 MiB, src/fqreader.cpp:10); smaller only in tests
+    FqReader(const std::string& path, bool phred64, int buf_size = 1 << 20);
     ~FqReader();
     FqReader(const FqReader&) = delete;
     FqReader& operator=(const FqReader&) = delete;
@@ -109,11 +117,53 @@ class FqReader {
     gzFile gz_ = nullptr;
     FILE* fp_ = nullptr;
     bool phred64_;
+    int buf_size_;
     std::vector<char> buf_;
     int len_ = 0, used_ = 0;
     bool eof_ = false;
     std::string err_;
     ByteBuf scratch_;  // the string overload's record
+};
+
+// The pack reader's FqReader: same records, errors and line semantics as FqReader (and the
+// reference), but zero copy: the file's bytes are read straight into the pack's text arena in
+// large blocks and records are located in place (Rec with gaps).  getLine's treatment of a '\n'
+// after a terminator depends on where the reference's 1 MiB read buffers end
+// (src/fqreader.cpp:90-150), so reads stay aligned to buf_size multiples of the stream and the
+// rule is evaluated on stream offsets.  Bytes read past the last record of a pack are carried
+// into the next pack's arena.
+class FqBulkReader {
+   public:
+    FqBulkReader(const std::string& path, bool phred64, int buf_size = 1 << 20);
+    ~FqBulkReader();
+    FqBulkReader(const FqBulkReader&) = delete;
+    FqBulkReader& operator=(const FqBulkReader&) = delete;
+    // start filling `text` (cleared by the caller): the carried bytes go first
+    void begin(ByteBuf& text);
+    // next record into the arena given to begin(); false at end of input or on a
+    // quality/sequence length mismatch (message in error())
+    bool read(Rec& r);
+    // the arena is done: unconsumed bytes are carried to the next begin()
+    void end();
+    const std::string& error() const { return err_; }
+
+   private:
+    bool line(size_t x, size_t& e, size_t& next);
+    bool at_end(size_t x) const { return eof_ && x >= text_->size(); }
+    bool skip_ok(uint64_t g) const;
+    void read_more();
+    gzFile gz_ = nullptr;
+    FILE* fp_ = nullptr;
+    bool phred64_;
+    uint64_t bsize_;
+    bool eof_ = false;
+    uint64_t total_ = 0;  // stream bytes read so far (the stream's size once eof_)
+    ByteBuf* text_ = nullptr;
+    uint64_t base_ = 0;   // stream offset of (*text_)[0]
+    size_t pos_ = 0;      // arena offset of the next unread line
+    std::string carry_;
+    uint64_t carry_off_ = 0;
+    std::string err_;
 };
 
 // Minimal fork-join pool: run(n, fn) calls fn(0..n-1) on the workers and the calling thread and
@@ -145,16 +195,18 @@ struct Pack {
     int stride = 0;
     bool paired = false;
     ByteBuf text[2];
+    bool shared_text = false;  // interleaved input: both mates' records in text[0]
     std::vector<Rec> rec[2];
     ByteBuf seq[2], qual[2];  // batch planes
     PodBuf<uint16_t> len[2];
     PodBuf<fq_read_result> res;  // engine records: n (SE) or 2n (PE)
     uint64_t seq_no = 0;
 
-    const char* name(int m, size_t i) const { return text[m].data() + rec[m][i].off; }
-    const char* seq_text(int m, size_t i) const { return name(m, i) + rec[m][i].name_len; }
-    const char* strand(int m, size_t i) const { return seq_text(m, i) + rec[m][i].len; }
-    const char* qual_text(int m, size_t i) const { return strand(m, i) + rec[m][i].strand_len; }
+    const char* arena(int m) const { return text[shared_text ? 0 : m].data(); }
+    const char* name(int m, size_t i) const { return arena(m) + rec[m][i].off; }
+    const char* seq_text(int m, size_t i) const { return arena(m) + rec[m][i].seq_off(); }
+    const char* strand(int m, size_t i) const { return arena(m) + rec[m][i].strand_off(); }
+    const char* qual_text(int m, size_t i) const { return arena(m) + rec[m][i].qual_off(); }
     void clear();
     fq_batch batch() const;
     fq_read_result* results() {  // sized for this pack
@@ -173,15 +225,16 @@ void pack_tiles(Pack& pk, Pool* pool);
 // Returns false when no record could be read.
 class PackReader {
    public:
-    PackReader(const std::string& in1, const std::string& in2, bool interleaved, bool phred64);
+    PackReader(const std::string& in1, const std::string& in2, bool interleaved, bool phred64,
+               int buf_size = 1 << 20);
     bool next(Pack& pk, size_t max_n, Pool* pool = nullptr);
     bool paired() const { return paired_; }
     uint64_t reads_seen() const { return reads_; }
+    double parse_s = 0, tiles_s = 0;  // time spent parsing records / filling batch planes
 
    private:
-    FqReader r1_;
-    FqReader* r2_ = nullptr;
-    std::unique_ptr<FqReader> r2_own_;
+    FqBulkReader r1_;
+    std::unique_ptr<FqBulkReader> r2_;
     bool paired_, interleaved_;
     bool done_ = false;
     uint64_t reads_ = 0, packs_ = 0;

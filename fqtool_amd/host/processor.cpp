@@ -456,11 +456,20 @@ int run_tool(int argc, char** argv) {
         Queue<std::unique_ptr<Pack>> packs(2), done(2), spare((size_t)n_packs);
         for (int i = 0; i < n_packs; ++i) spare.push(std::unique_ptr<Pack>(new Pack(true)));
         std::exception_ptr reader_err, format_err;
+        double parse_s = 0, tiles_s = 0, spare_wait_s = 0;
         std::thread reader([&] {
             try {
                 PackReader pr(o.in1, o.in2, o.interleaved, o.phred64);
                 std::unique_ptr<Pack> pk;
-                while (spare.pop(pk) && pr.next(*pk, pack_n, &pool)) packs.push(std::move(pk));
+                for (;;) {
+                    const auto w0 = std::chrono::steady_clock::now();
+                    if (!spare.pop(pk)) break;
+                    spare_wait_s += since(w0);
+                    if (!pr.next(*pk, pack_n, &pool)) break;
+                    packs.push(std::move(pk));
+                }
+                parse_s = pr.parse_s;
+                tiles_s = pr.tiles_s;
             } catch (...) {
                 reader_err = std::current_exception();
             }
@@ -552,7 +561,9 @@ int run_tool(int argc, char** argv) {
         js << rep.dump(4);
         log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s), wall " +
             std::to_string(since(t0)) + " s, engine submit/wait " + std::to_string(engine_s) + " s; pre-pass " +
-            std::to_string(prepass_s) + " s, format " + std::to_string(format_s) + " s; JSON report " + o.json_file +
+            std::to_string(prepass_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +
+            " s, tiles " + std::to_string(tiles_s) + " s, reader waiting " + std::to_string(spare_wait_s) +
+            " s; JSON report " + o.json_file +
             " (no HTML report in this build)");
     } catch (const std::exception& e) {
         std::cerr << "ERROR: " << e.what() << std::endl;

@@ -57,6 +57,13 @@ int fqh_session_add_acc(fqh_session* s, const uint64_t* acc, int max_cycles);
 char* fqh_session_finish(fqh_session* s);
 void fqh_session_close(fqh_session* s);
 
+/* Records of a FASTQ file as the tool's pack reader parses them (bulk = 1: the zero-copy pack
+ * reader, packs of `pack_n` records; bulk = 0: the line-by-line FqReader), with read buffers of
+ * `buf_size` bytes instead of the reference's 1 MiB (tests cross-check both readers on buffer
+ * boundaries).  Returns a malloc'd listing: one "name\tseq\tstrand\tqual\n" line per record,
+ * then the reader's error text, if any (fqh_free). */
+char* fqh_debug_records(const char* path, int bulk, int buf_size, int pack_n, int phred64);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,8 +70,5 @@ class OracleRunner:
     def parity_sample(self, target):
         return None  # the oracle is the engine here: nothing to check against
 
-    def cpu_baseline(self, pairs):
-        return None
-
     def close(self):
         pass
