@@ -201,16 +201,15 @@ char* fqh_debug_records(const char* path, int bulk, int buf_size, int pack_n, in
             FqBulkReader r(path, phred64 != 0, buf_size);
             ByteBuf text;
             Rec rc;
+            std::vector<Rec> recs;
             for (bool more = true; more;) {
                 r.begin(text);
-                int k = 0;
-                while (k < pack_n && (more = r.read(rc))) {
-                    const char* t = text.data();
-                    put(t + rc.off, rc.name_len, t + rc.seq_off(), rc.len, t + rc.strand_off(), rc.strand_len,
-                        t + rc.qual_off(), rc.len);
-                    ++k;
-                }
-                r.end();
+                recs.clear();
+                while ((int)recs.size() < pack_n && (more = r.read(rc))) recs.push_back(rc);
+                const char* t = r.end();
+                for (const Rec& x : recs)
+                    put(t + x.off, x.name_len, t + x.seq_off(), x.len, t + x.strand_off(), x.strand_len, t + x.qual_off(),
+                        x.len);
             }
             out += r.error();
         } else {

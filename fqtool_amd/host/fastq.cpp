@@ -8,6 +8,9 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <emmintrin.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <exception>
 #include <iostream>
 #include <memory>
@@ -212,33 +215,59 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
         if (!gz_) throw std::runtime_error("Failed to open file: " + path);
         gzbuffer(gz_, 1 << 20);
         gzrewind(gz_);
-    } else {
-        fp_ = path == "/dev/stdin" ? stdin : std::fopen(path.c_str(), "rb");
-        if (!fp_) throw std::runtime_error("Failed to open file: " + path);
+        return;
+    }
+    fp_ = path == "/dev/stdin" ? stdin : std::fopen(path.c_str(), "rb");
+    if (!fp_) throw std::runtime_error("Failed to open file: " + path);
+    struct stat st;
+    if (fp_ != stdin && fstat(fileno(fp_), &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
+        // a regular file is mapped (private, so phred64 conversion writes stay in this process)
+        void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ | PROT_WRITE, MAP_PRIVATE, fileno(fp_), 0);
+        if (m != MAP_FAILED) {
+            madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
+            map_ = static_cast<char*>(m);
+            map_size_ = (size_t)st.st_size;
+            total_ = map_size_;
+            eof_ = true;
+        }
     }
 }
 
 FqBulkReader::~FqBulkReader() {
+    if (map_) munmap(map_, map_size_);
     if (gz_) gzclose(gz_);
     if (fp_ && fp_ != stdin) std::fclose(fp_);
 }
 
 void FqBulkReader::begin(ByteBuf& text) {
+    if (map_) {  // the mapping is the arena: offsets are file offsets, nothing is carried
+        text.clear();
+        text_ = nullptr;
+        base_ = 0;
+        tbase_ = pos_ >> 6;
+        indexed_ = tbase_ << 6;
+        return;
+    }
     text_ = &text;
     text.clear();
+    tbase_ = 0;
+    indexed_ = 0;
     base_ = carry_off_;
     if (!carry_.empty()) std::memcpy(text.extend(carry_.size()), carry_.data(), carry_.size());
     carry_.clear();
     pos_ = 0;
 }
 
-void FqBulkReader::end() {
-    if (!text_) return;
+const char* FqBulkReader::end() {
+    if (map_) return map_;
+    if (!text_) return nullptr;
     const size_t n = text_->size();
     if (pos_ < n) carry_.assign(text_->data() + pos_, n - pos_);
     else carry_.clear();
     carry_off_ = base_ + pos_;
+    const char* base = text_->data();
     text_ = nullptr;
+    return base;
 }
 
 // Reads up to the next buffer boundary past at least 4 MiB more (or to the end of the stream), so
@@ -267,6 +296,43 @@ void FqBulkReader::read_more() {
     if (got < want) eof_ = true;
 }
 
+// One SSE2 pass over new arena bytes: a bitmap of line terminators (word w of tidx_ covers arena
+// bytes [64 (tbase_ + w), +64)), so finding the end of a line is a few word scans.
+void FqBulkReader::index_to(size_t n) {
+    const char* d = dat();
+    const size_t w0 = indexed_ >> 6, w1 = (n + 63) >> 6;
+    if (tidx_.size() < w1 - tbase_) tidx_.resize(w1 - tbase_ + 4096);
+    const __m128i nl = _mm_set1_epi8('\n'), cr = _mm_set1_epi8('\r');
+    for (size_t w = w0; w < w1; ++w) {
+        const size_t base = w << 6;
+        uint64_t m = 0;
+        if (base + 64 <= n) {
+            for (int k = 0; k < 4; ++k) {
+                const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(d + base + 16 * k));
+                const uint32_t mk =
+                    (uint32_t)_mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(v, nl), _mm_cmpeq_epi8(v, cr)));
+                m |= (uint64_t)mk << (16 * k);
+            }
+        } else {
+            for (size_t i = base; i < n; ++i)
+                if (d[i] == '\n' || d[i] == '\r') m |= 1ull << (i - base);
+        }
+        tidx_[w - tbase_] = m;
+    }
+    indexed_ = n;
+}
+
+// first terminator in [x, n) (n <= indexed_), or n
+size_t FqBulkReader::next_term(size_t x, size_t n) const {
+    size_t w = x >> 6;
+    uint64_t bits = tidx_[w - tbase_] & (~0ull << (x & 63));
+    while (!bits) {
+        if (((++w) << 6) >= n) return n;
+        bits = tidx_[w - tbase_];
+    }
+    return std::min(n, (w << 6) + (size_t)__builtin_ctzll(bits));
+}
+
 // getLine's rule (src/fqreader.cpp:139-140): a '\n' right after a terminator at buffer index e is
 // folded into it iff e + 1 < len - 1, len = that buffer's length (all but the stream's last
 // buffer are full).
@@ -276,20 +342,24 @@ bool FqBulkReader::skip_ok(uint64_t g) const {
     return e + 2 < len;
 }
 
-// the line at arena offset x: [x, e), next line at `next`; reads more of the stream as needed.
-// Past the end of the stream every line is empty (the reference's getLine at EOF).
+// the line at arena offset x: [x, e), next line at `next`; indexes (and reads) more of the stream
+// as needed.  Past the end of the stream every line is empty (the reference's getLine at EOF).
 bool FqBulkReader::line(size_t x, size_t& e, size_t& next) {
     for (;;) {
-        const size_t n = text_->size();
-        if (x < n) {
-            const char* d = text_->data();
-            const size_t t = (size_t)(line_end(d + x, n - x) - d);
-            if (t < n) {
+        const size_t n = sz();
+        if (x < indexed_) {
+            const size_t t = next_term(x, indexed_);
+            if (t < indexed_) {
+                const char* d = dat();
                 e = t;
                 next = t + 1;
                 if (next < n && d[next] == '\n' && skip_ok(base_ + t)) ++next;
                 return true;
             }
+        }
+        if (indexed_ < n) {  // index the next few MiB (the mapping is not indexed all at once)
+            index_to(std::min(n, std::max(indexed_, x) + (4u << 20)));
+            continue;
         }
         if (eof_) {  // the last line has no terminator, or we are past the end: empty lines
             e = std::max(x, n);
@@ -307,7 +377,7 @@ bool FqBulkReader::read(Rec& r) {  // FqReader::read, src/fqreader.cpp:160-195
     line(x, e, nx);
     for (;;) {  // skip to a line that starts with '@' (src/fqreader.cpp:169-171)
         const bool empty = e == x;
-        if ((empty && !at_end(nx)) || (!empty && text_->data()[x] != '@')) {
+        if ((empty && !at_end(nx)) || (!empty && dat()[x] != '@')) {
             x = nx;
             line(x, e, nx);
         } else {
@@ -328,10 +398,10 @@ bool FqBulkReader::read(Rec& r) {  // FqReader::read, src/fqreader.cpp:160-195
     }
     pos_ = y;
     const size_t seq_len = le[0] - ls[0], strand_len = le[1] - ls[1], qual_len = le[2] - ls[2];
-    char* d = text_->data();
+    char* d = dat();
     if (qual_len != seq_len) {
-        const char* z = "";
-        auto str = [&](size_t a, size_t b) { return a < text_->size() ? std::string(d + a, std::min(b, text_->size()) - a) : std::string(z); };
+        const size_t n = sz();
+        auto str = [&](size_t a, size_t b) { return a < n ? std::string(d + a, std::min(b, n) - a) : std::string(); };
         err_ = "Error: base sequnce and quality sequence have different length: \n" + str(name_off, e) + "\n" +
                str(ls[0], le[0]) + "\n" + str(ls[2], le[2]) + "\n" + str(ls[1], le[1]) + "\n";
         return false;
@@ -439,7 +509,7 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
 void Pack::clear() {
     n = 0;
     stride = 0;
-    shared_text = false;
+    base[0] = base[1] = nullptr;
     for (int m = 0; m < 2; ++m) {
         text[m].clear();
         rec[m].clear();
@@ -531,7 +601,7 @@ size_t read_mate(FqBulkReader& r, Pack& pk, int m, size_t max_n) {
         pk.rec[m].push_back(rc);
         ++k;
     }
-    r.end();
+    pk.base[m] = r.end();
     return k;
 }
 }  // namespace
@@ -541,7 +611,6 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     const auto t0 = std::chrono::steady_clock::now();
     pk.clear();
     pk.paired = paired_;
-    pk.shared_text = false;
     size_t n = 0;
     if (!paired_) {
         n = read_mate(r1_, pk, 0, max_n);
@@ -550,7 +619,6 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
             if (!r1_.error().empty()) std::cerr << r1_.error();
         }
     } else if (interleaved_) {  // FqReaderPair over one file: mate 1, then mate 2
-        pk.shared_text = true;
         r1_.begin(pk.text[0]);
         Rec a, b;
         while (n < max_n) {
@@ -568,7 +636,7 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
             pk.rec[1].push_back(b);
             ++n;
         }
-        r1_.end();
+        pk.base[0] = pk.base[1] = r1_.end();
     } else {
         // One thread per mate.  FqReaderPair::read (src/fqreader.cpp:254-267) reads mate 1, then
         // mate 2 (always both), and stops once either failed: the pair count is the shorter run,
@@ -590,7 +658,7 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     if (n == 0) return false;
     pk.n = (int)n;
     const auto t1 = std::chrono::steady_clock::now();
-    pack_tiles(pk, pool);
+    if (!defer_tiles) pack_tiles(pk, pool);
     parse_s += std::chrono::duration<double>(t1 - t0).count();
     tiles_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     pk.seq_no = packs_++;

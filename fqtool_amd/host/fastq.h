@@ -143,13 +143,18 @@ class FqBulkReader {
     // next record into the arena given to begin(); false at end of input or on a
     // quality/sequence length mismatch (message in error())
     bool read(Rec& r);
-    // the arena is done: unconsumed bytes are carried to the next begin()
-    void end();
+    // the arena is done: unconsumed bytes are carried to the next begin(); returns the base
+    // the records' offsets refer to (the arena, or the file mapping)
+    const char* end();
     const std::string& error() const { return err_; }
 
    private:
     bool line(size_t x, size_t& e, size_t& next);
-    bool at_end(size_t x) const { return eof_ && x >= text_->size(); }
+    void index_to(size_t n);                 // terminator bitmap of arena bytes [indexed_, n)
+    size_t next_term(size_t x, size_t n) const;  // first '\r' / '\n' at or after x, or n
+    bool at_end(size_t x) const { return eof_ && x >= sz(); }
+    char* dat() const { return map_ ? map_ : text_->data(); }
+    size_t sz() const { return map_ ? map_size_ : text_->size(); }
     bool skip_ok(uint64_t g) const;
     void read_more();
     gzFile gz_ = nullptr;
@@ -163,6 +168,10 @@ class FqBulkReader {
     size_t pos_ = 0;      // arena offset of the next unread line
     std::string carry_;
     uint64_t carry_off_ = 0;
+    std::vector<uint64_t> tidx_;  // bit i of word w: arena byte 64 (tbase_ + w) + i is '\r' or '\n'
+    size_t tbase_ = 0, indexed_ = 0;
+    char* map_ = nullptr;  // a regular file is read through a private mapping (zero copy)
+    size_t map_size_ = 0;
     std::string err_;
 };
 
@@ -194,15 +203,15 @@ struct Pack {
     int n = 0;
     int stride = 0;
     bool paired = false;
-    ByteBuf text[2];
-    bool shared_text = false;  // interleaved input: both mates' records in text[0]
+    ByteBuf text[2];           // arenas of buffered (gzip / pipe) input
+    const char* base[2] = {nullptr, nullptr};  // what each mate's record offsets refer to
     std::vector<Rec> rec[2];
     ByteBuf seq[2], qual[2];  // batch planes
     PodBuf<uint16_t> len[2];
     PodBuf<fq_read_result> res;  // engine records: n (SE) or 2n (PE)
     uint64_t seq_no = 0;
 
-    const char* arena(int m) const { return text[shared_text ? 0 : m].data(); }
+    const char* arena(int m) const { return base[m]; }
     const char* name(int m, size_t i) const { return arena(m) + rec[m][i].off; }
     const char* seq_text(int m, size_t i) const { return arena(m) + rec[m][i].seq_off(); }
     const char* strand(int m, size_t i) const { return arena(m) + rec[m][i].strand_off(); }
@@ -231,6 +240,7 @@ class PackReader {
     bool paired() const { return paired_; }
     uint64_t reads_seen() const { return reads_; }
     double parse_s = 0, tiles_s = 0;  // time spent parsing records / filling batch planes
+    bool defer_tiles = false;         // next() leaves pack_tiles to the caller (another thread)
 
    private:
     FqBulkReader r1_;

@@ -457,9 +457,11 @@ int run_tool(int argc, char** argv) {
         for (int i = 0; i < n_packs; ++i) spare.push(std::unique_ptr<Pack>(new Pack(true)));
         std::exception_ptr reader_err, format_err;
         double parse_s = 0, tiles_s = 0, spare_wait_s = 0;
+        // (owned here, not by the reader thread: packs in flight point into its file mappings)
+        PackReader pr(o.in1, o.in2, o.interleaved, o.phred64);
+        pr.defer_tiles = true;  // the dispatcher fills the planes while the reader parses on
         std::thread reader([&] {
             try {
-                PackReader pr(o.in1, o.in2, o.interleaved, o.phred64);
                 std::unique_ptr<Pack> pk;
                 for (;;) {
                     const auto w0 = std::chrono::steady_clock::now();
@@ -469,7 +471,6 @@ int run_tool(int argc, char** argv) {
                     packs.push(std::move(pk));
                 }
                 parse_s = pr.parse_s;
-                tiles_s = pr.tiles_s;
             } catch (...) {
                 reader_err = std::current_exception();
             }
@@ -485,7 +486,7 @@ int run_tool(int argc, char** argv) {
                 while (done.pop(pk)) {
                     const auto f0 = std::chrono::steady_clock::now();
                     const fq_params p = o.to_params(eng.max_cycles);
-                    if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p);
+                    if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p, &pool);
                     PackOutput out;
                     format_pack(o, *pk, pk->res.data(), out, &pool);
                     format_s += since(f0);
@@ -520,6 +521,9 @@ int run_tool(int argc, char** argv) {
         try {
             std::unique_ptr<Pack> pk;
             while (packs.pop(pk)) {
+                const auto p0 = std::chrono::steady_clock::now();
+                pack_tiles(*pk, &pool);
+                tiles_s += since(p0);
                 int max1 = 0, max2 = 0;
                 for (uint16_t l : pk->len[0]) max1 = std::max(max1, (int)l);
                 if (paired)

@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <numeric>
+#include <string_view>
+#include <unordered_map>
 
 #include "fastq.h"
 
@@ -26,22 +28,28 @@ void HostAcc::add(const uint64_t* acc, int max_cycles) {
     }
 }
 
-void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_params& p) {
+void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_params& p, Pool* pool) {
     const int mates = pk.paired ? 2 : 1;
-    for (int i = 0; i < pk.n; ++i) {
-        for (int m = 0; m < mates; ++m) {
-            const fq_read_result& r = res[(size_t)i * mates + m];
-            if (!(r.flags & (FQ_RF_AD_OVERLAP | FQ_RF_AD_SEQ)) || r.ad_len == 0) continue;
-            std::string s;
-            if (r.flags & FQ_RF_AD_NEG) {
-                const uint8_t* ad = m ? p.adapter2 : p.adapter1;
-                s.assign(reinterpret_cast<const char*>(ad) + r.ad_pos, r.ad_len);
-            } else {
-                s.assign(pk.seq_text(m, (size_t)i) + r.ad_pos, r.ad_len);
+    const int parts = pool ? std::max(1, std::min(pool->size() * 2, (pk.n + 16383) / 16384)) : 1;
+    std::vector<std::unordered_map<std::string_view, size_t>> local((size_t)parts * 2);
+    auto work = [&](int k) {
+        const int i0 = (int)((int64_t)pk.n * k / parts), i1 = (int)((int64_t)pk.n * (k + 1) / parts);
+        for (int i = i0; i < i1; ++i) {
+            for (int m = 0; m < mates; ++m) {
+                const fq_read_result& r = res[(size_t)i * mates + m];
+                if (!(r.flags & (FQ_RF_AD_OVERLAP | FQ_RF_AD_SEQ)) || r.ad_len == 0) continue;
+                const char* s = (r.flags & FQ_RF_AD_NEG)
+                                    ? reinterpret_cast<const char*>(m ? p.adapter2 : p.adapter1) + r.ad_pos
+                                    : pk.seq_text(m, (size_t)i) + r.ad_pos;
+                ++local[(size_t)(2 * k + m)][std::string_view(s, r.ad_len)];
             }
-            ++(m ? r2 : r1)[s];
         }
-    }
+    };
+    if (pool) pool->run(parts, work);
+    else work(0);
+    for (int k = 0; k < parts; ++k)
+        for (int m = 0; m < mates; ++m)
+            for (const auto& kv : local[(size_t)(2 * k + m)]) (m ? r2 : r1)[std::string(kv.first)] += kv.second;
 }
 
 namespace {

@@ -42,9 +42,13 @@ class HostAcc {
 };
 
 // FilterResult's adapter string -> count maps (src/filterresult.cpp:138-177)
+// FilterResult's adapter-string counts (src/filterresult.cpp:138-177): each trimmed tail's text is
+// sliced from the pack; ranges of a pack are counted on the pool in hash maps of views into
+// the pack, then merged into the ordered maps the report walks.
+class Pool;
 struct AdapterCounts {
     std::map<std::string, size_t> r1, r2;
-    void add(const Pack& pk, const fq_read_result* res, const fq_params& p);
+    void add(const Pack& pk, const fq_read_result* res, const fq_params& p, Pool* pool = nullptr);
 };
 
 Json build_report(const Options& o, const HostAcc& acc, const AdapterCounts& ac);
