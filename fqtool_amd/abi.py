@@ -27,6 +27,12 @@ FQ_RF_AD_SEQ = 0x04
 FQ_RF_AD_NEG = 0x08
 FQ_RF_MERGED = 0x10
 FQ_RF_OVERLAP = 0x20
+FQ_RF_CORRECTED = 0x40
+FQ_RF_INDEX_FILTERED = 0x80
+FQ_BF_INDEX_FILTERED = 0x01
+FQ_ACC_TAIL_CORRECTED_READS = 0
+FQ_ACC_TAIL_CORRECTED_BASES = 1
+FQ_ACC_TAIL_WORDS = 16
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
@@ -68,7 +74,9 @@ class FqParams(ctypes.Structure):
         ("complexity_enabled", ctypes.c_int32),
         ("complexity_threshold", ctypes.c_double),
         ("max_cycles", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 7),
+        ("correction_enabled", ctypes.c_int32),
+        ("umi_front1", ctypes.c_int32), ("umi_front2", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 4),
     ]
 
 
@@ -77,6 +85,7 @@ class FqBatch(ctypes.Structure):
         ("n", ctypes.c_int32), ("stride", ctypes.c_int32),
         ("seq1", ctypes.c_void_p), ("qual1", ctypes.c_void_p), ("len1", ctypes.c_void_p),
         ("seq2", ctypes.c_void_p), ("qual2", ctypes.c_void_p), ("len2", ctypes.c_void_p),
+        ("flags", ctypes.c_void_p),
     ]
 
 
@@ -139,8 +148,12 @@ def acc_stats_offset(insert_size_max, max_cycles, k):
     return base + k * acc_stats_words(max_cycles)
 
 
-def acc_words(insert_size_max, max_cycles):
+def acc_tail_offset(insert_size_max, max_cycles):
     return acc_stats_offset(insert_size_max, max_cycles, 4)
+
+
+def acc_words(insert_size_max, max_cycles):
+    return acc_tail_offset(insert_size_max, max_cycles) + FQ_ACC_TAIL_WORDS
 
 
 def default_params(paired=True, max_cycles=256):

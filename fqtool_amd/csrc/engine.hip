@@ -24,6 +24,7 @@ struct Scratch {
 struct Slot {
     uint8_t* d_rows = nullptr;  // 4 planes of fq_batch_bytes(max_batch, max_stride)
     uint16_t* d_lens = nullptr;  // 2 x max_batch
+    uint8_t* d_flags = nullptr;  // max_batch per-pair FQ_BF_* flags
     fq_read_result* d_res = nullptr;
     Scratch scratch;
     hipEvent_t ev_in = nullptr, ev_kern = nullptr, ev_done = nullptr;
@@ -117,6 +118,7 @@ static void free_scratch(Scratch& sc) {
 static void free_slot(Slot& s) {
     if (s.d_rows) (void)hipFree(s.d_rows);
     if (s.d_lens) (void)hipFree(s.d_lens);
+    if (s.d_flags) (void)hipFree(s.d_flags);
     if (s.d_res) (void)hipFree(s.d_res);
     if (s.h_err) (void)hipHostFree(s.h_err);
     if (s.ev_in) (void)hipEventDestroy(s.ev_in);
@@ -131,6 +133,7 @@ static int alloc_slot(fq_engine* e, Slot& s) {
     const size_t rows = (size_t)4 * fq_batch_bytes(e->max_batch, e->max_stride);
     HIP_TRY(e, hipMalloc(&s.d_rows, rows));
     HIP_TRY(e, hipMalloc(&s.d_lens, (size_t)2 * e->max_batch * sizeof(uint16_t)));
+    HIP_TRY(e, hipMalloc(&s.d_flags, (size_t)e->max_batch + 1));
     HIP_TRY(e, hipMalloc(&s.d_res, (size_t)2 * e->max_batch * sizeof(fq_read_result)));
     HIP_TRY(e, hipHostMalloc((void**)&s.h_err, sizeof(int), hipHostMallocDefault));
     *s.h_err = 0;
@@ -227,7 +230,8 @@ static int grid_for(const fq_engine* e, int n) {
 static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStream_t s, Scratch& sc, bool timed,
                   bool sync_device_on_grow) {
     if (db.n <= 0) return FQ_OK;
-    if (e->fast) {
+    // per-pair flags (index filter) run on the general kernel
+    if (e->fast && !db.flags) {
         const size_t ntiles = ((size_t)db.n + 31) / 32 + 1;  // single-end 64-read tiles enter as two
         int rc = ensure_scratch(e, sc, ntiles, sync_device_on_grow);
         if (rc != FQ_OK) return rc;
@@ -306,7 +310,7 @@ int fq_engine_submit(fq_engine* e, const fq_batch* hb, fq_read_result* results, 
     const bool pe = e->p.paired;
     const size_t rowbytes = fq_batch_bytes(hb->n, hb->stride);
     const size_t plane = fq_batch_bytes(e->max_batch, e->max_stride);
-    fq_batch db;
+    fq_batch db{};
     db.n = hb->n;
     db.stride = hb->stride;
     db.seq1 = s.d_rows;
@@ -323,6 +327,10 @@ int fq_engine_submit(fq_engine* e, const fq_batch* hb, fq_read_result* results, 
         HIP_TRY(e, hipMemcpyAsync((void*)db.seq2, hb->seq2, rowbytes, hipMemcpyHostToDevice, e->s_in));
         HIP_TRY(e, hipMemcpyAsync((void*)db.qual2, hb->qual2, rowbytes, hipMemcpyHostToDevice, e->s_in));
         HIP_TRY(e, hipMemcpyAsync((void*)db.len2, hb->len2, (size_t)hb->n * 2, hipMemcpyHostToDevice, e->s_in));
+    }
+    if (hb->flags) {
+        db.flags = s.d_flags;
+        HIP_TRY(e, hipMemcpyAsync((void*)db.flags, hb->flags, (size_t)hb->n, hipMemcpyHostToDevice, e->s_in));
     }
     HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
     // kernels on the compute stream (one accumulator: the packs' kernels run in order)

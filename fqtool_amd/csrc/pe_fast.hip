@@ -1331,8 +1331,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 }  // namespace
 
 bool fq_pe_fast_supported(const fq_params& p) {
-    return p.insert_size_max <= 512 && p.insert_size_max >= 0 &&
-           (!p.merge_enabled || (p.paired && !p.complexity_enabled));
+    // -c and UMI trims run on the general kernel (fq_pack_kernel)
+    return p.insert_size_max <= 512 && p.insert_size_max >= 0 && !p.correction_enabled && p.umi_front1 == 0 &&
+           p.umi_front2 == 0 && (!p.merge_enabled || (p.paired && !p.complexity_enabled));
 }
 
 // profiling aid (tools/ablate.py --phases): read and clear the per-phase cycle totals

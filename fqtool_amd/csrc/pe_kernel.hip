@@ -26,16 +26,21 @@ struct Smem {
     uint32_t* hist;         // [4][clds][17]
     unsigned long long* c;  // small u64 counters, indexed like the global accumulator head
     unsigned long long* scal;  // [4][4] reads, length_sum, q20, q30
+    unsigned long long* tail;  // [4] the accumulator's tail counters (-c)
     int clds;                  // cycles privatised in LDS; later cycles go to global atomics
     unsigned long long* gcyc;  // global per-cycle block of stats 0 (+ k * stats words)
     size_t gstride;            // u64 words between the stats blocks
 };
 
+// u32 LDS words of the small u64 counters: head (even count), 16 Stats scalars, 4 tail counters
+__host__ __device__ inline int small_words(const fq_params& p) {
+    const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
+    return 2 * (((nsmall + 1) & ~1) + 16 + 4);
+}
+
 // cycles the LDS histograms can hold next to the small counters
 __host__ __device__ inline int lds_cycles(const fq_params& p) {
-    const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
-    const int small_words = 2 * (((nsmall + 1) & ~1) + 16);
-    const int cap = (160 * 1024 / 4 - small_words) / (4 * kRec);
+    const int cap = (160 * 1024 / 4 - small_words(p)) / (4 * kRec);
     return p.max_cycles < cap ? p.max_cycles : cap;
 }
 
@@ -141,6 +146,63 @@ __device__ inline void apply_adapter_seq(const Smem& sm, Row s, int st, int& n, 
     }
 }
 
+// writable byte i of a batch row (the device planes are the engine's own copy; -c edits them)
+__device__ __forceinline__ uint8_t* row_ptr(Row r, int i) {
+    const int j = r.off + i;
+    return const_cast<uint8_t*>(r.base) + (j >> 4) * (FQ_TILE_READS * FQ_CHUNK) + (j & 15);
+}
+
+// BaseCorrector::correctByOverlapAnalysis, reference src/basecorrector.cpp:14-70: mismatches of the
+// overlap where one side is >= Q30 and the other <= Q14 take the good side's base (complemented)
+// and quality.  Applied to the rows in place, so every later step (adapter by sequence, polyX,
+// merge, passFilter, post statistics) sees the corrected read as the reference does.  The
+// FilterResult correction matrix is reported only through its sum (CorrectedBases).
+__device__ inline void correct_pair(const Smem& sm, Row s1, Row q1, Row s2, Row q2, int n2, const Overlap& ov,
+                                    fq_read_result& r1, fq_read_result& r2) {
+    if (ov.diff == 0 || ov.diff > 5) return;
+    const int ol = ov.len;
+    const int start1 = max(0, ov.offset);
+    const int start2 = n2 - max(0, -ov.offset) - 1;
+    const int good = 33 + 30, bad = 33 + 14;  // util::num2qual(30), util::num2qual(14)
+    int corrected = 0;
+    bool c1 = false, c2 = false;
+    for (int i = 0; i < ol; ++i) {
+        const int p1 = start1 + i, p2 = start2 - i;
+        const uint8_t b1 = s1[p1], b2 = s2[p2];
+        if (b1 == comp(b2)) continue;
+        const int x1 = qv(q1, p1), x2 = qv(q2, p2);
+        if (x1 >= good && x2 <= bad) {
+            *row_ptr(s2, p2) = comp(b1);
+            *row_ptr(q2, p2) = (uint8_t)x1;
+            ++corrected;
+            c2 = true;
+        } else if (x2 >= good && x1 <= bad) {
+            *row_ptr(s1, p1) = comp(b2);
+            *row_ptr(q1, p1) = (uint8_t)x2;
+            ++corrected;
+            c1 = true;
+        }
+    }
+    if (!corrected) return;
+    lds_add64(&sm.tail[FQ_ACC_TAIL_CORRECTED_READS], (c1 && c2) ? 2ull : 1ull);
+    lds_add64(&sm.tail[FQ_ACC_TAIL_CORRECTED_BASES], (unsigned long long)corrected);
+    if (c1) r1.flags |= FQ_RF_CORRECTED;
+    if (c2) r2.flags |= FQ_RF_CORRECTED;
+    r2.m_len1 = (uint16_t)(int16_t)ov.offset;
+    r2.m_len2 = (uint16_t)ol;
+    r2.reserved = (uint16_t)n2;
+}
+
+// Read::trimFront(umi length + skip) of UmiProcessor::process (src/umiprocessor.cpp:28-62,
+// src/read.h:203-208): min(k, len - 1) bases (a read of length 0 is left alone)
+__device__ __forceinline__ int umi_cut(int k, int len) { return (k > 0 && len > 0) ? min(k, len - 1) : 0; }
+
+__device__ __forceinline__ fq_read_result index_filtered_result() {
+    fq_read_result r = make_result(true, 0, 0);
+    r.flags = FQ_RF_INDEX_FILTERED;
+    return r;
+}
+
 template <bool PAIRED>
 __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                       unsigned long long* __restrict__ acc, int* __restrict__ err,
@@ -151,11 +213,12 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
     Smem sm;
     sm.c = reinterpret_cast<unsigned long long*>(lds);
     sm.scal = sm.c + ((nsmall + 1) & ~1);
-    sm.hist = reinterpret_cast<uint32_t*>(sm.scal + 16);
+    sm.tail = sm.scal + 16;
+    sm.hist = reinterpret_cast<uint32_t*>(sm.tail + 4);
     sm.clds = lds_cycles(p);
     sm.gstride = acc_stats_words(C);
     sm.gcyc = acc + acc_stats_offset(p.insert_size_max, C, 0) + FQ_ST_CYCLES;
-    const int total_words = 2 * (((nsmall + 1) & ~1) + 16) + 4 * sm.clds * kRec;
+    const int total_words = small_words(p) + 4 * sm.clds * kRec;
     for (int i = threadIdx.x; i < total_words; i += blockDim.x) lds[i] = 0;
     __syncthreads();
 
@@ -174,8 +237,14 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
                 continue;
             }
             row_stat(sm, 0, C, s1, q1, l1, skew);  // src/seprocessor.cpp:298
+            if (b.flags && (b.flags[idx] & FQ_BF_INDEX_FILTERED)) {  // :304-307
+                if (res) store_result(&res[idx], index_filtered_result());
+                continue;
+            }
+            const int u = umi_cut(p.umi_front1, l1);  // :309-311
             int st = 0, n = 0;
-            bool nn = trim_and_cut(p, s1, q1, l1, p.trim_front1, p.trim_tail1, st, n);
+            bool nn = trim_and_cut(p, s1 + u, q1 + u, l1 - u, p.trim_front1, p.trim_tail1, st, n);
+            st += u;
             fq_read_result rr = make_result(nn, st, n);
             if (nn && p.polyg_enabled) apply_polyg(p, sm, s1, st, n);
             if (nn && p.adapter_trimming && p.adapter1_len > 0) apply_adapter_seq(sm, s1, st, n, p.adapter1, p.adapter1_len, rr);
@@ -199,9 +268,19 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
         }
         row_stat(sm, 0, C, s1, q1, l1, skew);  // src/peprocessor.cpp:276-277
         row_stat(sm, 1, C, s2, q2, l2, skew);
+        if (b.flags && (b.flags[idx] & FQ_BF_INDEX_FILTERED)) {  // :283-286
+            if (res) {
+                store_result(&res[2 * (size_t)idx], index_filtered_result());
+                store_result(&res[2 * (size_t)idx + 1], index_filtered_result());
+            }
+            continue;
+        }
+        const int u1 = umi_cut(p.umi_front1, l1), u2 = umi_cut(p.umi_front2, l2);  // :288-290
         int st1 = 0, n1 = 0, st2 = 0, n2 = 0;  // :292-293
-        const bool nn1 = trim_and_cut(p, s1, q1, l1, p.trim_front1, p.trim_tail1, st1, n1);
-        const bool nn2 = trim_and_cut(p, s2, q2, l2, p.trim_front2, p.trim_tail2, st2, n2);
+        const bool nn1 = trim_and_cut(p, s1 + u1, q1 + u1, l1 - u1, p.trim_front1, p.trim_tail1, st1, n1);
+        const bool nn2 = trim_and_cut(p, s2 + u2, q2 + u2, l2 - u2, p.trim_front2, p.trim_tail2, st2, n2);
+        st1 += u1;
+        st2 += u2;
         fq_read_result r1 = make_result(nn1, st1, n1), r2 = make_result(nn2, st2, n2);
         const bool both = nn1 && nn2;
         if (both && p.polyg_enabled) {  // :295-299
@@ -214,6 +293,7 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
             if (ov.overlapped) isize = ov.offset > 0 ? n1 + n2 - ov.len : ov.len;
             if (isize > p.insert_size_max) isize = p.insert_size_max;
             lds_add64(&sm.c[FQ_ACC_INSERT + isize], 1ull);
+            if (p.correction_enabled) correct_pair(sm, s1 + st1, q1 + st1, s2 + st2, q2 + st2, n2, ov, r1, r2);  // :310-312
             if (p.adapter_trimming) {
                 const int ol = ov.len;  // AdapterTrimmer::trimByOverlapAnalysis, src/adaptertrimmer.cpp:14-27
                 if (ov.diff <= 5 && ov.overlapped && ov.offset < 0 && ol > n1 / 3) {
@@ -362,6 +442,10 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
     }
     const size_t st_base = acc_stats_offset(p.insert_size_max, C, 0);
     const size_t st_words = acc_stats_words(C);
+    if (threadIdx.x < 4) {
+        unsigned long long v = sm.tail[threadIdx.x];
+        if (v) atomicAdd(&acc[st_base + 4 * st_words + threadIdx.x], v);
+    }
     if (threadIdx.x < 16) {
         const int k = threadIdx.x >> 2, f = threadIdx.x & 3;
         unsigned long long v = sm.scal[threadIdx.x];
@@ -386,8 +470,7 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
 }  // namespace
 
 size_t fq_pack_kernel_lds_bytes(const fq_params& p) {
-    const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
-    return (size_t)(2 * (((nsmall + 1) & ~1) + 16) + 4 * lds_cycles(p) * kRec) * sizeof(uint32_t);
+    return (size_t)(small_words(p) + 4 * lds_cycles(p) * kRec) * sizeof(uint32_t);
 }
 
 hipError_t fq_launch_pack_kernel(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,

@@ -141,6 +141,7 @@ int fqh_session_next(fqh_session* s, int max_n, fq_batch* out) {
     try {
         s->pk = Pack();
         if (!s->reader->next(s->pk, (size_t)max_n, s->pool.get())) return 0;
+        prepare_pack(s->o, s->pk, s->pool.get());
         *out = s->pk.batch();
         return 1;
     } catch (const std::exception& e) {
@@ -154,6 +155,7 @@ int fqh_session_next(fqh_session* s, int max_n, fq_batch* out) {
 int fqh_session_consume(fqh_session* s, const fq_read_result* res, int max_cycles) {
     try {
         const fq_params p = s->o.to_params(max_cycles);
+        apply_corrections(s->o, s->pk, res, s->pool.get());
         if (s->o.adapter_trimming) s->ac.add(s->pk, res, p);
         PackOutput out;
         format_pack(s->o, s->pk, res, out, s->pool.get());

@@ -517,10 +517,14 @@ void Pack::clear() {
         qual[m].clear();
         len[m].clear();
     }
+    fix.clear();
+    fix_arena.clear();
+    flags.clear();
+    use_flags = false;
 }
 
 fq_batch Pack::batch() const {
-    fq_batch b;
+    fq_batch b{};
     b.n = n;
     b.stride = stride;
     b.seq1 = reinterpret_cast<const uint8_t*>(seq[0].data());
@@ -529,6 +533,7 @@ fq_batch Pack::batch() const {
     b.seq2 = paired ? reinterpret_cast<const uint8_t*>(seq[1].data()) : nullptr;
     b.qual2 = paired ? reinterpret_cast<const uint8_t*>(qual[1].data()) : nullptr;
     b.len2 = paired ? len[1].data() : nullptr;
+    b.flags = use_flags ? flags.data() : nullptr;
     return b;
 }
 

@@ -199,6 +199,7 @@ struct Pack {
         : seq{ByteBuf(pinned), ByteBuf(pinned)},
           qual{ByteBuf(pinned), ByteBuf(pinned)},
           len{PodBuf<uint16_t>(pinned), PodBuf<uint16_t>(pinned)},
+          flags(pinned),
           res(pinned) {}
     int n = 0;
     int stride = 0;
@@ -208,14 +209,27 @@ struct Pack {
     std::vector<Rec> rec[2];
     ByteBuf seq[2], qual[2];  // batch planes
     PodBuf<uint16_t> len[2];
+    PodBuf<uint8_t> flags;       // per-pair FQ_BF_* flags (index filter), sent when use_flags
+    bool use_flags = false;
     PodBuf<fq_read_result> res;  // engine records: n (SE) or 2n (PE)
     uint64_t seq_no = 0;
 
+    // -c: pairs whose bases the engine corrected read their seq/qual from a corrected copy
+    // (fix[i] -> seq1 qual1 seq2 qual2 back to back; nullptr = the original text)
+    std::vector<const char*> fix;
+    std::vector<std::string> fix_arena;
+
     const char* arena(int m) const { return base[m]; }
     const char* name(int m, size_t i) const { return arena(m) + rec[m][i].off; }
-    const char* seq_text(int m, size_t i) const { return arena(m) + rec[m][i].seq_off(); }
+    const char* seq_text(int m, size_t i) const {
+        if (!fix.empty() && fix[i]) return fix[i] + (m ? 2 * (size_t)rec[0][i].len : 0);
+        return arena(m) + rec[m][i].seq_off();
+    }
     const char* strand(int m, size_t i) const { return arena(m) + rec[m][i].strand_off(); }
-    const char* qual_text(int m, size_t i) const { return arena(m) + rec[m][i].qual_off(); }
+    const char* qual_text(int m, size_t i) const {
+        if (!fix.empty() && fix[i]) return fix[i] + (m ? 2 * (size_t)rec[0][i].len + rec[1][i].len : rec[0][i].len);
+        return arena(m) + rec[m][i].qual_off();
+    }
     void clear();
     fq_batch batch() const;
     fq_read_result* results() {  // sized for this pack

@@ -8,6 +8,7 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <functional>
 #include <map>
 #include <set>
@@ -83,12 +84,11 @@ Table make_table(Options& o) {
     t.add({"--phred64"}, Kind::Flag, &o.phred64, "input fastq is phred64");
     range(t.add({"-z"}, Kind::Int, &o.compression, "gzip output compress level"), 1, 9);
     t.add({"--in_fq_interleaved"}, Kind::Flag, &o.interleaved, "input fastq interleaved").excludes = {"-I"};
-    // ---- duplication (outside the hot-path scope)
-    Spec& dup = t.add({"-d"}, Kind::Flag, &t.dummy_bool, "enable duplication analysis");
-    dup.unsupported = true;
-    Spec& dk = range(t.add({"--dup_ana_key_len"}, Kind::Int, &t.dummy_int, "duplication analysis key length"), 12, 31);
+    // ---- duplication
+    t.add({"-d"}, Kind::Flag, &o.dup, "enable duplication analysis");
+    Spec& dk = range(t.add({"--dup_ana_key_len"}, Kind::Int, &o.dup_keylen, "duplication analysis key length"), 12, 31);
     dk.needs = {"-d"};
-    Spec& dh = range(t.add({"--dup_ana_hist_size"}, Kind::Int, &t.dummy_int, "duplicate analysis hist size"), 1, 10000);
+    Spec& dh = range(t.add({"--dup_ana_hist_size"}, Kind::Int, &o.dup_hist_size, "duplicate analysis hist size"), 1, 10000);
     dh.needs = {"-d"};
     // ---- adapter
     t.add({"-a"}, Kind::Flag, &o.adapter_trimming, "enable adapter trimming");
@@ -153,30 +153,30 @@ Table make_table(Options& o) {
     t.add({"-y"}, Kind::Flag, &o.complexity_filter, "enable low complexity filter");
     range(t.add({"-Y"}, Kind::Double, &o.complexity_threshold, "min complexity required for a read"), 0, 1).needs = {
         "-y"};
-    // ---- index filtering (outside scope)
-    t.add({"--enable_index_filter"}, Kind::Flag, &t.dummy_bool, "enable index filtering").unsupported = true;
-    Spec& i1 = t.add({"--index1_file"}, Kind::Str, &t.dummy_str, "index1 file to filter");
+    // ---- index filtering
+    t.add({"--enable_index_filter"}, Kind::Flag, &o.index_filter, "enable index filtering");
+    Spec& i1 = t.add({"--index1_file"}, Kind::Str, &o.index1_file, "index1 file to filter");
     i1.existing_file = true;
     i1.needs = {"--enable_index_filter"};
-    Spec& i2 = t.add({"--index2_file"}, Kind::Str, &t.dummy_str, "index2 file to filetr");
+    Spec& i2 = t.add({"--index2_file"}, Kind::Str, &o.index2_file, "index2 file to filetr");
     i2.existing_file = true;
     i2.needs = {"--enable_index_filter"};
-    range(t.add({"--max_diff_for_match"}, Kind::Int, &t.dummy_int, "max ed to validate index matcha"), 0, 10).needs = {
+    range(t.add({"--max_diff_for_match"}, Kind::Int, &o.index_threshold, "max ed to validate index matcha"), 0, 10).needs = {
         "--enable_index_filter"};
-    // ---- base correction (outside scope) + overlap parameters
-    t.add({"-c"}, Kind::Flag, &t.dummy_bool, "enable base correction in PE reads").unsupported = true;
+    // ---- base correction + overlap parameters
+    t.add({"-c"}, Kind::Flag, &o.correction, "enable base correction in PE reads");
     range(t.add({"--min_overlap_len"}, Kind::Int, &o.overlap_require, "min overlap length needed for overlap analysis"),
           0, 1000);
     range(t.add({"--max_diff_for_overlap"}, Kind::Int, &o.overlap_diff_limit, "max ed to validate overlap"), 0, 10);
-    // ---- UMI (outside scope)
-    t.add({"-u"}, Kind::Flag, &t.dummy_bool, "enable UMI preprocess").unsupported = true;
-    range(t.add({"--umi_location"}, Kind::Int, &t.dummy_int, "0[none]1[index1]2[index2]3[read1]4[read2]5[perindex]6[perread]"),
+    // ---- UMI
+    t.add({"-u"}, Kind::Flag, &o.umi, "enable UMI preprocess");
+    range(t.add({"--umi_location"}, Kind::Int, &o.umi_location, "0[none]1[index1]2[index2]3[read1]4[read2]5[perindex]6[perread]"),
           1, 6)
         .needs = {"-u"};
-    range(t.add({"--umi_length"}, Kind::Int, &t.dummy_int, "umi length"), 0, 1000).needs = {"-u"};
-    range(t.add({"--umi_skip_length"}, Kind::Int, &t.dummy_int, "bases to skip after umi"), 0, 1000).needs = {"-u"};
-    t.add({"--umi_drop_comment"}, Kind::Flag, &t.dummy_bool, "drop other comment information").needs = {"-u"};
-    t.add({"--umi_not_trim"}, Kind::Flag, &t.dummy_bool, "do not trim reads").needs = {"-u"};
+    range(t.add({"--umi_length"}, Kind::Int, &o.umi_length, "umi length"), 0, 1000).needs = {"-u"};
+    range(t.add({"--umi_skip_length"}, Kind::Int, &o.umi_skip, "bases to skip after umi"), 0, 1000).needs = {"-u"};
+    t.add({"--umi_drop_comment"}, Kind::Flag, &o.umi_drop_comment, "drop other comment information").needs = {"-u"};
+    t.add({"--umi_not_trim"}, Kind::Flag, &o.umi_not_trim, "do not trim reads").needs = {"-u"};
     // ---- ORA / k-mer (outside scope)
     t.add({"--ora"}, Kind::Flag, &t.dummy_bool, "enable ORA").unsupported = true;
     range(t.add({"--ora_sample"}, Kind::Int, &t.dummy_int, "ORA sampling steps"), 1, 10000).needs = {"--ora"};
@@ -186,16 +186,15 @@ Table make_table(Options& o) {
     t.add({"-J"}, Kind::Str, &o.json_file, "json format report file");
     t.add({"-H"}, Kind::Str, &o.html_file, "html format report file");
     range(t.add({"-w"}, Kind::Int, &o.threads, "worker thread number"), 1, 16);
-    // ---- split (outside scope)
-    Spec& sfn = t.add({"-s"}, Kind::Flag, &t.dummy_bool, "split output by file number");
+    // ---- split (--digits_file_name sets Options::digits, which the split writers never read:
+    //      they use SplitOptions::digits = 4, src/threadconfig.cpp:91-96)
+    Spec& sfn = t.add({"-s"}, Kind::Flag, &o.split_by_number, "split output by file number");
     sfn.excludes = {"-m"};
-    sfn.unsupported = true;
-    t.add({"--split_file_number"}, Kind::Int, &t.dummy_int, "total split output file number").needs = {"-s"};
-    Spec& sln = t.add({"-S"}, Kind::Flag, &t.dummy_bool, "max line of each output file");
+    t.add({"--split_file_number"}, Kind::Int, &o.split_number, "total split output file number").needs = {"-s"};
+    Spec& sln = t.add({"-S"}, Kind::Flag, &o.split_by_lines, "max line of each output file");
     sln.excludes = {"-s", "-m"};
-    sln.unsupported = true;
-    t.add({"--splie_file_line"}, Kind::SizeT, &t.dummy_size, "split output file line limit").needs = {"-S"};
-    range(t.add({"--digits_file_name"}, Kind::Int, &t.dummy_int, "digits for sequential output filename"), 1, 10);
+    t.add({"--splie_file_line"}, Kind::SizeT, &o.split_size, "split output file line limit").needs = {"-S"};
+    range(t.add({"--digits_file_name"}, Kind::Int, &o.digits, "digits for sequential output filename"), 1, 10);
     range(t.add({"--max_packs_in_repo"}, Kind::SizeT, &o.max_packs_in_repo, "max packs in repo"), 1, 1000000);
     range(t.add({"--max_item_in_pack"}, Kind::SizeT, &o.max_reads_in_pack, "max read/pairs in pack"), 1, 1000000);
     range(t.add({"--max_packs_in_mem"}, Kind::SizeT, &o.max_packs_in_mem, "max packs in memory"), 1, 1000000);
@@ -413,11 +412,48 @@ Options parse_cli(int argc, char** argv) {
     return o;
 }
 
+namespace {
+
+// Options::makeListFromFileByLine, src/options.cpp:92-104 (util::strip's result is discarded
+// there, so lines are taken as they are)
+std::vector<std::string> index_list(const std::string& file) {
+    std::vector<std::string> out;
+    std::ifstream in(file);
+    std::string line;
+    while (std::getline(in, line)) {
+        if (line.find_first_not_of("ATCG") != std::string::npos)
+            throw CliError("processing " + file + ", each line should be one index, which can only contain A/T/C/G", 255);
+        out.push_back(line);
+    }
+    return out;
+}
+
+// util::validFile, src/util.h:311-318
+void valid_file(const std::string& path) {
+    struct stat st;
+    if (stat(path.c_str(), &st) == 0 && S_ISDIR(st.st_mode)) throw CliError("this is not a file path!", 255);
+    if (!is_file(path)) throw CliError("file does not exist", 255);
+}
+
+}  // namespace
+
 void Options::update(int argc, char** argv) {
     // src/options.cpp:24-58
     low_qual_limit += 33;
     if (adapter_trimming && adapter1.empty() && adapter2.empty() && paired()) detect_pe_adapter = true;
+    if (index_filter && !(index1_file.empty() && index2_file.empty())) {  // Options::initIndexFilter, :73-90
+        if (!index1_file.empty()) {
+            valid_file(index1_file);
+            blacklist1 = index_list(index1_file);
+        }
+        if (!index2_file.empty()) {
+            valid_file(index2_file);
+            blacklist2 = index_list(index2_file);
+        }
+    }
     low_qual_base_limit = (int)(low_qual_ratio * est_seq_len1);  // est_seq_len1 is still 151 here
+    if (umi && (umi_location == 3 || umi_location == 4 || umi_location == 6) && umi_length == 0)
+        throw CliError("umi length can not be zero if it's in read1/2", 255);
     std::transform(polyx_chars.begin(), polyx_chars.end(), polyx_chars.begin(),
                    [](unsigned char c) { return (char)std::toupper(c); });
     command.clear();
@@ -518,6 +554,9 @@ fq_params Options::to_params(int max_cycles) const {
     p.complexity_enabled = complexity_filter;
     p.complexity_threshold = complexity_threshold;
     p.max_cycles = max_cycles;
+    p.correction_enabled = correction && paired();
+    p.umi_front1 = umi_front(0);  // UmiProcessor::process, src/umiprocessor.cpp:28-62
+    p.umi_front2 = umi_front(1);
     return p;
 }
 

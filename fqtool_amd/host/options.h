@@ -2,9 +2,9 @@
 //
 // Mirrors the reference's Options tree (src/options.h:15-386), its CLI (src/main.cpp:18-120,
 // CLI11 1.7.1 semantics: bool flags reset to false at registration, range checks, needs /
-// excludes), and Options::update / validate (src/options.cpp:24-71).  Options outside the
-// hot-path scope (duplication, UMI, index filter, base correction, ORA, k-mer, split output)
-// are parsed and rejected with a clear message instead of being silently ignored.
+// excludes), and Options::update / validate (src/options.cpp:24-71).  ORA and k-mer analysis
+// (outside this build's scope) are parsed and rejected with a clear message instead of being
+// silently ignored.
 #pragma once
 
 #include <cstdint>
@@ -52,6 +52,27 @@ struct Options {
     double avg_qual = 0.0;
     int min_len = 15, max_len = 0;
     double complexity_threshold = 0.3;
+    // base correction (-c), UMI (-u), index filter, duplication (-d), split (-s / -S)
+    bool correction = false;
+    bool umi = false, umi_drop_comment = false, umi_not_trim = false;
+    int umi_location = 0, umi_length = 0, umi_skip = 0;
+    bool index_filter = false;
+    std::string index1_file, index2_file;
+    int index_threshold = 0;
+    std::vector<std::string> blacklist1, blacklist2;  // Options::initIndexFilter
+    bool dup = false;
+    int dup_keylen = 12, dup_hist_size = 32;
+    bool split_by_number = false, split_by_lines = false;
+    int split_number = 0, digits = 4;
+    size_t split_size = 0;
+    int est_reads_num = 0;  // Evaluator::evaluateReadNum
+    bool split() const { return split_by_number || split_by_lines; }
+    // leading bases UmiProcessor::process trims from mate m (before clamping to the read length)
+    int umi_front(int m) const {
+        if (!umi || umi_not_trim) return 0;
+        const bool r1 = umi_location == 3 || umi_location == 6, r2 = umi_location == 4 || umi_location == 6;
+        return (m == 0 ? r1 : (r2 && paired())) ? umi_length + umi_skip : 0;
+    }
     // overlap
     int overlap_require = 30, overlap_diff_limit = 5;
     int insert_size_max = 512;

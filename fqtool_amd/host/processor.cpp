@@ -54,16 +54,97 @@ struct View {
     int len;
 };
 
-View view(const Pack& pk, int m, int i, const fq_read_result* r) {
+// Read::trimFront of the UMI step (src/read.h:203-208): min(k, len - 1) bases
+int umi_cut(int k, int len) { return (k > 0 && len > 0) ? std::min(k, len - 1) : 0; }
+
+// umi_front: the leading bases UmiProcessor::process cut off this mate (Options::umi_front)
+View view(const Pack& pk, int m, int i, const fq_read_result* r, int umi_front = 0) {
     const Rec& rc = pk.rec[m][(size_t)i];
     View v{pk.name(m, (size_t)i), rc.name_len, pk.strand(m, (size_t)i), rc.strand_len,
            pk.seq_text(m, (size_t)i), pk.qual_text(m, (size_t)i), (int)rc.len};
-    if (r && !(r->flags & FQ_RF_NULL)) {  // trimmed in place; a NULL read keeps the original
+    if (r && !(r->flags & FQ_RF_NULL)) {  // trimmed in place
         v.seq += r->start;
         v.qual += r->start;
         v.len = r->len;
+    } else if (umi_front) {  // a NULL read keeps the (UMI-trimmed) original
+        const int u = umi_cut(umi_front, v.len);
+        v.seq += u;
+        v.qual += u;
+        v.len -= u;
     }
     return v;
+}
+
+// Read::firstIndex, reference src/read.h:107-124 (sic: with two indexes the character before
+// the '+' is dropped)
+std::string first_index(const char* name, size_t n) {
+    const int len = (int)n;
+    int end = len;
+    if (len < 5) return "";
+    for (int i = len - 3; i >= 0; --i) {
+        if (name[i] == '+') end = i - 1;
+        if (name[i] == ':') return std::string(name, n).substr((size_t)i + 1, (size_t)(end - i));
+    }
+    return "";
+}
+
+// UmiProcessor::process (src/umiprocessor.cpp:10-79): the tag appended to both names, or ""
+std::string umi_tag(const Options& o, const Pack& pk, int i) {
+    std::string umi = " OX:Z:", qua = " BZ:Z:";
+    const int L = o.umi_length;
+    const bool pe = pk.paired;
+    const int len1 = (int)pk.rec[0][(size_t)i].len, len2 = pe ? (int)pk.rec[1][(size_t)i].len : 0;
+    auto idx = [&](int m) { return first_index(pk.name(m, (size_t)i), pk.rec[m][(size_t)i].name_len); };
+    // the original text (UMI runs before base correction, src/peprocessor.cpp:288-312)
+    auto seq = [&](int m, int from, int n) {
+        return std::string(pk.arena(m) + pk.rec[m][(size_t)i].seq_off() + from, (size_t)n);
+    };
+    auto qual = [&](int m, int from, int n) {
+        return std::string(pk.arena(m) + pk.rec[m][(size_t)i].qual_off() + from, (size_t)n);
+    };
+    const int cut1 = o.umi_not_trim ? 0 : umi_cut(L + o.umi_skip, len1);
+    const int cut2 = o.umi_not_trim ? 0 : umi_cut(L + o.umi_skip, len2);
+    switch (o.umi_location) {
+        case 1: umi += idx(0); break;
+        case 2:
+            if (pe) umi += idx(1);
+            break;
+        case 3:
+            umi += seq(0, 0, std::min(len1, L));
+            qua += qual(0, 0, std::min(len1, L));
+            break;
+        case 4:
+            if (pe) {
+                umi += seq(1, 0, std::min(len2, L));
+                qua += qual(1, 0, std::min(std::min(len1, L), len2));  // sic: r1's length (:44)
+            }
+            break;
+        case 5:
+            umi += idx(0);
+            if (pe) umi += "-" + idx(1);
+            break;
+        case 6:
+            umi += seq(0, 0, std::min(len1, L));
+            qua += qual(0, 0, std::min(len1, L));
+            if (pe) {  // r2's quality is taken after its trim, bounded by r1's trimmed length (:64-67)
+                umi += "-" + seq(1, 0, std::min(len2, L));
+                qua += "-" + qual(1, cut2, std::min(std::min(len1 - cut1, L), len2 - cut2));
+            }
+            break;
+        default: break;
+    }
+    std::string tag = umi;
+    if (tag.size() > 6 && qua.size() > 6) tag += qua;
+    return tag.size() > 6 ? tag : std::string();
+}
+
+// UmiProcessor::addTagToName, src/umiprocessor.cpp:81-89
+std::string tagged_name(const char* name, size_t n, const std::string& tag, bool drop_comment) {
+    const std::string s(name, n);
+    const size_t pos = s.find_first_of(' ');
+    if (pos == std::string::npos) return s + tag;
+    if (drop_comment) return s.substr(0, pos) + tag;
+    return s.substr(0, pos) + tag + s.substr(pos);
 }
 
 // Read::toString / toStringWithTag, reference src/read.h:166-178
@@ -101,10 +182,26 @@ void format_range(const Options& o, const Pack& pk, const fq_read_result* res, i
     std::string& u2 = out.unpaired2[k];
     std::string& fl = out.failed[k];
     std::string& mg = out.merged[k];
+    const int uf1 = o.umi_front(0), uf2 = o.umi_front(1);
+    std::string name1, name2;  // UMI-tagged names
+    auto apply_umi = [&](int i, View& v1, View* v2) {
+        const std::string tag = umi_tag(o, pk, i);
+        if (tag.empty()) return;
+        name1 = tagged_name(v1.name, v1.name_len, tag, o.umi_drop_comment);
+        v1.name = name1.data();
+        v1.name_len = name1.size();
+        if (v2) {
+            name2 = tagged_name(v2->name, v2->name_len, tag, o.umi_drop_comment);
+            v2->name = name2.data();
+            v2->name_len = name2.size();
+        }
+    };
     if (!pk.paired) {  // src/seprocessor.cpp:337-350
         for (int i = i0; i < i1; ++i) {
             const fq_read_result& r = res[i];
-            const View v = view(pk, 0, i, &r);
+            if (r.flags & FQ_RF_INDEX_FILTERED) continue;  // :304-307
+            View v = view(pk, 0, i, &r, uf1);
+            if (o.umi) apply_umi(i, v, nullptr);
             if (!(r.flags & FQ_RF_NULL) && r.code == FQ_PASS_FILTER) append_read(o1, v);
             else if (has_failed) append_read(fl, v, failed_type(r.code));
         }
@@ -113,8 +210,10 @@ void format_range(const Options& o, const Pack& pk, const fq_read_result* res, i
     for (int i = i0; i < i1; ++i) {  // src/peprocessor.cpp:351-429
         const fq_read_result& a = res[2 * (size_t)i];
         const fq_read_result& b = res[2 * (size_t)i + 1];
+        if (a.flags & FQ_RF_INDEX_FILTERED) continue;  // :283-286
         const bool nn1 = !(a.flags & FQ_RF_NULL), nn2 = !(b.flags & FQ_RF_NULL);
-        const View v1 = view(pk, 0, i, &a), v2 = view(pk, 1, i, &b);
+        View v1 = view(pk, 0, i, &a, uf1), v2 = view(pk, 1, i, &b, uf2);
+        if (o.umi) apply_umi(i, v1, &v2);
         bool merge_processed = false;
         if (o.merge && nn1 && nn2) {
             if (a.flags & FQ_RF_MERGED) {
@@ -170,6 +269,74 @@ std::string merged_name(const std::string& name, int len1, int len2) {
     const size_t pos = name.find_first_of(' ');
     if (pos == std::string::npos) return tag;
     return name.substr(0, pos - 1) + tag + name.substr(pos);
+}
+
+// Filter::match, reference src/filter.cpp:191-207
+bool index_match(const std::vector<std::string>& list, const std::string& target, int threshold) {
+    const size_t tlen = target.size();
+    for (const std::string& s : list) {
+        int diff = 0;
+        for (size_t k = 0; k < s.size() && k < tlen; ++k)
+            if (s[k] != target[k] && ++diff > threshold) break;
+        if (diff <= threshold) return true;
+    }
+    return false;
+}
+
+void prepare_pack(const Options& o, Pack& pk, Pool* pool) {
+    pk.use_flags = o.index_filter;
+    if (!o.index_filter) return;
+    pk.flags.resize((size_t)pk.n);
+    const int parts = pool ? std::max(1, std::min(pool->size() * 2, (pk.n + 16383) / 16384)) : 1;
+    auto work = [&](int k) {
+        const int i0 = (int)((int64_t)pk.n * k / parts), i1 = (int)((int64_t)pk.n * (k + 1) / parts);
+        for (int i = i0; i < i1; ++i) {  // Filter::filterByIndex, src/filter.cpp:209-232
+            bool hit = index_match(o.blacklist1, first_index(pk.name(0, (size_t)i), pk.rec[0][(size_t)i].name_len),
+                                   o.index_threshold);
+            if (!hit && pk.paired)
+                hit = index_match(o.blacklist2, first_index(pk.name(1, (size_t)i), pk.rec[1][(size_t)i].name_len),
+                                  o.index_threshold);
+            pk.flags[(size_t)i] = hit ? FQ_BF_INDEX_FILTERED : 0;
+        }
+    };
+    if (pool) pool->run(parts, work);
+    else work(0);
+}
+
+void apply_corrections(const Options& o, Pack& pk, const fq_read_result* res, Pool* pool) {
+    pk.fix.clear();
+    pk.fix_arena.clear();
+    if (!o.correction || !pk.paired) return;
+    const int parts = pool ? std::max(1, std::min(pool->size() * 2, (pk.n + 16383) / 16384)) : 1;
+    pk.fix.assign((size_t)pk.n, nullptr);
+    pk.fix_arena.resize((size_t)parts);
+    auto work = [&](int k) {
+        const int i0 = (int)((int64_t)pk.n * k / parts), i1 = (int)((int64_t)pk.n * (k + 1) / parts);
+        auto corrected = [&](int i) { return ((res[2 * (size_t)i].flags | res[2 * (size_t)i + 1].flags) & FQ_RF_CORRECTED) != 0; };
+        size_t bytes = 0;
+        for (int i = i0; i < i1; ++i)
+            if (corrected(i)) bytes += 2 * ((size_t)pk.rec[0][(size_t)i].len + pk.rec[1][(size_t)i].len);
+        std::string& ar = pk.fix_arena[(size_t)k];
+        ar.resize(bytes);
+        size_t at = 0;
+        for (int i = i0; i < i1; ++i) {
+            if (!corrected(i)) continue;
+            const size_t l1 = pk.rec[0][(size_t)i].len, l2 = pk.rec[1][(size_t)i].len;
+            char* d = &ar[at];
+            std::memcpy(d, pk.seq_text(0, (size_t)i), l1);
+            std::memcpy(d + l1, pk.qual_text(0, (size_t)i), l1);
+            std::memcpy(d + 2 * l1, pk.seq_text(1, (size_t)i), l2);
+            std::memcpy(d + 2 * l1 + l2, pk.qual_text(1, (size_t)i), l2);
+            const fq_read_result& a = res[2 * (size_t)i];
+            const fq_read_result& b = res[2 * (size_t)i + 1];
+            fq_correct_pair_text(d + a.start, d + l1 + a.start, d + 2 * l1 + b.start, d + 2 * l1 + l2 + b.start,
+                                 (int16_t)b.m_len1, b.m_len2, b.reserved);
+            pk.fix[(size_t)i] = d;
+            at += 2 * (l1 + l2);
+        }
+    };
+    if (pool) pool->run(parts, work);
+    else work(0);
 }
 
 void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out, Pool* pool) {
@@ -486,6 +653,7 @@ int run_tool(int argc, char** argv) {
                 while (done.pop(pk)) {
                     const auto f0 = std::chrono::steady_clock::now();
                     const fq_params p = o.to_params(eng.max_cycles);
+                    apply_corrections(o, *pk, pk->res.data(), &pool);
                     if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p, &pool);
                     PackOutput out;
                     format_pack(o, *pk, pk->res.data(), out, &pool);
@@ -523,6 +691,7 @@ int run_tool(int argc, char** argv) {
             while (packs.pop(pk)) {
                 const auto p0 = std::chrono::steady_clock::now();
                 pack_tiles(*pk, &pool);
+                prepare_pack(o, *pk, &pool);
                 tiles_s += since(p0);
                 int max1 = 0, max2 = 0;
                 for (uint16_t l : pk->len[0]) max1 = std::max(max1, (int)l);

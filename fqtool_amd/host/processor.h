@@ -45,6 +45,11 @@ class OutputSet {
 // With a pool, ranges of the pack are formatted in parallel into consecutive blocks.
 void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out, Pool* pool = nullptr);
 
+// Before the engine call: per-pair index-filter flags (Filter::filterByIndex) when enabled.
+void prepare_pack(const Options& o, Pack& pk, Pool* pool = nullptr);
+// After it (-c): pairs with FQ_RF_CORRECTED records read corrected copies of their text.
+void apply_corrections(const Options& o, Pack& pk, const fq_read_result* res, Pool* pool = nullptr);
+
 // OverlapAnalysis::merge name rule (src/overlapanalysis.cpp:93-101)
 std::string merged_name(const std::string& name, int len1, int len2);
 

@@ -26,6 +26,8 @@ void HostAcc::add(const uint64_t* acc, int max_cycles) {
         const uint64_t* cy = st + FQ_ST_CYCLES;
         for (size_t i = 0; i < (size_t)max_cycles * 16; ++i) cyc_[k][i] += cy[i];
     }
+    const uint64_t* t = acc + fq_acc_tail_offset(ism_, max_cycles);
+    for (int j = 0; j < FQ_ACC_TAIL_WORDS; ++j) tail_[j] += t[j];
 }
 
 void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_params& p, Pool* pool) {
@@ -188,6 +190,10 @@ Json build_report(const Options& o, const HostAcc& a, const AdapterCounts& ac) {
     fr["PassedFilterReads"] = Json::u(a.filter(FQ_PASS_FILTER));
     fr["LowQualityReads"] = Json::u(a.filter(FQ_FAIL_QUALITY));
     fr["TooManyNReads"] = Json::u(a.filter(FQ_FAIL_N_BASE));
+    if (o.correction) {
+        fr["CorrectedReads"] = Json::u(a.tail(FQ_ACC_TAIL_CORRECTED_READS));
+        fr["CorrectedBases"] = Json::u(a.tail(FQ_ACC_TAIL_CORRECTED_BASES));
+    }
     if (o.complexity_filter) fr["LowComplexityReads"] = Json::u(a.filter(FQ_FAIL_COMPLEXITY));
     if (o.length_filter) {
         fr["TooShortReads"] = Json::u(a.filter(FQ_FAIL_LENGTH));

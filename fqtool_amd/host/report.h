@@ -32,6 +32,10 @@ class HostAcc {
     uint64_t stat(int k, int field) const { return st_[k][field]; }
     uint64_t cyc(int k, int c, int slot) const { return (size_t)c < cyc_[k].size() / 16 ? cyc_[k][(size_t)c * 16 + slot] : 0; }
     int insert_size_max() const { return ism_; }
+    uint64_t tail(int k) const { return tail_[k]; }  // FQ_ACC_TAIL_*
+    // duplication analysis result (Duplicate::statAll), filled by the engine caller
+    std::vector<uint64_t> dup_hist, dup_gc_sum;
+    double dup_rate = 0;
 
    private:
     int ism_;
@@ -39,6 +43,7 @@ class HostAcc {
     std::vector<uint64_t> head_;   // everything before the stats blocks
     uint64_t st_[4][4] = {};       // reads, length_sum, q20, q30
     std::vector<uint64_t> cyc_[4];  // [cycle][16]
+    uint64_t tail_[FQ_ACC_TAIL_WORDS] = {};
 };
 
 // FilterResult's adapter string -> count maps (src/filterresult.cpp:138-177)

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define FQ_ABI_VERSION 2
+#define FQ_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define FQ_OK 0
@@ -117,7 +117,17 @@ typedef struct fq_params {
 
     /* engine sizing */
     int32_t max_cycles; /* per-cycle Stats buffer length; reads longer than this are rejected */
-    int32_t reserved[7];
+
+    /* -c: BaseCorrector::correctByOverlapAnalysis (src/basecorrector.cpp:14-70), PE only, run
+     * between the insert-size statistics and adapter trimming (src/peprocessor.cpp:310-312).
+     * The engine corrects the bases/qualities of the DEVICE batch planes in place. */
+    int32_t correction_enabled;
+    /* -u with the UMI in the read (UmiProcessor::process, src/umiprocessor.cpp:10-79): after the
+     * pre-filter statistics each mate loses min(umi_front, len - 1) leading bases
+     * (Read::trimFront, src/read.h:203-208); 0 = no UMI trim.  The UMI tag itself only changes
+     * the read names and is the host's business. */
+    int32_t umi_front1, umi_front2;
+    int32_t reserved[4];
 } fq_params;
 
 /* One pack of reads.  Each plane (seq1, qual1, seq2, qual2) holds every read's row of `stride`
@@ -140,7 +150,14 @@ typedef struct fq_batch {
     const uint8_t* seq2; /* PE only, else NULL */
     const uint8_t* qual2;
     const uint16_t* len2;
+    /* optional per-pair (per-read in SE) FQ_BF_* flags, n bytes; NULL = all zero */
+    const uint8_t* flags;
 } fq_batch;
+
+/* fq_batch.flags: the pair (read) was dropped by Filter::filterByIndex
+ * (src/filter.cpp:209-232, called at src/peprocessor.cpp:283 / src/seprocessor.cpp:304): only the
+ * pre-filter statistics count it, its record carries FQ_RF_INDEX_FILTERED and nothing else. */
+#define FQ_BF_INDEX_FILTERED 0x01
 
 static inline size_t fq_batch_offset(int32_t stride, int64_t i, int32_t j) {
     return (size_t)(i / FQ_TILE_READS) * FQ_TILE_READS * (size_t)stride +
@@ -178,6 +195,8 @@ static inline void fq_batch_get_row(const uint8_t* plane, int32_t stride, int64_
 #define FQ_RF_AD_NEG 0x08    /* trimBySequence matched at pos<0: recorded adapter = adapter[ad_pos:] */
 #define FQ_RF_MERGED 0x10    /* (read-1 record) pair was merged (-m) */
 #define FQ_RF_OVERLAP 0x20   /* (read-1 record) OverlapAnalysis reported overlapped for this pair */
+#define FQ_RF_CORRECTED 0x40 /* -c corrected bases of this read (see fq_read_result) */
+#define FQ_RF_INDEX_FILTERED 0x80 /* the pair/read was dropped by the index filter (FQ_BF_INDEX_FILTERED) */
 
 /*
  * Everything the loop body's in-place std::string edits leave behind, per read (16 bytes).
@@ -187,6 +206,11 @@ static inline void fq_batch_get_row(const uint8_t* plane, int32_t stride, int64_
  * FQ_RF_AD_NEG, adapter[ad_pos .. ad_pos+ad_len).  For a merged pair (FQ_RF_MERGED, read-1
  * record) the merged read is r1[0:m_len1] + revcomp(r2)[ol : ol+m_len2] with ol = len2 - m_len2
  * (src/overlapanalysis.cpp:74-104); the read-1 record's code is the merged read's code.
+ * Base correction (-c, FQ_RF_CORRECTED on either mate's record): the read-2 record carries the
+ * correcting overlap, m_len1 = (int16_t) offset, m_len2 = overlap length, reserved = read 2's length
+ * at correction time; both reads' windows start at their final `start`.  The corrected bytes are
+ * those BaseCorrector::correctByOverlapAnalysis rewrites for that overlap (src/basecorrector.cpp:
+ * 14-70), which a host re-applies to its copy of the text (fq_correct_pair_text below).
  */
 typedef struct fq_read_result {
     uint16_t start;
@@ -200,6 +224,39 @@ typedef struct fq_read_result {
     uint16_t reserved;
 } fq_read_result;
 
+/* util::complement, reference src/util.h:438-451 */
+static inline char fq_complement(char c) {
+    switch (c) {
+        case 'A': case 'a': return 'T';
+        case 'T': case 't': return 'A';
+        case 'C': case 'c': return 'G';
+        case 'G': case 'g': return 'C';
+        default: return 'N';
+    }
+}
+
+/* Re-applies the edits of BaseCorrector::correctByOverlapAnalysis (src/basecorrector.cpp:14-70)
+ * for a FQ_RF_CORRECTED pair to a host copy of its text: s1/q1 = read 1 from its record's start,
+ * s2/q2 = read 2 from its record's start, (offset, ol, len2) from the read-2 record
+ * ((int16_t) m_len1, m_len2, reserved).  The engine took the same decisions on the device. */
+static inline void fq_correct_pair_text(char* s1, char* q1, char* s2, char* q2, int offset, int ol, int len2) {
+    const int start1 = offset > 0 ? offset : 0;
+    const int start2 = len2 - (offset < 0 ? -offset : 0) - 1;
+    const char good = (char)(33 + 30), bad = (char)(33 + 14); /* util::num2qual(30), (14) */
+    int i;
+    for (i = 0; i < ol; ++i) {
+        const int p1 = start1 + i, p2 = start2 - i;
+        if (s1[p1] == fq_complement(s2[p2])) continue;
+        if ((signed char)q1[p1] >= good && (signed char)q2[p2] <= bad) {
+            s2[p2] = fq_complement(s1[p1]);
+            q2[p2] = q1[p1];
+        } else if ((signed char)q2[p2] >= good && (signed char)q1[p1] <= bad) {
+            s1[p1] = fq_complement(s2[p2]);
+            q1[p1] = q2[p2];
+        }
+    }
+}
+
 /*
  * Flat accumulator (uint64 words).  Layout (indices into the uint64 array):
  *   FQ_ACC_FILTER + code          FilterResult::mFilterReadStats[32]
@@ -212,6 +269,7 @@ typedef struct fq_read_result {
  *        +FQ_ST_READS, +FQ_ST_LENGTH_SUM, +FQ_ST_Q20, +FQ_ST_Q30 then, from +FQ_ST_CYCLES,
  *        [max_cycles][16] = per cycle 8 base-class counts (mCycleBaseContents[b][c], b = byte&7)
  *        followed by 8 base-class quality sums (mCycleBaseQuality[b][c]).
+ *   fq_acc_tail_offset + FQ_ACC_TAIL_*  the -c counters.
  * All counters are sums, so N engines (GPUs) combine by element-wise uint64 addition.
  */
 #define FQ_ACC_FILTER 0
@@ -221,6 +279,10 @@ typedef struct fq_read_result {
 #define FQ_ACC_POLYX_BASES 39
 #define FQ_ACC_MERGED_PAIRS 44
 #define FQ_ACC_INSERT 48
+/* after the four Stats blocks (fq_acc_tail_offset): -c counters */
+#define FQ_ACC_TAIL_CORRECTED_READS 0 /* FilterResult::mCorrectedReads                        */
+#define FQ_ACC_TAIL_CORRECTED_BASES 1 /* sum of FilterResult::mCorrectionMatrix (CorrectedBases) */
+#define FQ_ACC_TAIL_WORDS 16
 #define FQ_ST_READS 0
 #define FQ_ST_LENGTH_SUM 1
 #define FQ_ST_Q20 2
@@ -236,8 +298,11 @@ static inline size_t fq_acc_stats_offset(int32_t insert_size_max, int32_t max_cy
     base = (base + 15) & ~(size_t)15;
     return base + (size_t)k * fq_acc_stats_words(max_cycles);
 }
-static inline size_t fq_acc_words(int32_t insert_size_max, int32_t max_cycles) {
+static inline size_t fq_acc_tail_offset(int32_t insert_size_max, int32_t max_cycles) {
     return fq_acc_stats_offset(insert_size_max, max_cycles, 4);
+}
+static inline size_t fq_acc_words(int32_t insert_size_max, int32_t max_cycles) {
+    return fq_acc_tail_offset(insert_size_max, max_cycles) + FQ_ACC_TAIL_WORDS;
 }
 
 /* ---- engine ------------------------------------------------------------------------- */

@@ -373,6 +373,54 @@ static void apply_polyg(const fq_params* p, const uint8_t* seq, int start, int* 
     }
 }
 
+/* Read::trimFront(umi length + skip) of UmiProcessor::process, src/umiprocessor.cpp:28-62 and
+ * src/read.h:203-208: min(k, len - 1) leading bases go (a read of length 0 is left alone) */
+static int umi_cut(int k, int len) { return (k > 0 && len > 0) ? ORC_MIN(k, len - 1) : 0; }
+
+static int index_filtered(const fq_batch* b, int i) { return b->flags && (b->flags[i] & FQ_BF_INDEX_FILTERED); }
+
+/* src/basecorrector.cpp:14-70 BaseCorrector::correctByOverlapAnalysis on the pair's windows (the
+ * gathered row copies are edited in place, as the reference edits its strings) */
+static void correct_by_overlap(uint8_t* s1, uint8_t* q1, uint8_t* s2, uint8_t* q2, int len2, orc_overlap ov,
+                               fq_read_result* rr1, fq_read_result* rr2, uint64_t* tail) {
+    if (ov.diff == 0 || ov.diff > 5) return;
+    int ol = ov.overlap_len;
+    int start1 = ORC_MAX(0, ov.offset);
+    int start2 = len2 - ORC_MAX(0, -ov.offset) - 1;
+    const int GOOD_QUAL = 33 + 30, BAD_QUAL = 33 + 14; /* util::num2qual */
+    int corrected = 0, r1c = 0, r2c = 0;
+    for (int i = 0; i < ol; ++i) {
+        int p1 = start1 + i, p2 = start2 - i;
+        if (s1[p1] != complement_base(s2[p2])) {
+            if (qv(q1, p1) >= GOOD_QUAL && qv(q2, p2) <= BAD_QUAL) {
+                s2[p2] = complement_base(s1[p1]);
+                q2[p2] = q1[p1];
+                ++corrected;
+                r2c = 1;
+            } else if (qv(q2, p2) >= GOOD_QUAL && qv(q1, p1) <= BAD_QUAL) {
+                s1[p1] = complement_base(s2[p2]);
+                q1[p1] = q2[p2];
+                ++corrected;
+                r1c = 1;
+            }
+        }
+    }
+    if (corrected > 0) {
+        tail[FQ_ACC_TAIL_CORRECTED_READS] += (r1c && r2c) ? 2 : 1; /* incCorrectedReads */
+        tail[FQ_ACC_TAIL_CORRECTED_BASES] += (uint64_t)corrected; /* one addCorrection per base */
+        if (r1c) rr1->flags |= FQ_RF_CORRECTED;
+        if (r2c) rr2->flags |= FQ_RF_CORRECTED;
+        rr2->m_len1 = (uint16_t)(int16_t)ov.offset;
+        rr2->m_len2 = (uint16_t)ol;
+        rr2->reserved = (uint16_t)len2;
+    }
+}
+
+static void set_index_filtered(fq_read_result* r) {
+    memset(r, 0, sizeof *r);
+    r->flags = FQ_RF_INDEX_FILTERED;
+}
+
 /* src/seprocessor.cpp:290-388 SingleEndProcessor::processSingleEnd, loop body */
 static int process_se(const fq_params* p, const fq_batch* b, fq_read_result* res, uint64_t* acc) {
     uint64_t* pre = acc + fq_acc_stats_offset(p->insert_size_max, p->max_cycles, 0);
@@ -384,8 +432,14 @@ static int process_se(const fq_params* p, const fq_batch* b, fq_read_result* res
         if (l > p->max_cycles) return FQ_E_TOO_LONG;
         fq_read_result* rr = &res[i];
         orc_stat_read(pre, p->max_cycles, seq, qual, l); /* :298 */
+        if (index_filtered(b, i)) { /* :304-307 */
+            set_index_filtered(rr);
+            continue;
+        }
+        int u = umi_cut(p->umi_front1, l); /* :309-311 */
         int s = 0, len = 0;
-        int nonnull = orc_trim_and_cut(p, seq, qual, l, p->trim_front1, p->trim_tail1, &s, &len); /* :313 */
+        int nonnull = orc_trim_and_cut(p, seq + u, qual + u, l - u, p->trim_front1, p->trim_tail1, &s, &len); /* :313 */
+        s += u;
         set_result(rr, !nonnull, s, len);
         if (nonnull && p->polyg_enabled) apply_polyg(p, seq, s, &len, acc);          /* :315-319 */
         if (nonnull && p->adapter_trimming && p->adapter1_len > 0)                  /* :321-323 */
@@ -428,9 +482,17 @@ static int process_pe(const fq_params* p, const fq_batch* b, fq_read_result* res
         fq_read_result* rr2 = &res[2 * i + 1];
         orc_stat_read(pre1, p->max_cycles, s1, q1, l1); /* :276-277 */
         orc_stat_read(pre2, p->max_cycles, s2, q2, l2);
+        if (index_filtered(b, i)) { /* :283-286 */
+            set_index_filtered(rr1);
+            set_index_filtered(rr2);
+            continue;
+        }
+        int u1 = umi_cut(p->umi_front1, l1), u2 = umi_cut(p->umi_front2, l2); /* :288-290 */
         int st1 = 0, n1 = 0, st2 = 0, n2 = 0; /* :292-293 */
-        int nn1 = orc_trim_and_cut(p, s1, q1, l1, p->trim_front1, p->trim_tail1, &st1, &n1);
-        int nn2 = orc_trim_and_cut(p, s2, q2, l2, p->trim_front2, p->trim_tail2, &st2, &n2);
+        int nn1 = orc_trim_and_cut(p, s1 + u1, q1 + u1, l1 - u1, p->trim_front1, p->trim_tail1, &st1, &n1);
+        int nn2 = orc_trim_and_cut(p, s2 + u2, q2 + u2, l2 - u2, p->trim_front2, p->trim_tail2, &st2, &n2);
+        st1 += u1;
+        st2 += u2;
         set_result(rr1, !nn1, st1, n1);
         set_result(rr2, !nn2, st2, n2);
         const int both = nn1 && nn2;
@@ -441,6 +503,9 @@ static int process_pe(const fq_params* p, const fq_batch* b, fq_read_result* res
         if (both) { /* :302-333: overlap once per pair (every pair == reference -w 1) */
             orc_overlap ov = orc_analyze(s1 + st1, n1, s2 + st2, n2, p->overlap_diff_limit, p->overlap_require);
             stat_insert(p, acc, n1, n2, ov);
+            if (p->correction_enabled) /* :310-312 */
+                correct_by_overlap((uint8_t*)s1 + st1, (uint8_t*)q1 + st1, (uint8_t*)s2 + st2, (uint8_t*)q2 + st2, n2, ov,
+                                   rr1, rr2, acc + fq_acc_tail_offset(p->insert_size_max, p->max_cycles));
             if (p->adapter_trimming) {
                 /* AdapterTrimmer::trimByOverlapAnalysis, src/adaptertrimmer.cpp:14-27 */
                 int ol = ov.overlap_len;

@@ -32,6 +32,8 @@ class Pack:
         q[i, : len(qual)] = np.frombuffer(qual, np.uint8)
         getattr(self, "len%d" % mate)[i] = len(seq)
 
+    flags = None  # optional per-pair FQ_BF_* flags (np.uint8, n)
+
     def planes(self):
         return ("seq1", "qual1", "seq2", "qual2") if self.paired else ("seq1", "qual1")
 
@@ -42,6 +44,8 @@ class Pack:
         b.seq1, b.qual1, b.len1 = self._tiled["seq1"].ctypes.data, self._tiled["qual1"].ctypes.data, self.len1.ctypes.data
         if self.paired:
             b.seq2, b.qual2, b.len2 = self._tiled["seq2"].ctypes.data, self._tiled["qual2"].ctypes.data, self.len2.ctypes.data
+        if self.flags is not None:
+            b.flags = self.flags.ctypes.data
         return b
 
     def load_batch(self):
@@ -105,7 +109,7 @@ def edge_pack(n, paired, stride=160, seed=7):
 
 def config(name, max_cycles=256):
     """Parameter presets: the BASELINE configs plus extra option coverage."""
-    paired = name not in ("C2", "SE_adapter", "SE_all")
+    paired = name not in ("C2", "SE_adapter", "SE_all", "SE_umi")
     p = abi.default_params(paired=paired, max_cycles=max_cycles)
     p.qual_filter_enabled = 1  # every config has -q
     if name == "C2":
@@ -176,6 +180,23 @@ def config(name, max_cycles=256):
         p.overlap_diff_limit, p.overlap_require = 5, 12
         p.avg_qual_limit = 20.0
         p.length_filter_enabled, p.min_len = 1, 40
+    elif name == "PE_correct":  # -c with the C3 options
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.correction_enabled = 1
+    elif name == "PE_correct_all":  # -c ahead of adapters by sequence, polyX, merge
+        p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
+        abi.set_adapter(p, 1, AD1)
+        p.correction_enabled = 1
+        p.merge_enabled = 1
+        p.cut_right = 1
+    elif name == "PE_umi":  # UMI in both reads (trimFront after the pre-filter stats)
+        p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
+        p.cut_front = 1
+        p.umi_front1, p.umi_front2 = 10, 7
+    elif name == "SE_umi":
+        p.polyg_enabled = 1
+        p.cut_tail = 1
+        p.umi_front1 = 12
     elif name.startswith("PE_cutR"):  # cut_right alone (removed-mode stats), window w
         w = int(name[7:])
         p.adapter_trimming = p.polyg_enabled = 1
@@ -192,7 +213,8 @@ def config(name, max_cycles=256):
 
 
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
-               "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR5", "PE_merge_q"]
+               "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR5", "PE_merge_q",
+               "PE_correct", "PE_correct_all", "PE_umi", "SE_umi"]
 
 
 def run_oracle(oracle, p, pk):

@@ -84,6 +84,43 @@ CASES = {
     "edge_se_all": "-i {in}/edge_r1.fq -o {out}/o1.fq -q -a -g -x -y -l --enable_cut_front --enable_cut_tail "
                    "--failed_out {out}/failed.fq",
     "edge64_pe": "-i {in}/edge64_r1.fq -I {in}/edge64_r2.fq --phred64 -o {out}/o1.fq -O {out}/o2.fq -q -a -g",
+    # base correction (-c), alone, with adapters/merge, on hostile reads
+    "td_pe_correct": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -c -q -a -g "
+                     "--failed_out {out}/failed.fq",
+    "td_pe_correct_only": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -c",
+    "synth_pe_correct_merge": "-i {in}/synth_r1.fq.gz -I {in}/synth_r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -c -q -a "
+                              "-g -m --merge_output {out}/merged.fq",
+    "edge_pe_correct": "-i {in}/edge_r1.fq -I {in}/edge_r2.fq -o {out}/o1.fq -O {out}/o2.fq -c -q -a -g -x "
+                       "--adapter_of_read1 AGATCGGAAGAGCACACGTCTGAACTCCAGTCA --unpaired_read1 {out}/u1.fq "
+                       "--unpaired_read2 {out}/u2.fq --failed_out {out}/failed.fq",
+    # UMI: every location, trim / no trim, comment dropping, SE
+    "td_pe_umi_idx1": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -u --umi_location 1",
+    "td_pe_umi_idx2": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -u --umi_location 2 "
+                      "--umi_drop_comment",
+    "td_pe_umi_r1": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -a -g -u --umi_location 3 "
+                    "--umi_length 8 --umi_skip_length 2 --failed_out {out}/failed.fq",
+    "td_pe_umi_r2_notrim": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -u --umi_location 4 "
+                           "--umi_length 5 --umi_not_trim",
+    "td_pe_umi_perindex": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -u --umi_location 5",
+    "td_pe_umi_perread": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -g -u --umi_location 6 "
+                         "--umi_length 6 --umi_skip_length 1 --umi_drop_comment -m --merge_output {out}/merged.fq",
+    "edge_pe_umi_perread": "-i {in}/edge_r1.fq -I {in}/edge_r2.fq -o {out}/o1.fq -O {out}/o2.fq -q -a -g "
+                           "--enable_cut_front -u --umi_location 6 --umi_length 12 --umi_skip_length 3 "
+                           "--unpaired_read1 {out}/u1.fq --failed_out {out}/failed.fq",
+    "td_se_umi_r1": "-i {in}/r1.fq.gz -o {out}/o1.fq -q -u --umi_location 3 --umi_length 7 --failed_out {out}/failed.fq",
+    "td_se_umi_perindex": "-i {in}/r1.fq.gz -o {out}/o1.fq -u --umi_location 5",
+    "edge_se_umi_r2": "-i {in}/edge_r1.fq -o {out}/o1.fq -q -u --umi_location 4 --umi_length 4",
+    # index filter
+    "td_pe_index": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -a -g --enable_index_filter "
+                   "--index1_file {in}/idx_a.txt --index2_file {in}/idx_b.txt --failed_out {out}/failed.fq",
+    "td_pe_index_diff1": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q --enable_index_filter "
+                         "--index1_file {in}/idx_c.txt --max_diff_for_match 1 -u --umi_location 1",
+    "td_se_index": "-i {in}/r1.fq.gz -o {out}/o1.fq -q --enable_index_filter --index1_file {in}/idx_a.txt",
+    "synth_pe_index_all": "-i {in}/synth_r1.fq.gz -I {in}/synth_r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q "
+                          "--enable_index_filter --index2_file {in}/idx_empty_line.txt",
+    "td_pe_index_nofile": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q --enable_index_filter",
+    "err_index_bad": "-i {in}/r1.fq.gz -o {out}/o1.fq --enable_index_filter --index1_file {in}/idx_bad.txt",
+    "err_umi_len0": "-i {in}/r1.fq.gz -o {out}/o1.fq -u --umi_location 3",
     # validation / CLI failures: exit status only (messages are compared for validate errors)
     "err_merge_no_out": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -m",
     "err_polyx_chars": "-i {in}/r1.fq.gz -o {out}/o1.fq -x --base_to_trim ACGU",
@@ -154,6 +191,11 @@ def make_inputs():
         with open(os.path.join(INP, "edge64_r%d.fq" % m), "wb") as f:
             for name, s, q in recs[m]:
                 f.write(name + b"\n" + s + b"\n+\n" + bytes(c + 31 for c in q) + b"\n")
+    # index-filter blacklists (Options::makeListFromFileByLine input)
+    for name, text in (("idx_a.txt", b"TAGGTCC\nTAGTTCA\n"), ("idx_b.txt", b"TAGTTAC\n"), ("idx_c.txt", b"TAGGTCA\n"),
+                       ("idx_empty_line.txt", b"ACGTAC\n\n"), ("idx_bad.txt", b"ACGT\nacgt\n")):
+        with open(os.path.join(INP, name), "wb") as f:
+            f.write(text)
     # interleaved
     with gzip.open(os.path.join(INP, "r1.fq.gz")) as f1, gzip.open(os.path.join(INP, "r2.fq.gz")) as f2:
         l1, l2 = f1.read().split(b"\n"), f2.read().split(b"\n")

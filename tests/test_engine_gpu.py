@@ -103,6 +103,33 @@ def test_mixed_fast_and_handoff_tiles(eng_lib, oracle, name):
     assert_same(p, res_o, acc_o, res_e, acc_e)
 
 
+@pytest.mark.parametrize("name", ["C3", "C2", "PE_correct", "PE_umi", "C4"])
+def test_index_filtered_pairs(eng_lib, oracle, name, mode):
+    """fq_batch.flags: pairs the host's index filter dropped count only in the pre-filter stats
+    (src/peprocessor.cpp:283-286); the flags travel with the pack in both dispatch modes."""
+    p = config(name, max_cycles=512)
+    pk = synth_pack(oracle, 5000, bool(p.paired), first=4321)
+    rng = np.random.default_rng(11)
+    pk.flags = (rng.random(pk.n) < 0.2).astype(np.uint8) * abi.FQ_BF_INDEX_FILTERED
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    mates = 2 if p.paired else 1
+    assert ((res_o["flags"].reshape(-1, mates)[:, 0] & abi.FQ_RF_INDEX_FILTERED) != 0).sum() == int(pk.flags.astype(bool).sum())
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+def test_correction_counts(eng_lib, oracle):
+    """-c on hostile reads corrects bases (the oracle is pinned to the reference by the
+    td_pe_correct / edge_pe_correct e2e fixtures); the engine agrees on every record and word."""
+    p = config("PE_correct", max_cycles=512)
+    pk = edge_pack(6000, True, seed=99)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    tail = abi.acc_tail_offset(p.insert_size_max, p.max_cycles)
+    assert acc_o[tail + abi.FQ_ACC_TAIL_CORRECTED_BASES] > 0
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
 def test_empty_pack(eng_lib, oracle):
     p = config("C3", max_cycles=256)
     pk = Pack(0, 160, True)
