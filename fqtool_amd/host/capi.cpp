@@ -105,7 +105,7 @@ struct fqh_session {
     std::unique_ptr<Pool> pool;  // -w threads: tile packing, formatting, gzip
     std::unique_ptr<PackReader> reader;
     Pack pk;
-    std::unique_ptr<OutputSet> outs;
+    std::unique_ptr<Sink> outs;
     HostAcc acc;
     AdapterCounts ac;
     std::string err;
@@ -121,7 +121,7 @@ int fqh_session_open(int argc, char** argv, fqh_session** out) {
         s->acc = HostAcc(s->o.insert_size_max);
         s->reader.reset(new PackReader(s->o.in1, s->o.in2, s->o.interleaved, s->o.phred64));
         s->pool.reset(new Pool(std::max(0, s->o.threads - 1)));
-        s->outs.reset(new OutputSet(s->o, s->pool.get()));
+        s->outs.reset(new Sink(s->o, s->pool.get()));
     } catch (const std::exception& e) {
         s->err = e.what();
         *out = s.release();
@@ -157,9 +157,7 @@ int fqh_session_consume(fqh_session* s, const fq_read_result* res, int max_cycle
         const fq_params p = s->o.to_params(max_cycles);
         apply_corrections(s->o, s->pk, res, s->pool.get());
         if (s->o.adapter_trimming) s->ac.add(s->pk, res, p);
-        PackOutput out;
-        format_pack(s->o, s->pk, res, out, s->pool.get());
-        s->outs->write(std::move(out));
+        s->outs->consume(s->pk, res);
         return 0;
     } catch (const std::exception& e) {
         s->err = e.what();

@@ -4,6 +4,7 @@
 // (src/filterresult.cpp:315-317).
 #include "evaluator.h"
 
+#include <fstream>
 #include <algorithm>
 #include <cstring>
 #include <iostream>
@@ -141,6 +142,35 @@ int evaluate_read_len(const std::string& path) {  // Evaluator::computeReadLen, 
     int len = 0;
     for (int i = 0; i < 1000 && r.read(n, s, d, q); ++i) len = std::max(len, (int)s.size());
     return len;
+}
+
+int evaluate_read_num(const std::string& path) {  // Evaluator::evaluateReadNum, src/evaluator.cpp:191-227
+    const size_t kReadLimit = 512 * 1024, kBaseLimit = 151 * 512 * 1024;
+    FqReader r(path, false, 1 << 20, true);
+    ByteBuf text;
+    Rec rec;
+    size_t records = 0, bases = 0;
+    uint64_t first_pos = 0;
+    bool eof = false;
+    while (records < kReadLimit && bases < kBaseLimit) {
+        text.clear();
+        if (!r.read(text, rec)) {
+            if (!r.error().empty()) std::cerr << r.error();
+            eof = true;
+            break;
+        }
+        if (records == 0) first_pos = r.stream_pos();
+        ++records;
+        bases += rec.len;
+    }
+    if (eof) return (int)records;
+    if (records <= 1) return 0;
+    const uint64_t pos = r.stream_pos();
+    std::ifstream is(path, std::ios::binary);  // bytesTotal: the file's size
+    is.seekg(0, is.end);
+    const double total = (double)(long long)is.tellg();
+    const double per_read = (double)(pos - first_pos) / (double)(records - 1);
+    return (int)(size_t)(total * 1.01 / per_read);
 }
 
 // Evaluator::evaluateAdapterSeq, src/evaluator.cpp:229-390

@@ -8,6 +8,9 @@ namespace fqhost {
 
 // longest of the first 1000 reads
 int evaluate_read_len(const std::string& path);
+// Evaluator::evaluateReadNum (src/evaluator.cpp:191-227): the record count when the file ends
+// within 512 Ki records / 151 x 512 Ki bases, else an estimate from the bytes per record
+int evaluate_read_num(const std::string& path);
 // detected adapter of one mate file ("" when none), trim_tail1 = -t as the reference passes it.
 // A read error message goes to *msgs when given (so two concurrent detections can report in
 // the reference's order), else straight to stderr.

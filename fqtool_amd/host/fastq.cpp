@@ -82,18 +82,24 @@ void ByteBuf::reserve(size_t n) {
     is_pinned_ = pinned;
 }
 
-FqReader::FqReader(const std::string& path, bool phred64, int buf_size)
+FqReader::FqReader(const std::string& path, bool phred64, int buf_size, bool zlib_default_buffer)
     : phred64_(phred64), buf_size_(buf_size), buf_((size_t)buf_size) {
     if (ends_with(path, ".gz")) {
         gz_ = gzopen(path.c_str(), "r");
         if (!gz_) throw std::runtime_error("Failed to open file: " + path);
-        gzbuffer(gz_, 1 << 20);
+        if (!zlib_default_buffer) gzbuffer(gz_, 1 << 20);
         gzrewind(gz_);
     } else {
         fp_ = path == "/dev/stdin" ? stdin : std::fopen(path.c_str(), "rb");
         if (!fp_) throw std::runtime_error("Failed to open file: " + path);
     }
     fill();
+}
+
+uint64_t FqReader::stream_pos() const {
+    if (gz_) return (uint64_t)gzoffset(gz_);
+    const long t = std::ftell(fp_);
+    return t < 0 ? 0 : (uint64_t)t;
 }
 
 FqReader::~FqReader() {

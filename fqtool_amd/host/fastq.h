@@ -99,8 +99,12 @@ struct Rec {
 class FqReader {
    public:
     // buf_size: the reference's read buffer (1 MiB, src/fqreader.cpp:10); smaller only in tests
-    FqReader(const std::string& path, bool phred64, int buf_size = 1 << 20);
+    // zlib_default_buffer: keep zlib's own input buffer size as the reference's reader does (only
+    // stream_pos() can tell the difference)
+    FqReader(const std::string& path, bool phred64, int buf_size = 1 << 20, bool zlib_default_buffer = false);
     ~FqReader();
+    // FqReader::getBytes' bytesRead (src/fqreader.cpp:64-75): gzoffset / ftell of the stream
+    uint64_t stream_pos() const;
     FqReader(const FqReader&) = delete;
     FqReader& operator=(const FqReader&) = delete;
     // Next record appended to `text`; false at end of input or on a quality/sequence length

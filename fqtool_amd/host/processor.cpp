@@ -339,14 +339,17 @@ void apply_corrections(const Options& o, Pack& pk, const fq_read_result* res, Po
     else work(0);
 }
 
-void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out, Pool* pool) {
-    const int parts = pool ? std::max(1, std::min(pool->size() * 2, (pk.n + 8191) / 8192)) : 1;
+void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out, Pool* pool,
+                 const std::vector<int>* cuts) {
+    const int parts = cuts ? std::max(0, (int)cuts->size() - 1)
+                           : pool ? std::max(1, std::min(pool->size() * 2, (pk.n + 8191) / 8192)) : 1;
     for (auto* v : {&out.out1, &out.out2, &out.unpaired1, &out.unpaired2, &out.failed, &out.merged}) {
         v->clear();
         v->resize((size_t)parts);
     }
     auto work = [&](int k) {
-        const int i0 = (int)((int64_t)pk.n * k / parts), i1 = (int)((int64_t)pk.n * (k + 1) / parts);
+        const int i0 = cuts ? (*cuts)[(size_t)k] : (int)((int64_t)pk.n * k / parts);
+        const int i1 = cuts ? (*cuts)[(size_t)k + 1] : (int)((int64_t)pk.n * (k + 1) / parts);
         out.out1[(size_t)k].reserve(span_bytes(pk, 0, i0, i1));
         if (pk.paired) {
             if (o.merge) out.merged[(size_t)k].reserve(span_bytes(pk, 0, i0, i1) + span_bytes(pk, 1, i0, i1));
@@ -354,8 +357,9 @@ void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, Pa
         }
         format_range(o, pk, res, i0, i1, (size_t)k, out);
     };
-    if (pool) pool->run(parts, work);
-    else work(0);
+    if (pool && parts > 1) pool->run(parts, work);
+    else
+        for (int k = 0; k < parts; ++k) work(k);
 }
 
 namespace {
@@ -496,6 +500,200 @@ void OutputSet::close() {
 
 namespace {
 
+// util::replace / basename / dirname / joinpath, reference src/util.h:121-250
+std::string home_path(const std::string& path) {
+    const char* h = std::getenv("HOME");
+    const std::string des = std::string(h ? h : "") + "/";
+    std::string ret;
+    size_t las = 0, cur = 0;
+    while ((cur = path.find('~', cur)) != std::string::npos) {
+        ret.append(path.substr(las, cur - las)).append(des);
+        las = ++cur;
+    }
+    return ret + path.substr(las);
+}
+
+std::string path_basename(const std::string& path) {
+    const std::string f = home_path(path);
+    if (f.find_first_of(" \t\n\v\f\r") != std::string::npos) return "";
+    const size_t p1 = f.find_last_of("/\\");
+    if (p1 == std::string::npos) return f;
+    const size_t p2 = f.find_last_not_of("/\\");
+    if (p2 == f.size() - 1) return f.substr(p1 + 1, p2 - p1);
+    const size_t p3 = f.find_last_of("/\\", p2);
+    if (p3 == std::string::npos) return f.substr(0, p2 + 1);
+    return f.substr(p3 + 1, p2 - p3);
+}
+
+std::string path_dirname(const std::string& path) {
+    const std::string f = home_path(path);
+    const size_t pos = f.find_last_of("/\\");
+    if (pos == std::string::npos) return "./";
+    if (pos == f.size() - 1) {
+        const size_t p1 = f.find_last_not_of("/\\");
+        if (p1 == std::string::npos) return "/";
+        const size_t p2 = f.find_last_of("/\\", p1);
+        return p2 == std::string::npos ? "./" : f.substr(0, p2 + 1);
+    }
+    return f.substr(0, pos + 1);
+}
+
+}  // namespace
+
+// The split outputs of -s / -S: ThreadConfig::initWriterForSplit / markProcessed /
+// writeEmptyFilesForSplitting (src/threadconfig.cpp:88-137) with the reference's packs of
+// --max_item_in_pack pairs.  Worker t of -w T writes files t+1, t+1+T, ... (4-digit prefix,
+// src/options.h:272); a pack's passing pairs go to its worker's current file, then the worker
+// moves on once it has seen split_size pairs (-s: packed pairs; -S: passed pairs).  With -w 1
+// (the reference's deterministic setting) this is the reference's output; with more workers the
+// packs are dealt round-robin over the workers still running, one schedule the reference can take.
+// Unpaired / failed / merged outputs are not written in split mode (PairEndProcessor::process
+// skips initOutput).
+class SplitSink {
+   public:
+    SplitSink(const Options& o, Pool* pool) : o_(o), pool_(pool), T_(std::max(1, o.threads)), th_((size_t)T_) {
+        for (int t = 0; t < T_; ++t) {
+            th_[(size_t)t].working = t;
+            open(t);
+        }
+    }
+    void write(const Pack& pk, const fq_read_result* res, uint64_t first) {
+        const uint64_t P = std::max<uint64_t>(1, o_.max_reads_in_pack);
+        std::vector<int> cuts{0};
+        for (int i = 0; i < pk.n;) {  // blocks never straddle a reference pack
+            const uint64_t g = first + (uint64_t)i;
+            const int end = (int)std::min<uint64_t>((uint64_t)pk.n, (g / P + 1) * P - first);
+            const int step = std::min(end - i, 16384);
+            i += step;
+            cuts.push_back(i);
+        }
+        PackOutput out;
+        format_pack(o_, pk, res, out, pool_, &cuts);
+        for (size_t j = 0; j + 1 < cuts.size(); ++j) {
+            const uint64_t ref = (first + (uint64_t)cuts[j]) / P;
+            if (!have_ref_ || ref != ref_) {
+                finish_ref();
+                start_ref(ref);
+            }
+            Worker& w = th_[(size_t)t_];
+            if (w.w1) w.w1->write(std::vector<std::string>{std::move(out.out1[j])}, pool_);
+            if (w.w2) w.w2->write(std::vector<std::string>{std::move(out.out2[j])}, pool_);
+            count_ += (uint64_t)(cuts[j + 1] - cuts[j]);
+            passed_ += passed(pk, res, cuts[j], cuts[j + 1]);
+        }
+    }
+    void close() {
+        finish_ref();
+        for (int t = 0; t < T_; ++t) {
+            Worker& w = th_[(size_t)t];
+            if (o_.split_by_number)  // writeEmptyFilesForSplitting
+                while (w.working + T_ < o_.split_number) {
+                    w.working += T_;
+                    open(t);
+                }
+            if (w.w1) w.w1->close();
+            if (w.w2) w.w2->close();
+            w.w1.reset();
+            w.w2.reset();
+        }
+    }
+
+   private:
+    struct Worker {
+        int working = 0;
+        uint64_t cur = 0;
+        bool stopped = false;
+        std::unique_ptr<Writer> w1, w2;
+    };
+    // readPassed of the loop bodies (src/peprocessor.cpp:380-403, src/seprocessor.cpp:341-345)
+    uint64_t passed(const Pack& pk, const fq_read_result* res, int i0, int i1) const {
+        uint64_t n = 0;
+        auto ok = [](const fq_read_result& r) { return !(r.flags & (FQ_RF_NULL | FQ_RF_INDEX_FILTERED)) && r.code == FQ_PASS_FILTER; };
+        for (int i = i0; i < i1; ++i)
+            n += pk.paired ? (ok(res[2 * (size_t)i]) && ok(res[2 * (size_t)i + 1])) : ok(res[i]);
+        return n;
+    }
+    void open(int t) {  // initWriterForSplit
+        Worker& w = th_[(size_t)t];
+        if (w.w1) w.w1->close();
+        if (w.w2) w.w2->close();
+        w.w1.reset();
+        w.w2.reset();
+        std::string num = std::to_string(w.working + 1);
+        while (num.size() < 4) num = "0" + num;
+        w.w1.reset(new Writer(path_dirname(o_.out1) + "/" + num + "." + path_basename(o_.out1), o_.compression));
+        if (o_.paired())
+            w.w2.reset(new Writer(path_dirname(o_.out2) + "/" + num + "." + path_basename(o_.out2), o_.compression));
+    }
+    void start_ref(uint64_t ref) {
+        for (int k = 0; k < T_; ++k) {  // the next worker still taking packs
+            const int t = (next_ + k) % T_;
+            if (!th_[(size_t)t].stopped) {
+                t_ = t;
+                next_ = (t + 1) % T_;
+                break;
+            }
+        }
+        ref_ = ref;
+        have_ref_ = true;
+        count_ = passed_ = 0;
+    }
+    void finish_ref() {  // markProcessed
+        if (!have_ref_) return;
+        have_ref_ = false;
+        Worker& w = th_[(size_t)t_];
+        w.cur += o_.split_by_lines ? passed_ : count_;
+        if (w.cur >= o_.split_size) {
+            if (o_.split_by_lines || w.working + T_ < o_.split_number) {
+                w.working += T_;
+                open(t_);
+                w.cur = 0;
+            } else if (o_.split_number % T_ > 0 && t_ >= o_.split_number % T_) {
+                w.stopped = true;
+            }
+        }
+    }
+    const Options& o_;
+    Pool* pool_;
+    int T_;
+    std::vector<Worker> th_;
+    int t_ = 0, next_ = 0;
+    uint64_t ref_ = 0, count_ = 0, passed_ = 0;
+    bool have_ref_ = false;
+};
+
+Sink::Sink(const Options& o, Pool* pool) : o_(o), pool_(pool) {
+    if (o.split()) split_.reset(new SplitSink(o, pool));
+    else outs_.reset(new OutputSet(o, pool));
+}
+
+Sink::~Sink() {
+    try {
+        close();
+    } catch (...) {
+    }
+}
+
+void Sink::consume(const Pack& pk, const fq_read_result* res) {
+    if (split_) {
+        split_->write(pk, res, pairs_);
+    } else {
+        PackOutput out;
+        format_pack(o_, pk, res, out, pool_);
+        outs_->write(std::move(out));
+    }
+    pairs_ += (uint64_t)pk.n;
+}
+
+void Sink::close() {
+    if (split_) split_->close();
+    if (outs_) outs_->close();
+    split_.reset();
+    outs_.reset();
+}
+
+namespace {
+
 // One engine per entry of --devices (several may share a GPU).  All have the same geometry;
 // a pack with longer reads (or more of them) re-creates them larger after draining them.
 struct Engines {
@@ -561,6 +759,13 @@ Options prepare_options(int argc, char** argv) {
     // Evaluator pre-pass, src/main.cpp:126-143
     if (!o.in1.empty()) o.est_seq_len1 = evaluate_read_len(o.in1);
     if (!o.in2.empty()) o.est_seq_len2 = evaluate_read_len(o.in2);
+    if (o.split_by_number) {  // evaluateReadNum + the split size, src/main.cpp:130-134
+        o.est_reads_num = evaluate_read_num(o.in1);
+        if (o.split_number == 0) throw std::runtime_error("--split_file_number must be given (non-zero) with -s");
+        o.split_size = (size_t)std::max(o.est_reads_num / o.split_number, 1);
+    }
+    if (o.split() && o.paired() && o.out2.empty())  // the reference dereferences a null split writer
+        throw std::runtime_error("split output of paired-end reads needs both -o and -O");
     if (o.detect_pe_adapter) {
         // the two mates' detections run concurrently; their read errors are printed in the
         // reference's order (read 1's first; read 2's only when read 1's detection succeeded).
@@ -615,7 +820,7 @@ int run_tool(int argc, char** argv) {
         make_engines(eng, o, std::max(16, round16(o.merge ? 2 * est : est)), (int)pack_n, round16(std::max(est, 16)));
         // -w host threads (the reference's worker count) pack tiles, format and compress
         Pool pool(std::max(0, o.threads - 1));
-        OutputSet outs(o, &pool);
+        Sink outs(o, &pool);
         // reader thread -> dispatcher (this thread: submit to engine seq_no mod G, poll in
         // submission order) -> formatter thread (records -> output text, in input order) ->
         // writer threads.  Packs (pinned planes and records) are recycled.
@@ -655,10 +860,8 @@ int run_tool(int argc, char** argv) {
                     const fq_params p = o.to_params(eng.max_cycles);
                     apply_corrections(o, *pk, pk->res.data(), &pool);
                     if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p, &pool);
-                    PackOutput out;
-                    format_pack(o, *pk, pk->res.data(), out, &pool);
+                    outs.consume(*pk, pk->res.data());
                     format_s += since(f0);
-                    outs.write(std::move(out));
                     reads += (uint64_t)pk->n * (paired ? 2 : 1);
                     spare.push(std::move(pk));
                 }

@@ -42,8 +42,29 @@ class OutputSet {
 
 // Builds the output text of one processed pack from the engine's per-read records, exactly as
 // the loop body of processPairEnd / processSingleEnd appends to its strings.
-// With a pool, ranges of the pack are formatted in parallel into consecutive blocks.
-void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out, Pool* pool = nullptr);
+// With a pool, ranges of the pack are formatted in parallel into consecutive blocks; `cuts`
+// (optional, ascending, 0 .. n) fixes the block boundaries.
+void format_pack(const Options& o, const Pack& pk, const fq_read_result* res, PackOutput& out, Pool* pool = nullptr,
+                 const std::vector<int>* cuts = nullptr);
+
+class SplitSink;
+
+// Where a run's output goes: the regular files (OutputSet), or with -s / -S the numbered split
+// files of ThreadConfig (src/threadconfig.cpp:88-137).  Packs must arrive in input order.
+class Sink {
+   public:
+    Sink(const Options& o, Pool* pool);
+    ~Sink();
+    void consume(const Pack& pk, const fq_read_result* res);  // format + write one processed pack
+    void close();
+
+   private:
+    const Options& o_;
+    Pool* pool_;
+    std::unique_ptr<OutputSet> outs_;
+    std::unique_ptr<SplitSink> split_;
+    uint64_t pairs_ = 0;  // pairs (reads) consumed so far: the next pack's first global index
+};
 
 // Before the engine call: per-pair index-filter flags (Filter::filterByIndex) when enabled.
 void prepare_pack(const Options& o, Pack& pk, Pool* pool = nullptr);

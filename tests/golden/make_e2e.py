@@ -119,6 +119,15 @@ CASES = {
     "synth_pe_index_all": "-i {in}/synth_r1.fq.gz -I {in}/synth_r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q "
                           "--enable_index_filter --index2_file {in}/idx_empty_line.txt",
     "td_pe_index_nofile": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q --enable_index_filter",
+    # split output (-s by file number from the evaluator's read-count estimate, -S by passed reads)
+    "td_pe_split_num": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -a -g -s "
+                       "--split_file_number 3 --max_item_in_pack 3000",
+    "td_pe_split_num_gz": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq.gz -O {out}/o2.fq.gz -q -s "
+                          "--split_file_number 4 --max_item_in_pack 1000 --failed_out {out}/failed.fq",
+    "td_se_split_num_many": "-i {in}/r1.fq.gz -o {out}/o1.fq -q -s --split_file_number 9 --max_item_in_pack 4000",
+    "td_se_split_lines": "-i {in}/r1.fq.gz -o {out}/o1.fq -q -S --splie_file_line 2000 --max_item_in_pack 1500",
+    "synth_pe_split_lines": "-i {in}/synth_r1.fq.gz -I {in}/synth_r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -a -g "
+                            "-S --splie_file_line 500 --max_item_in_pack 400 --digits_file_name 2",
     "err_index_bad": "-i {in}/r1.fq.gz -o {out}/o1.fq --enable_index_filter --index1_file {in}/idx_bad.txt",
     "err_umi_len0": "-i {in}/r1.fq.gz -o {out}/o1.fq -u --umi_location 3",
     # validation / CLI failures: exit status only (messages are compared for validate errors)
@@ -137,9 +146,6 @@ CASES = {
     "err_size_range": "-i {in}/r1.fq.gz -o {out}/o1.fq --max_item_in_pack -5",
     "err_missing_value": "-i {in}/r1.fq.gz -o {out}/o1.fq -q -w 1 -Q",
 }
-
-OUTPUT_NAMES = ["o1.fq", "o2.fq", "o1.fq.gz", "o2.fq.gz", "u1.fq", "u2.fq", "u.fq", "failed.fq", "merged.fq"]
-
 
 def make_inputs():
     os.makedirs(INP, exist_ok=True)
@@ -218,10 +224,9 @@ def run_case(binary, name, args, workdir, extra=()):
     argv += list(extra) + args.format(**{"in": INP, "out": out}).split()
     p = subprocess.run(argv, cwd=out, capture_output=True, timeout=600)
     res = {"args": args, "exit": p.returncode, "outputs": {}}
-    for o in OUTPUT_NAMES:
-        fp = os.path.join(out, o)
-        if os.path.exists(fp):
-            res["outputs"][o] = digest(fp)
+    for o in sorted(os.listdir(out)):  # every output file but the reports
+        if not o.startswith("report."):
+            res["outputs"][o] = digest(os.path.join(out, o))
     js = os.path.join(out, "report.json")
     res["json"] = open(js).read() if os.path.exists(js) and p.returncode == 0 else None
     # error text of a failed run (CLI11 message or util::errorExit line), with paths relative

@@ -35,7 +35,8 @@ def test_host_pipeline_threaded(case, host, oracle, tmp_path):
     run on the host pool; outputs and JSON must not change."""
     argv = E.argv_for("fqtool", case, str(tmp_path))
     assert argv[1:3] == ["-w", "1"]
-    argv[2] = "4"
+    if not E.is_split(case):  # with -s / -S, -w is the number of file sequences
+        argv[2] = "4"
     report = E.run_session_with_oracle(host, oracle, argv, max_n=700)
     E.check_outputs(case, str(tmp_path), report)
 
@@ -73,9 +74,38 @@ def test_fqtool_multi_engine_matches_reference(case, tmp_path):
     reorders by pack sequence number and the accumulators are summed, so the FASTQ and JSON
     must still equal the reference's -w 1 outputs."""
     argv = E.argv_for(abi.FQTOOL_BIN, case, str(tmp_path))
-    argv[2] = "4"
+    if not E.is_split(case):
+        argv[2] = "4"
     argv += ["--devices", "0,0,0", "--pack_pairs", "777"]
     p = subprocess.run(argv, capture_output=True, cwd=tmp_path, timeout=300)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     assert "on 3 engine(s)" in p.stderr.decode()
     E.check_outputs(case, str(tmp_path))
+
+
+@pytest.mark.parametrize("case", ["td_pe_split_num", "td_se_split_lines", "td_se_split_num_many"])
+def test_split_with_several_workers(case, host, oracle, tmp_path):
+    """-s / -S with -w 3: each worker writes its own file sequence (t+1, t+1+3, ...; the
+    reference's ThreadConfig).  Whatever the schedule, the files together hold exactly the
+    records of the -w 1 run, each file a run of whole packs in input order."""
+    import glob
+
+    one, three = tmp_path / "w1", tmp_path / "w3"
+    one.mkdir()
+    three.mkdir()
+    E.run_session_with_oracle(host, oracle, E.argv_for("fqtool", case, str(one)))
+    argv = E.argv_for("fqtool", case, str(three))
+    argv[2] = "3"
+    E.run_session_with_oracle(host, oracle, argv)
+
+    def records(d, mate):
+        out = []
+        for f in sorted(glob.glob(str(d / ("*." + mate)))):
+            lines = open(f, "rb").read().split(b"\n")[:-1]
+            out += [b"\n".join(lines[k:k + 4]) for k in range(0, len(lines), 4)]
+        return out
+
+    for mate in ("o1.fq", "o2.fq"):
+        assert sorted(records(one, mate)) == sorted(records(three, mate))
+    names = sorted(os.path.basename(f) for f in glob.glob(str(three / "0*")))
+    assert names[0].startswith("0001.") and len(names) >= len(glob.glob(str(one / "0*")))
