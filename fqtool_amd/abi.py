@@ -221,6 +221,12 @@ def load_engine(path=ENGINE_LIB):
     lib.fq_engine_pending.argtypes = [vp]
     lib.fq_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
     lib.fq_host_free.argtypes = [vp]
+    lib.fq_dup_create.argtypes = [ctypes.c_int, i32, ctypes.POINTER(vp)]
+    lib.fq_dup_destroy.argtypes = [vp]
+    lib.fq_dup_reset.argtypes = [vp]
+    lib.fq_engine_set_dup.argtypes = [vp, vp]
+    lib.fq_dup_merge.argtypes = [vp, vp]
+    lib.fq_dup_stat.argtypes = [vp, i32, vp, vp, vp]
     return lib
 
 
@@ -229,7 +235,8 @@ ENGINE_SYMBOLS = [
     "fq_engine_acc_words", "fq_engine_acc_device_ptr", "fq_engine_read_acc", "fq_engine_reset_acc",
     "fq_engine_sync", "fq_engine_set_acc_buffer", "fq_engine_last_error", "fq_engine_device_info", "fq_synth_fill_device",
     "fq_engine_last_kernel_ms", "fq_engine_submit", "fq_engine_poll", "fq_engine_pending", "fq_host_alloc",
-    "fq_host_free",
+    "fq_host_free", "fq_dup_create", "fq_dup_destroy", "fq_dup_reset", "fq_engine_set_dup", "fq_dup_merge",
+    "fq_dup_stat",
 ]
 
 
@@ -254,6 +261,8 @@ def load_host(path=HOST_LIB):
     lib.fqh_session_next.argtypes = [vp, ci, ctypes.POINTER(FqBatch)]
     lib.fqh_session_consume.argtypes = [vp, vp, ci]
     lib.fqh_session_add_acc.argtypes = [vp, vp, ci]
+    lib.fqh_session_dup_params.argtypes = [vp, ctypes.POINTER(ci), ctypes.POINTER(ci), ctypes.POINTER(ci)]
+    lib.fqh_session_set_dup.argtypes = [vp, vp, vp, vp]
     lib.fqh_session_finish.argtypes = [vp]
     lib.fqh_session_finish.restype = vp
     lib.fqh_session_close.argtypes = [vp]
@@ -273,5 +282,5 @@ HOST_SYMBOLS = [
     "fqh_run", "fqh_json_double", "fqh_merged_name", "fqh_evaluate_read_len", "fqh_detect_adapter",
     "fqh_report_json", "fqh_free", "fqh_session_open", "fqh_session_error", "fqh_session_params",
     "fqh_session_next", "fqh_session_consume", "fqh_session_add_acc", "fqh_session_finish",
-    "fqh_session_close", "fqh_debug_records",
+    "fqh_session_close", "fqh_debug_records", "fqh_session_dup_params", "fqh_session_set_dup",
 ]

@@ -61,6 +61,8 @@ struct fq_engine {
     bool fast = false;  // pe_fast kernel usable for these params
     Scratch scratch;    // hand-off list of fq_engine_process_device
     bool timed = false;
+    fq_dup* dup = nullptr;    // duplication table fed by every pack (-d)
+    uint64_t calls = 0;       // order of process / process_device packs for the table
     std::string last_error;
 };
 
@@ -228,8 +230,12 @@ static int grid_for(const fq_engine* e, int n) {
 // Enqueues the kernels of one batch on stream s.  `sc` is the hand-off list of this launch; it
 // must not be shared with a launch that can run concurrently (different stream).
 static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStream_t s, Scratch& sc, bool timed,
-                  bool sync_device_on_grow) {
+                  bool sync_device_on_grow, uint64_t order) {
     if (db.n <= 0) return FQ_OK;
+    if (e->dup) {  // Duplicate::statPair / statRead run on the untrimmed reads (src/peprocessor.cpp:279-281)
+        const int rc = fq_dup_pack(e->dup, db, e->p.paired, order, s);
+        if (rc != FQ_OK) return fail(e, rc, std::string("duplication analysis: ") + fq_dup_error(e->dup));
+    }
     // per-pair flags (index filter) run on the general kernel
     if (e->fast && !db.flags) {
         const size_t ntiles = ((size_t)db.n + 31) / 32 + 1;  // single-end 64-read tiles enter as two
@@ -335,7 +341,7 @@ int fq_engine_submit(fq_engine* e, const fq_batch* hb, fq_read_result* results, 
     HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
     // kernels on the compute stream (one accumulator: the packs' kernels run in order)
     HIP_TRY(e, hipStreamWaitEvent(e->stream, s.ev_in, 0));
-    if ((rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false)) != FQ_OK) return rc;
+    if ((rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false, seq_no)) != FQ_OK) return rc;
     HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
     // D2H of the records (and of the error flag) on the copy-out stream
     HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
@@ -393,10 +399,23 @@ int fq_engine_process_device(fq_engine* e, const fq_batch* db, fq_read_result* d
         return fail(e, FQ_E_INVALID, "bad device batch");
     HIP_TRY(e, hipSetDevice(e->device));
     // NULL is the HIP default stream
-    return launch(e, *db, dres, (hipStream_t)stream, e->scratch, true, true);
+    return launch(e, *db, dres, (hipStream_t)stream, e->scratch, true, true, e->calls++);
 }
 
 size_t fq_engine_acc_words(const fq_engine* e) { return e ? e->acc_words : 0; }
+
+int fq_engine_set_dup(fq_engine* e, fq_dup* d) {
+    if (!e) return FQ_E_INVALID;
+    if (d) {
+        int dev = -1;
+        if (fq_dup_device(d, &dev) != FQ_OK || dev != e->device)
+            return fail(e, FQ_E_INVALID, "the duplication table is on another device");
+    }
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());  // packs in flight finish with the old table
+    e->dup = d;
+    return FQ_OK;
+}
 
 int fq_engine_acc_device_ptr(fq_engine* e, uint64_t** dptr) {
     if (!e || !dptr) return FQ_E_INVALID;

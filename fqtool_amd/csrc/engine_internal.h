@@ -18,3 +18,8 @@ hipError_t fq_pe_fast_prepare();
 hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
                              int* slow_tiles, int* slow_count, int grid, hipStream_t stream);
 hipError_t fq_launch_synth(const fq_batch& b, uint64_t seed, uint64_t first_index, int read_len, hipStream_t stream);
+// Duplication analysis of one pack into a table (dup.hip); order_base orders the pack's reads
+// against other packs (the pack's sequence number).
+int fq_dup_pack(fq_dup* d, const fq_batch& b, int paired, unsigned long long order_base, hipStream_t s);
+const char* fq_dup_error(const fq_dup* d);
+int fq_dup_device(const fq_dup* d, int* device);

@@ -165,6 +165,20 @@ int fqh_session_consume(fqh_session* s, const fq_read_result* res, int max_cycle
     }
 }
 
+// -d: what the caller's duplication analysis needs, and its statAll result
+int fqh_session_dup_params(fqh_session* s, int* enabled, int* keylen, int* hist_size) {
+    *enabled = s->o.dup;
+    *keylen = s->o.dup_keylen;
+    *hist_size = s->o.dup_hist_size;
+    return 0;
+}
+
+int fqh_session_set_dup(fqh_session* s, const uint64_t* hist, const uint64_t* gc_sum, const uint64_t* totals) {
+    const size_t n = (size_t)s->o.dup_hist_size;
+    s->acc.set_dup(std::vector<uint64_t>(hist, hist + n), std::vector<uint64_t>(gc_sum, gc_sum + n), totals[0], totals[1]);
+    return 0;
+}
+
 int fqh_session_add_acc(fqh_session* s, const uint64_t* acc, int max_cycles) {
     s->acc.add(acc, max_cycles);
     return 0;

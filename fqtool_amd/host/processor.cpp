@@ -699,8 +699,12 @@ namespace {
 struct Engines {
     std::vector<int> devices;
     std::vector<fq_engine*> e;
+    std::vector<fq_dup*> dup;  // -d: one table per engine slot, kept across re-creation
     int max_cycles = 0, max_batch = 0, max_stride = 0;
-    ~Engines() { destroy(); }
+    ~Engines() {
+        destroy();
+        for (fq_dup* d : dup) fq_dup_destroy(d);
+    }
     void destroy() {
         for (fq_engine* x : e) fq_engine_destroy(x);
         e.clear();
@@ -718,6 +722,17 @@ void make_engines(Engines& en, const Options& o, int max_cycles, int max_batch, 
         if (rc != FQ_OK)
             throw std::runtime_error("fq_engine_create (device " + std::to_string(dev) + "): " + fq_engine_last_error(nullptr));
         en.e.push_back(x);
+        if (o.dup) {
+            const size_t g = en.e.size() - 1;
+            if (en.dup.size() <= g) {
+                fq_dup* d = nullptr;
+                if (fq_dup_create(dev, o.dup_keylen, &d) != FQ_OK)
+                    throw std::runtime_error("fq_dup_create (device " + std::to_string(dev) + ") failed");
+                en.dup.push_back(d);
+            }
+            if (fq_engine_set_dup(x, en.dup[g]) != FQ_OK)
+                throw std::runtime_error(std::string("fq_engine_set_dup: ") + fq_engine_last_error(x));
+        }
     }
     en.max_cycles = max_cycles;
     en.max_batch = max_batch;
@@ -931,6 +946,15 @@ int run_tool(int argc, char** argv) {
         if (format_err) std::rethrow_exception(format_err);
         if (reader_err) std::rethrow_exception(reader_err);
         drain(eng, acc);
+        if (o.dup) {  // Duplicate::statAll over the merged tables, src/peprocessor.cpp:200-207
+            for (size_t g = 1; g < eng.dup.size(); ++g)
+                if (fq_dup_merge(eng.dup[0], eng.dup[g]) != FQ_OK) throw std::runtime_error("fq_dup_merge failed");
+            std::vector<uint64_t> hist((size_t)o.dup_hist_size), gcs((size_t)o.dup_hist_size);
+            uint64_t tot[2] = {0, 0};
+            if (fq_dup_stat(eng.dup[0], o.dup_hist_size, hist.data(), gcs.data(), tot) != FQ_OK)
+                throw std::runtime_error("fq_dup_stat failed");
+            acc.set_dup(hist, gcs, tot[0], tot[1]);
+        }
         outs.close();
         const Json rep = build_report(o, acc, ac);
         std::ofstream js(o.json_file, std::ios::binary);

@@ -201,6 +201,21 @@ Json build_report(const Options& o, const HostAcc& a, const AdapterCounts& ac) {
     }
     rep["FilterResult"] = fr;
 
+    if (o.dup) {  // src/jsonreporter.cpp:99-108 with Duplicate::statAll's results
+        Json d = Json::object();
+        d["Rate"] = Json::d(a.dup_total == 0 ? 0.0 : (double)a.dup_dups / (double)a.dup_total);
+        Json h = Json::array(), g = Json::array();
+        for (int i = 0; i < o.dup_hist_size; ++i) {
+            const uint64_t n = i < (int)a.dup_hist.size() ? a.dup_hist[(size_t)i] : 0;
+            const uint64_t gs = i < (int)a.dup_gc_sum.size() ? a.dup_gc_sum[(size_t)i] : 0;
+            h.push(Json::i((int32_t)n));
+            g.push(Json::d((int)n > 0 ? (double)gs / 255.0 / (int)n : 0.0));
+        }
+        d["Histogram"] = h;
+        d["MeanGC"] = g;
+        rep["Duplication"] = d;
+    }
+
     if (paired) {  // insert size, src/jsonreporter.cpp:107-114 + getPeakInsertSize src/peprocessor.cpp:249-259
         const int ism = a.insert_size_max();
         Json ins = Json::object();

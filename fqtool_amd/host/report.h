@@ -33,9 +33,15 @@ class HostAcc {
     uint64_t cyc(int k, int c, int slot) const { return (size_t)c < cyc_[k].size() / 16 ? cyc_[k][(size_t)c * 16 + slot] : 0; }
     int insert_size_max() const { return ism_; }
     uint64_t tail(int k) const { return tail_[k]; }  // FQ_ACC_TAIL_*
-    // duplication analysis result (Duplicate::statAll), filled by the engine caller
+    // duplication analysis result (Duplicate::statAll: bins, GC sums, reads counted, duplicates)
+    void set_dup(const std::vector<uint64_t>& hist, const std::vector<uint64_t>& gc_sum, uint64_t total, uint64_t dups) {
+        dup_hist = hist;
+        dup_gc_sum = gc_sum;
+        dup_total = total;
+        dup_dups = dups;
+    }
     std::vector<uint64_t> dup_hist, dup_gc_sum;
-    double dup_rate = 0;
+    uint64_t dup_total = 0, dup_dups = 0;
 
    private:
     int ism_;

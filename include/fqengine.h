@@ -376,6 +376,24 @@ int fq_engine_device_info(const fq_engine* e, int* device, char* arch, size_t ar
 int fq_synth_fill_device(const fq_batch* device_batch, uint64_t seed, uint64_t first_index,
                          int32_t read_len, void* stream);
 
+/* ---- duplication analysis (-d) ----------------------------------------------------------
+ * Duplicate::statRead / statPair / statAll, reference src/duplicate.cpp:46-166.  A table lives
+ * on one device and outlives engines (the tool re-creates engines when reads grow); an engine
+ * with a table attached adds every later pack's reads to it, on its compute stream, in input
+ * order (packs are ordered by their seq_no; fq_engine_process / process_device use a per-engine
+ * call counter).  Tables of engines that processed interleaved packs of one input merge exactly
+ * (fq_dup_merge), since each key remembers the order of its first read.  fq_dup_stat returns
+ * statAll's histogram and GC sums (hist_size bins; a key seen more than hist_size times counts in
+ * the last bin; exactly hist_size lands past the reference's array and is not reported) and
+ * totals[0] = reads counted, totals[1] = duplicates (Rate = totals[1] / totals[0]). */
+typedef struct fq_dup fq_dup;
+int fq_dup_create(int device, int32_t keylen, fq_dup** out); /* keylen 1..31 (-dup_ana_key_len) */
+int fq_dup_destroy(fq_dup* d);
+int fq_dup_reset(fq_dup* d);
+int fq_engine_set_dup(fq_engine* e, fq_dup* d); /* NULL detaches; d must be on the engine's device */
+int fq_dup_merge(fq_dup* dst, const fq_dup* src);
+int fq_dup_stat(fq_dup* d, int32_t hist_size, uint64_t* hist, uint64_t* gc_sum, uint64_t* totals);
+
 /* Kernel timing of the engine's last process_device call (HIP events on the launch stream),
  * in milliseconds; 0 when unavailable. */
 double fq_engine_last_kernel_ms(const fq_engine* e);

@@ -51,6 +51,11 @@ int fqh_session_next(fqh_session* s, int max_n, fq_batch* out);
 /* per-read records of the current pack (fq_engine_process output) -> output files, written with
  * the tool's rules, and adapter string counts */
 int fqh_session_consume(fqh_session* s, const fq_read_result* res, int max_cycles);
+/* -d: whether the command line enables duplication analysis, its key length and histogram size;
+ * the caller runs it (fq_dup_* on the engine's device) and hands statAll's result back
+ * (hist_size bins, GC sums, totals = {reads counted, duplicates}) before fqh_session_finish */
+int fqh_session_dup_params(fqh_session* s, int* enabled, int* keylen, int* hist_size);
+int fqh_session_set_dup(fqh_session* s, const uint64_t* hist, const uint64_t* gc_sum, const uint64_t* totals);
 /* adds an accumulator block (fq_engine_read_acc layout at max_cycles) */
 int fqh_session_add_acc(fqh_session* s, const uint64_t* acc, int max_cycles);
 /* closes the outputs, writes the JSON report file (-J) and returns its text (malloc'd, fqh_free) */

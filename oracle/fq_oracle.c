@@ -8,6 +8,8 @@
  */
 #include "fq_oracle.h"
 
+#include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #define ORC_MIN(a, b) ((a) < (b) ? (a) : (b))
@@ -600,6 +602,119 @@ static int process_pe(const fq_params* p, const fq_batch* b, fq_read_result* res
 int orc_process_batch(const fq_params* p, const fq_batch* b, fq_read_result* results, uint64_t* acc) {
     if (!p || !b || !results || !acc) return FQ_E_INVALID;
     return p->paired ? process_pe(p, b, results, acc) : process_se(p, b, results, acc);
+}
+
+/* ------------------------------------------------------------------------------------ *
+ * Duplicate, src/duplicate.cpp:3-166
+ * ------------------------------------------------------------------------------------ */
+struct orc_dup {
+    int keylen;
+    uint64_t keys;
+    uint64_t* dups;
+    uint32_t* counts;
+    uint8_t* gc;
+};
+
+orc_dup* orc_dup_create(int keylen) {
+    orc_dup* d = (orc_dup*)calloc(1, sizeof *d);
+    d->keylen = keylen;
+    d->keys = keylen >= 16 ? (1ull << 32) : (1ull << (2 * keylen)); /* keys are (uint32_t) truncated */
+    d->dups = (uint64_t*)calloc(d->keys, 8);
+    d->counts = (uint32_t*)calloc(d->keys, 4);
+    d->gc = (uint8_t*)calloc(d->keys, 1);
+    return d;
+}
+
+void orc_dup_destroy(orc_dup* d) {
+    if (!d) return;
+    free(d->dups);
+    free(d->counts);
+    free(d->gc);
+    free(d);
+}
+
+/* Duplicate::seq2int, src/duplicate.cpp:20-44 */
+static uint64_t dup_seq2int(const uint8_t* s, int start, int keylen, int* valid) {
+    uint64_t ret = 0;
+    for (int i = 0; i < keylen; ++i) {
+        ret <<= 2;
+        switch (s[start + i]) {
+            case 'A': ret += 0; break;
+            case 'T': ret += 1; break;
+            case 'C': ret += 2; break;
+            case 'G': ret += 3; break;
+            default: *valid = 0; return 0;
+        }
+    }
+    return ret;
+}
+
+/* Duplicate::addRecord, src/duplicate.cpp:46-69 */
+static void dup_add_record(orc_dup* d, uint32_t key, uint64_t kmer32, uint8_t gc) {
+    if (d->counts[key] == 0) {
+        d->counts[key] = 1;
+        d->dups[key] = kmer32;
+        d->gc[key] = gc;
+    } else if (d->dups[key] == kmer32) {
+        ++d->counts[key];
+    } else if (d->dups[key] > kmer32) {
+        d->dups[key] = kmer32;
+        d->counts[key] = 1;
+        d->gc[key] = gc;
+    }
+}
+
+void orc_dup_add_batch(orc_dup* d, const fq_batch* b, int paired) {
+    for (int i = 0; i < b->n; ++i) {
+        int l1 = b->len1[i];
+        const uint8_t* s1 = gather(0, b->seq1, b->stride, i, l1);
+        int valid = 1;
+        uint8_t gc = 0; /* uint8_t counter, as the reference's */
+        if (paired) { /* Duplicate::statPair, src/duplicate.cpp:101-130 */
+            int l2 = b->len2[i];
+            const uint8_t* s2 = gather(2, b->seq2, b->stride, i, l2);
+            if (l1 < 32 || l2 < 32) continue;
+            uint32_t key = (uint32_t)dup_seq2int(s1, 0, d->keylen, &valid);
+            if (!valid) continue;
+            uint64_t kmer32 = dup_seq2int(s2, 0, 32, &valid);
+            if (!valid) continue;
+            if (d->counts[key] == 0) {
+                for (int k = 0; k < l1; ++k) gc += s1[k] == 'C' || s1[k] == 'G';
+                for (int k = 0; k < l2; ++k) gc += s2[k] == 'C' || s2[k] == 'G';
+            }
+            gc = (uint8_t)round(255.0 * (double)gc / (double)(l1 + l2));
+            dup_add_record(d, key, kmer32, gc);
+        } else { /* Duplicate::statRead, src/duplicate.cpp:71-99 */
+            if (l1 < 32) continue;
+            int start2 = ORC_MAX(0, l1 - 32 - 5);
+            uint32_t key = (uint32_t)dup_seq2int(s1, 0, d->keylen, &valid);
+            if (!valid) continue;
+            uint64_t kmer32 = dup_seq2int(s1, start2, 32, &valid);
+            if (!valid) continue;
+            if (d->counts[key] == 0)
+                for (int k = 0; k < l1; ++k) gc += s1[k] == 'C' || s1[k] == 'G';
+            gc = (uint8_t)round(255.0 * (double)gc / (double)l1);
+            dup_add_record(d, key, kmer32, gc);
+        }
+    }
+}
+
+/* Duplicate::statAll, src/duplicate.cpp:132-166 (counts == hist_size land past the reference's
+ * arrays and are not reported) */
+void orc_dup_stat(const orc_dup* d, int hist_size, uint64_t* hist, uint64_t* gc_sum, uint64_t* totals) {
+    memset(hist, 0, (size_t)hist_size * 8);
+    memset(gc_sum, 0, (size_t)hist_size * 8);
+    totals[0] = totals[1] = 0;
+    for (uint64_t key = 0; key < d->keys; ++key) {
+        uint32_t count = d->counts[key];
+        if (count == 0) continue;
+        totals[0] += count;
+        totals[1] += count - 1;
+        int bin = count > (uint32_t)hist_size ? hist_size - 1 : (int)count;
+        if (bin >= hist_size) continue;
+        hist[bin] += 1;
+        gc_sum[bin] += d->gc[key];
+    }
 }
 
 /* ------------------------------------------------------------------------------------ *

@@ -58,6 +58,15 @@ void orc_stat_read(uint64_t* st, int max_cycles, const uint8_t* seq, const uint8
  * Returns FQ_OK, or FQ_E_TOO_LONG / FQ_E_INVALID. */
 int orc_process_batch(const fq_params* p, const fq_batch* b, fq_read_result* results, uint64_t* acc);
 
+/* Duplicate (src/duplicate.cpp:46-166): a table of 4^keylen (at most 2^32) keys; add_batch runs
+ * statPair (PE) / statRead (SE) on every read of a pack in order (before any filter, as the
+ * reference does); stat is statAll (hist / gc sums of hist_size bins, totals = reads, dups). */
+typedef struct orc_dup orc_dup;
+orc_dup* orc_dup_create(int keylen);
+void orc_dup_destroy(orc_dup* d);
+void orc_dup_add_batch(orc_dup* d, const fq_batch* b, int paired);
+void orc_dup_stat(const orc_dup* d, int hist_size, uint64_t* hist, uint64_t* gc_sum, uint64_t* totals);
+
 /* Synthetic workload generator (host twin of fq_synth_fill_device, bit-identical output). */
 void orc_synth_fill(const fq_batch* b, uint64_t seed, uint64_t first_index, int read_len);
 

@@ -41,6 +41,16 @@ def is_split(case):
     return " -s " in manifest()[case]["args"] + " " or " -S " in manifest()[case]["args"] + " "
 
 
+def mask_se_dup(text):
+    j = json.loads(text)
+    h = j.get("Duplication", {}).get("Histogram")
+    if h is not None:
+        half = len(h) // 2
+        j["Duplication"]["Histogram"] = h[:half] + [0] * (len(h) - half)
+        return json.dumps(j, indent=4)
+    return text
+
+
 def mask_software(text):
     text = re.sub(r'"CWD": "[^"]*"', '"CWD": ""', text)
     return re.sub(r'"Command": "[^"]*"', '"Command": ""', text)
@@ -74,6 +84,10 @@ def check_outputs(case, outdir, report_text=None):
             report_text = f.read()
     ref = mask_software(golden_json(case))
     got = mask_software(report_text)
+    if " -d" in m["args"] and " -I " not in m["args"] and "--in_fq_interleaved" not in m["args"]:
+        # SingleEndProcessor zeroes only sizeof(int) * histSize bytes of the size_t histogram
+        # (src/seprocessor.cpp:245): its upper half is uninitialised memory -- masked
+        ref, got = mask_se_dup(ref), mask_se_dup(got)
     if got != ref:
         a, b = json.loads(got), json.loads(ref)
         for k in sorted(set(a) | set(b)):
@@ -94,7 +108,26 @@ def oracle_process(orc):
     return process
 
 
-def run_session(host, argv, process, max_n=1500):
+class OracleDup:
+    """Duplicate (-d) on the CPU restatement, standing in for the engine's fq_dup table."""
+
+    def __init__(self, orc, keylen):
+        self.orc = orc
+        self.d = orc.orc_dup_create(keylen)
+
+    def add(self, b, paired):
+        self.orc.orc_dup_add_batch(self.d, ctypes.byref(b), int(paired))
+
+    def stat(self, hist_size):
+        hist, gcs, tot = np.zeros(hist_size, np.uint64), np.zeros(hist_size, np.uint64), np.zeros(2, np.uint64)
+        self.orc.orc_dup_stat(self.d, hist_size, hist.ctypes.data, gcs.ctypes.data, tot.ctypes.data)
+        return hist, gcs, tot
+
+    def close(self):
+        self.orc.orc_dup_destroy(self.d)
+
+
+def run_session(host, argv, process, max_n=1500, dup_engine=None):
     """The tool's host pipeline (libfqhost session API) with `process(params, batch, n_results,
     max_cycles) -> (results, accumulator)` standing in for the engine call."""
     enc = [a.encode() for a in argv]
@@ -105,6 +138,9 @@ def run_session(host, argv, process, max_n=1500):
         assert rc == 0, host.fqh_session_error(s)
         p0 = abi.FqParams()
         host.fqh_session_params(s, 16, ctypes.byref(p0))
+        dup_on, keylen, hist_size = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        host.fqh_session_dup_params(s, ctypes.byref(dup_on), ctypes.byref(keylen), ctypes.byref(hist_size))
+        dup = dup_engine(keylen.value) if dup_on.value else None
         while True:
             b = abi.FqBatch()
             r = host.fqh_session_next(s, max_n, ctypes.byref(b))
@@ -123,18 +159,25 @@ def run_session(host, argv, process, max_n=1500):
             mc = max(16, round16(need))
             p = abi.FqParams()
             host.fqh_session_params(s, mc, ctypes.byref(p))
+            if dup is not None:
+                dup.add(b, paired)
             res, acc = process(p, b, n * (2 if paired else 1), mc)
             assert host.fqh_session_consume(s, res.ctypes.data, mc) == 0, host.fqh_session_error(s)
             host.fqh_session_add_acc(s, acc.ctypes.data, mc)
+        if dup is not None:
+            hist, gcs, tot = dup.stat(hist_size.value)
+            host.fqh_session_set_dup(s, hist.ctypes.data, gcs.ctypes.data, tot.ctypes.data)
         return abi.take_string(host, host.fqh_session_finish(s))
     finally:
+        if dup is not None:
+            dup.close()
         host.fqh_session_close(s)
 
 
 def run_session_with_oracle(host, orc, argv, max_n=1500):
     """Host pipeline with the CPU oracle in the engine's place: checks the host side (parsing,
     packing, formatting, writers, report) on CPU."""
-    return run_session(host, argv, oracle_process(orc), max_n)
+    return run_session(host, argv, oracle_process(orc), max_n, dup_engine=lambda k: OracleDup(orc, k))
 
 
 def read_row(b, mate, i, length):

@@ -119,6 +119,17 @@ CASES = {
     "synth_pe_index_all": "-i {in}/synth_r1.fq.gz -I {in}/synth_r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q "
                           "--enable_index_filter --index2_file {in}/idx_empty_line.txt",
     "td_pe_index_nofile": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q --enable_index_filter",
+    # duplication analysis (-d)
+    "td_pe_dup": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -d -q -a -g",
+    "td_pe_dup_key13": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -d --dup_ana_key_len 13 "
+                       "--dup_ana_hist_size 8 -q",
+    "td_pe_dup_hist2": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -d --dup_ana_hist_size 2 "
+                       "--enable_index_filter --index1_file {in}/idx_a.txt",
+    "td_se_dup": "-i {in}/r1.fq.gz -o {out}/o1.fq -d -q",
+    "inter_pe_dup": "-i {in}/inter.fq --in_fq_interleaved -o {out}/o1.fq -d --dup_ana_hist_size 5",
+    "edge_pe_dup": "-i {in}/edge_r1.fq -I {in}/edge_r2.fq -o {out}/o1.fq -O {out}/o2.fq -d -q -a -g",
+    "synth_pe_dup": "-i {in}/synth_r1.fq.gz -I {in}/synth_r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -d -q -a -g -x "
+                    "--enable_cut_right",
     # split output (-s by file number from the evaluator's read-count estimate, -S by passed reads)
     "td_pe_split_num": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -a -g -s "
                        "--split_file_number 3 --max_item_in_pack 3000",

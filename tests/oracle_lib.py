@@ -37,6 +37,12 @@ def load_oracle():
     lib.orc_trim_by_sequence.argtypes = [cp, ci, cp, ci, ip]
     lib.orc_process_batch.argtypes = [P, ctypes.POINTER(abi.FqBatch), ctypes.c_void_p, ctypes.c_void_p]
     lib.orc_synth_fill.argtypes = [ctypes.POINTER(abi.FqBatch), ctypes.c_uint64, ctypes.c_uint64, ci]
+    vp = ctypes.c_void_p
+    lib.orc_dup_create.argtypes = [ci]
+    lib.orc_dup_create.restype = vp
+    lib.orc_dup_destroy.argtypes = [vp]
+    lib.orc_dup_add_batch.argtypes = [vp, ctypes.POINTER(abi.FqBatch), ci]
+    lib.orc_dup_stat.argtypes = [vp, ci, vp, vp, vp]
     lib.orc_sizeof_params.restype = ctypes.c_size_t
     lib.orc_sizeof_result.restype = ctypes.c_size_t
     assert lib.orc_sizeof_params() == ctypes.sizeof(abi.FqParams), "fq_params ABI mismatch"
