@@ -134,13 +134,16 @@ def run_session(host, argv, process, max_n=1500, dup_engine=None):
     arr = (ctypes.c_char_p * len(enc))(*enc)
     s = ctypes.c_void_p()
     rc = host.fqh_session_open(len(enc), arr, ctypes.byref(s))
+    dup = None
     try:
         assert rc == 0, host.fqh_session_error(s)
         p0 = abi.FqParams()
         host.fqh_session_params(s, 16, ctypes.byref(p0))
         dup_on, keylen, hist_size = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         host.fqh_session_dup_params(s, ctypes.byref(dup_on), ctypes.byref(keylen), ctypes.byref(hist_size))
-        dup = dup_engine(keylen.value) if dup_on.value else None
+        if dup_on.value:
+            assert dup_engine is not None, "-d needs a duplication engine"
+            dup = dup_engine(keylen.value)
         while True:
             b = abi.FqBatch()
             r = host.fqh_session_next(s, max_n, ctypes.byref(b))

@@ -67,7 +67,7 @@ def engine_vs_oracle(eng, orc, mode):
 def test_engine_matches_oracle_on_golden_inputs(case, mode, host, eng, oracle, tmp_path):
     try:
         report = E.run_session(host, E.argv_for("fqtool", case, str(tmp_path)), engine_vs_oracle(eng, oracle, mode),
-                               max_n=4000)
+                               max_n=4000, dup_engine=lambda k: E.OracleDup(oracle, k))
     finally:
         os.environ.pop("FQ_ENGINE_GENERAL_ONLY", None)
     E.check_outputs(case, str(tmp_path), report)
