@@ -197,6 +197,10 @@ char* fqh_session_finish(fqh_session* s) {
         std::ofstream js(s->o.json_file, std::ios::binary);
         js << t;
     }
+    {
+        std::ofstream hs(s->o.html_file, std::ios::binary);
+        hs << build_html(s->o, s->acc, s->ac, html_time_now());
+    }
     char* r = (char*)std::malloc(t.size() + 1);
     std::memcpy(r, t.c_str(), t.size() + 1);
     return r;

@@ -957,14 +957,19 @@ int run_tool(int argc, char** argv) {
         }
         outs.close();
         const Json rep = build_report(o, acc, ac);
-        std::ofstream js(o.json_file, std::ios::binary);
-        js << rep.dump(4);
+        {
+            std::ofstream js(o.json_file, std::ios::binary);
+            js << rep.dump(4);
+        }
+        {  // HtmlReporter::report, src/peprocessor.cpp:214-217 (always written; -H names the file)
+            std::ofstream hs(o.html_file, std::ios::binary);
+            hs << build_html(o, acc, ac, html_time_now());
+        }
         log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s), wall " +
             std::to_string(since(t0)) + " s, engine submit/wait " + std::to_string(engine_s) + " s; pre-pass " +
             std::to_string(prepass_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +
             " s, tiles " + std::to_string(tiles_s) + " s, reader waiting " + std::to_string(spare_wait_s) +
-            " s; JSON report " + o.json_file +
-            " (no HTML report in this build)");
+            " s; JSON report " + o.json_file + ", HTML report " + o.html_file);
     } catch (const std::exception& e) {
         std::cerr << "ERROR: " << e.what() << std::endl;
         return 255;

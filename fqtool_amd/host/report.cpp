@@ -56,13 +56,7 @@ void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_para
 
 namespace {
 
-// Stats::summarize + reportJson for one accumulator block (src/stats.cpp:147-228, :392-430)
-struct Summary {
-    uint64_t reads = 0, bases = 0, q20 = 0, q30 = 0, gc = 0, length_sum = 0;
-    int cycles = 0;
-    Json json;
-    int mean_length() const { return reads ? (int)(length_sum / reads) : 0; }
-};
+}  // namespace
 
 Summary summarize(const HostAcc& a, int k) {
     Summary s;
@@ -94,6 +88,8 @@ Summary summarize(const HostAcc& a, int k) {
         content_c += a.cyc(k, i, C);
     }
     s.gc = content_g + content_c;
+    for (int b = 0; b < 8; ++b)
+        for (int i = 0; i < s.cycles; ++i) s.base_contents[b] += a.cyc(k, i, b);
     Json qc = Json::object(), cc = Json::object();
     Json mean = Json::array();
     std::vector<double> meanv((size_t)s.cycles);
@@ -101,22 +97,29 @@ Summary summarize(const HostAcc& a, int k) {
         meanv[(size_t)i] = (double)total_qual(i) / (double)total_base(i);
         mean.push(Json::d(meanv[(size_t)i]));
     }
+    s.qual_curves[4] = meanv;
     const char names[5] = {'A', 'T', 'C', 'G', 'N'};
     const int cls[5] = {A, T, C, G, N};
     for (int j = 0; j < 5; ++j) {
         Json qv = Json::array(), cv = Json::array();
         for (int i = 0; i < s.cycles; ++i) {
             const uint64_t cnt = a.cyc(k, i, cls[j]);
-            qv.push(Json::d(cnt == 0 ? meanv[(size_t)i] : (double)a.cyc(k, i, 8 + cls[j]) / (double)cnt));
-            cv.push(Json::d((double)cnt / (double)total_base(i)));
+            const double q = cnt == 0 ? meanv[(size_t)i] : (double)a.cyc(k, i, 8 + cls[j]) / (double)cnt;
+            const double c = (double)cnt / (double)total_base(i);
+            if (j < 4) s.qual_curves[j].push_back(q);
+            s.content_curves[j].push_back(c);
+            qv.push(Json::d(q));
+            cv.push(Json::d(c));
         }
         if (names[j] != 'N') qc[std::string(1, names[j])] = qv;
         cc[std::string(1, names[j])] = cv;
     }
     qc["Mean"] = mean;
     Json gcv = Json::array();
-    for (int i = 0; i < s.cycles; ++i)
-        gcv.push(Json::d((double)(a.cyc(k, i, G) + a.cyc(k, i, C)) / (double)total_base(i)));
+    for (int i = 0; i < s.cycles; ++i) {
+        s.content_curves[5].push_back((double)(a.cyc(k, i, G) + a.cyc(k, i, C)) / (double)total_base(i));
+        gcv.push(Json::d(s.content_curves[5].back()));
+    }
     cc["GC"] = gcv;
     s.json["TotalReads"] = Json::u(s.reads);
     s.json["TotalBases"] = Json::u(s.bases);
@@ -127,6 +130,8 @@ Summary summarize(const HostAcc& a, int k) {
     s.json["ContentCurves"] = cc;
     return s;
 }
+
+namespace {
 
 // FilterResult::reportAdaptersJsonDetails, src/filterresult.cpp:231-251 (null when no adapters)
 Json adapter_details(const std::map<std::string, size_t>& m) {

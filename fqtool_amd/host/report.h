@@ -62,6 +62,23 @@ struct AdapterCounts {
     void add(const Pack& pk, const fq_read_result* res, const fq_params& p, Pool* pool = nullptr);
 };
 
+// Stats::summarize + reportJson for accumulator stats block k (src/stats.cpp:147-228, :392-430)
+struct Summary {
+    uint64_t reads = 0, bases = 0, q20 = 0, q30 = 0, gc = 0, length_sum = 0;
+    int cycles = 0;
+    uint64_t base_contents[8] = {};           // mBaseContents
+    std::vector<double> qual_curves[5];       // A, T, C, G, Mean
+    std::vector<double> content_curves[6];    // A, T, C, G, N, GC
+    Json json;
+    int mean_length() const { return reads ? (int)(length_sum / reads) : 0; }
+};
+Summary summarize(const HostAcc& a, int k);
+
 Json build_report(const Options& o, const HostAcc& acc, const AdapterCounts& ac);
+
+// HtmlReporter::report (src/htmlreporter.cpp:23-95): the whole HTML page; `now` is the footer's
+// time stamp (htmlutil::getCurrentSystemTime)
+std::string build_html(const Options& o, const HostAcc& acc, const AdapterCounts& ac, const std::string& now);
+std::string html_time_now();
 
 }  // namespace fqhost

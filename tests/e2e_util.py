@@ -56,6 +56,24 @@ def mask_software(text):
     return re.sub(r'"Command": "[^"]*"', '"Command": ""', text)
 
 
+def mask_html(text):
+    """The footer's time stamp and the Software rows (command line, cwd) vary per run."""
+    text = re.sub(r"Fqtool Report @ [^<]*", "Fqtool Report @ ", text)
+    text = re.sub(r'(<td class="col1">Command</td><td class="col2">)[^<]*', r"\1", text)
+    return re.sub(r'(<td class="col1">CWD</td><td class="col2">)[^<]*', r"\1", text)
+
+
+def mask_html_se_dup(text):
+    """SE duplication percentages come from the partly uninitialised histogram (see mask_se_dup)."""
+    return re.sub(r"(<script type=\"text/javascript\">var data=\[\{x:\[[^\]]*\],y:\[)[^\]]*(\],name: 'Read percent)"
+                  r"[^<]*", r"\1\2", text)
+
+
+def golden_html(case):
+    with gzip.open(os.path.join(E2E, manifest()[case]["html"]), "rt") as f:
+        return f.read()
+
+
 def golden_json(case):
     with gzip.open(os.path.join(E2E, manifest()[case]["json"]), "rt") as f:
         return f.read()
@@ -79,6 +97,16 @@ def check_outputs(case, outdir, report_text=None):
     for name, d in m["outputs"].items():
         assert present[name] == d, "%s: %s differs from the reference (%s vs %s lines)" % (
             case, name, present[name]["lines"], d["lines"])
+    if m.get("html"):
+        with open(os.path.join(outdir, "report.html")) as f:
+            got_html = mask_html(f.read())
+        ref_html = mask_html(golden_html(case))
+        if " -d" in m["args"] and " -I " not in m["args"] and "--in_fq_interleaved" not in m["args"]:
+            got_html, ref_html = mask_html_se_dup(got_html), mask_html_se_dup(ref_html)
+        if got_html != ref_html:
+            k = next(i for i in range(min(len(got_html), len(ref_html)) + 1) if got_html[i:i + 1] != ref_html[i:i + 1])
+            raise AssertionError("%s: HTML report differs at %d: ours ...%r... reference ...%r..." % (
+                case, k, got_html[max(0, k - 80):k + 80], ref_html[max(0, k - 80):k + 80]))
     if report_text is None:
         with open(os.path.join(outdir, "report.json")) as f:
             report_text = f.read()

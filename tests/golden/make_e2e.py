@@ -240,6 +240,8 @@ def run_case(binary, name, args, workdir, extra=()):
             res["outputs"][o] = digest(os.path.join(out, o))
     js = os.path.join(out, "report.json")
     res["json"] = open(js).read() if os.path.exists(js) and p.returncode == 0 else None
+    hf = os.path.join(out, "report.html")
+    res["html"] = open(hf).read() if os.path.exists(hf) and p.returncode == 0 else None
     # error text of a failed run (CLI11 message or util::errorExit line), with paths relative
     res["stderr"] = p.stderr.decode(errors="replace").replace(INP, "{in}").replace(out, "{out}") \
         if p.returncode != 0 else None
@@ -259,6 +261,10 @@ def main():
                 with gzip.GzipFile(os.path.join(OUT, name + ".json.gz"), "wb", compresslevel=9, mtime=0) as f:
                     f.write(r["json"].encode())
             r["json"] = (name + ".json.gz") if r["json"] is not None else None
+            if r["html"] is not None:
+                with gzip.GzipFile(os.path.join(OUT, name + ".html.gz"), "wb", compresslevel=9, mtime=0) as f:
+                    f.write(r["html"].encode())
+            r["html"] = (name + ".html.gz") if r["html"] is not None else None
             manifest[name] = r
             print(name, r["exit"], sorted(r["outputs"]), file=sys.stderr)
     with open(os.path.join(OUT, "manifest.json"), "w") as f:
