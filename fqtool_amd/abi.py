@@ -227,6 +227,10 @@ def load_engine(path=ENGINE_LIB):
     lib.fq_engine_set_dup.argtypes = [vp, vp]
     lib.fq_dup_merge.argtypes = [vp, vp]
     lib.fq_dup_stat.argtypes = [vp, i32, vp, vp, vp]
+    lib.fq_kmer_open.argtypes = [ctypes.c_int, vp, vp, i32, ctypes.POINTER(vp)]
+    lib.fq_kmer_close.argtypes = [vp]
+    lib.fq_kmer_count.argtypes = [vp, i32, i32, i32, vp]
+    lib.fq_kmer_find.argtypes = [vp, i32, i32, i32, ctypes.c_uint32, vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
     return lib
 
 
@@ -236,7 +240,7 @@ ENGINE_SYMBOLS = [
     "fq_engine_sync", "fq_engine_set_acc_buffer", "fq_engine_last_error", "fq_engine_device_info", "fq_synth_fill_device",
     "fq_engine_last_kernel_ms", "fq_engine_submit", "fq_engine_poll", "fq_engine_pending", "fq_host_alloc",
     "fq_host_free", "fq_dup_create", "fq_dup_destroy", "fq_dup_reset", "fq_engine_set_dup", "fq_dup_merge",
-    "fq_dup_stat",
+    "fq_dup_stat", "fq_kmer_open", "fq_kmer_close", "fq_kmer_count", "fq_kmer_find",
 ]
 
 
@@ -266,6 +270,7 @@ def load_host(path=HOST_LIB):
     lib.fqh_session_finish.argtypes = [vp]
     lib.fqh_session_finish.restype = vp
     lib.fqh_session_close.argtypes = [vp]
+    lib.fqh_set_kmer_backend.argtypes = [vp]
     lib.fqh_debug_records.argtypes = [ctypes.c_char_p, ci, ci, ci, ci]
     lib.fqh_debug_records.restype = vp
     return lib
@@ -283,4 +288,5 @@ HOST_SYMBOLS = [
     "fqh_report_json", "fqh_free", "fqh_session_open", "fqh_session_error", "fqh_session_params",
     "fqh_session_next", "fqh_session_consume", "fqh_session_add_acc", "fqh_session_finish",
     "fqh_session_close", "fqh_debug_records", "fqh_session_dup_params", "fqh_session_set_dup",
+    "fqh_set_kmer_backend",
 ]

@@ -38,7 +38,7 @@ int fqh_merged_name(const char* name, int len1, int len2, char* buf, size_t n) {
 
 int fqh_detect_adapter(const char* path, int trim_tail1, char* buf, size_t n) {
     try {
-        return copy_out(detect_adapter(path, trim_tail1), buf, n);
+        return copy_out(detect_adapter(path, trim_tail1, nullptr, 0), buf, n);
     } catch (...) {
         return -1;
     }
@@ -98,6 +98,8 @@ char* fqh_report_json(int argc, const char* argv_blob, const uint64_t* acc, int 
 }
 
 void fqh_free(char* p) { std::free(p); }
+
+void fqh_set_kmer_backend(const fqh_kmer_backend* b) { set_kmer_backend(b); }
 
 // ---- host session: the tool's pipeline with the per-pack engine call left to the caller ----
 struct fqh_session {

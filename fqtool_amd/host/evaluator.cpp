@@ -12,6 +12,7 @@
 #include <sstream>
 
 #include "fastq.h"
+#include "../../include/fqhost.h"
 
 namespace fqhost {
 namespace {
@@ -19,24 +20,6 @@ namespace {
 const char* const kKnownAdapters[] = {
 #include "known_adapters.inc"
 };
-
-// Evaluator::seq2int, src/evaluator.cpp:3-47
-int seq2int(const std::string& seq, int pos, int keylen, int last) {
-    auto code = [](char c) { return c == 'A' ? 0 : c == 'T' ? 1 : c == 'C' ? 2 : c == 'G' ? 3 : -1; };
-    if (last >= 0) {
-        const int mask = (1 << (keylen * 2)) - 1;
-        const int b = code(seq[pos + keylen - 1]);
-        if (b < 0) return -1;
-        return ((last << 2) & mask) + b;
-    }
-    int key = 0;
-    for (int i = pos; i < pos + keylen; ++i) {
-        const int b = code(seq[i]);
-        if (b < 0) return -1;
-        key = (key << 2) + b;
-    }
-    return key;
-}
 
 // Evaluator::int2seq, src/evaluator.cpp:49-59
 std::string int2seq(size_t val, int len) {
@@ -106,22 +89,48 @@ std::string match_known(const std::string& seq) {
     return "";
 }
 
-// Evaluator::getAdapterWithSeed, src/evaluator.cpp:392-426
-std::string adapter_with_seed(int seed, const std::vector<std::string>& reads, int keylen, int trim) {
+// The detection pre-pass's reads: bases back to back, read i = seq[off[i] .. off[i + 1])
+struct ReadSet {
+    std::string seq;
+    std::vector<uint32_t> off{0};
+    size_t size() const { return off.size() - 1; }
+};
+
+// k-mer work on the GPU (fq_kmer_*, kmer.hip) unless a caller registered another backend
+int gpu_open(int device, const uint8_t* seq, const uint32_t* off, int32_t n, void** out) {
+    fq_kmer_set* k = nullptr;
+    const int rc = fq_kmer_open(device, seq, off, n, &k);
+    *out = k;
+    return rc;
+}
+int gpu_close(void* h) { return fq_kmer_close(static_cast<fq_kmer_set*>(h)); }
+int gpu_count(void* h, int32_t keylen, int32_t first, int32_t tail, uint32_t* counts) {
+    return fq_kmer_count(static_cast<fq_kmer_set*>(h), keylen, first, tail, counts);
+}
+int gpu_find(void* h, int32_t keylen, int32_t first, int32_t tail, uint32_t seed, uint64_t* occ, size_t cap, size_t* n) {
+    return fq_kmer_find(static_cast<fq_kmer_set*>(h), keylen, first, tail, seed, occ, cap, n);
+}
+const fqh_kmer_backend kGpuKmer = {gpu_open, gpu_close, gpu_count, gpu_find};
+fqh_kmer_backend g_kmer = kGpuKmer;
+
+// Evaluator::getAdapterWithSeed, src/evaluator.cpp:392-426: the occurrences of the seed come from
+// the k-mer backend; the prefix trees do not depend on their order
+std::string adapter_with_seed(int seed, const ReadSet& reads, void* kset, uint32_t seed_count, int keylen, int trim) {
     const int shift_tail = std::max(1, trim);
     Node fwd, bwd;
-    for (const std::string& s : reads) {
-        int key = -1;
-        const int len = (int)s.size();
-        for (int pos = 20; pos <= len - keylen - shift_tail; ++pos) {
-            key = seq2int(s, pos, keylen, key);
-            if (key == seed) {
-                add_seq(&fwd, s.substr((size_t)(pos + keylen), (size_t)(len - keylen - shift_tail - pos)));
-                std::string head = s.substr(0, (size_t)pos);
-                std::reverse(head.begin(), head.end());
-                add_seq(&bwd, head);
-            }
-        }
+    std::vector<uint64_t> occ(seed_count);
+    size_t n = 0;
+    if (g_kmer.find(kset, keylen, 20, shift_tail, (uint32_t)seed, occ.data(), occ.size(), &n) != FQ_OK)
+        throw std::runtime_error("adapter detection: k-mer search failed");
+    for (size_t k = 0; k < std::min(n, occ.size()); ++k) {
+        const size_t r = (size_t)(occ[k] >> 32);
+        const int pos = (int)(uint32_t)occ[k];
+        const char* s = reads.seq.data() + reads.off[r];
+        const int len = (int)(reads.off[r + 1] - reads.off[r]);
+        add_seq(&fwd, std::string(s + pos + keylen, (size_t)(len - keylen - shift_tail - pos)));
+        std::string head(s, (size_t)pos);
+        std::reverse(head.begin(), head.end());
+        add_seq(&bwd, head);
     }
     bool reached_leaf = true;
     const std::string f = dominant_path(&fwd, reached_leaf);
@@ -174,10 +183,10 @@ int evaluate_read_num(const std::string& path) {  // Evaluator::evaluateReadNum,
 }
 
 // Evaluator::evaluateAdapterSeq, src/evaluator.cpp:229-390
-std::string detect_adapter(const std::string& path, int trim_tail1, std::string* msgs) {
+std::string detect_adapter(const std::string& path, int trim_tail1, std::string* msgs, int device) {
     const size_t kReadLimit = 256 * 1024, kBaseLimit = 151 * kReadLimit;
     FqReader r(path, false);
-    std::vector<std::string> reads;
+    ReadSet reads;
     size_t bases = 0;
     ByteBuf text;
     Rec rec;
@@ -191,20 +200,25 @@ std::string detect_adapter(const std::string& path, int trim_tail1, std::string*
             break;
         }
         bases += rec.len;
-        reads.emplace_back(text.data() + rec.seq_off(), rec.len);
+        reads.seq.append(text.data() + rec.seq_off(), rec.len);
+        reads.off.push_back((uint32_t)reads.seq.size());
     }
     if (reads.size() < 10000) return "";
     const int shift_tail = std::max(1, trim_tail1);
     const int keylen = 10;
     const size_t size = (size_t)1 << (keylen * 2);
-    std::vector<size_t> counts(size, 0);
-    for (const std::string& sq : reads) {
-        int key = -1;
-        for (int pos = 20; pos <= (int)sq.size() - keylen - shift_tail; ++pos) {
-            key = seq2int(sq, pos, keylen, key);
-            if (key >= 0) ++counts[(size_t)key];
-        }
-    }
+    // the 10-mer histogram of evaluateAdapterSeq (src/evaluator.cpp:265-279)
+    void* kset = nullptr;
+    if (g_kmer.open(device, reinterpret_cast<const uint8_t*>(reads.seq.data()), reads.off.data(), (int32_t)reads.size(),
+                    &kset) != FQ_OK)
+        throw std::runtime_error("adapter detection: no k-mer device (the pre-pass runs on the GPU)");
+    struct Closer {
+        void* h;
+        ~Closer() { g_kmer.close(h); }
+    } closer{kset};
+    std::vector<uint32_t> counts(size, 0);
+    if (g_kmer.count(kset, keylen, 20, shift_tail, counts.data()) != FQ_OK)
+        throw std::runtime_error("adapter detection: k-mer count failed");
     counts[0] = 0;
     const int topnum = 10;
     int top[topnum] = {0};
@@ -242,10 +256,15 @@ std::string detect_adapter(const std::string& path, int trim_tail1, std::string*
         int diff = 0;
         for (size_t i = 0; i + 1 < sq.size(); ++i) diff += sq[i] != sq[i + 1];
         if (diff < 3) continue;
-        const std::string est = adapter_with_seed(key, reads, keylen, trim_tail1);
+        const std::string est = adapter_with_seed(key, reads, kset, counts[(size_t)key], keylen, trim_tail1);
         if (!est.empty()) return est;
     }
     return "";
+}
+
+void set_kmer_backend(const fqh_kmer_backend* b) {
+    if (b) g_kmer = *b;
+    else g_kmer = kGpuKmer;
 }
 
 }  // namespace fqhost

@@ -787,15 +787,16 @@ Options prepare_options(int argc, char** argv) {
         // An interleaved input has no read2 file: opening "" fails as in the reference.
         std::string a1, a2, msg1, msg2;
         std::exception_ptr e1, e2;
+        const int dev = o.device_list()[0];
         std::thread t([&] {
             try {
-                a2 = detect_adapter(o.in2, o.tail1, &msg2);
+                a2 = detect_adapter(o.in2, o.tail1, &msg2, dev);
             } catch (...) {
                 e2 = std::current_exception();
             }
         });
         try {
-            a1 = detect_adapter(o.in1, o.tail1, &msg1);
+            a1 = detect_adapter(o.in1, o.tail1, &msg1, dev);
         } catch (...) {
             e1 = std::current_exception();
         }

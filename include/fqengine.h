@@ -394,6 +394,20 @@ int fq_engine_set_dup(fq_engine* e, fq_dup* d); /* NULL detaches; d must be on t
 int fq_dup_merge(fq_dup* dst, const fq_dup* src);
 int fq_dup_stat(fq_dup* d, int32_t hist_size, uint64_t* hist, uint64_t* gc_sum, uint64_t* totals);
 
+/* ---- adapter-detection k-mers (Evaluator::evaluateAdapterSeq, src/evaluator.cpp:229-426) ------
+ * A read set uploaded once (read i = seq[off[i] .. off[i+1]), n + 1 offsets).  For every read,
+ * every window [pos, pos + keylen) of uppercase A/C/G/T bases with
+ * first <= pos <= len - keylen - shift_tail is one k-mer (key = 2-bit codes A0 T1 C2 G3, first
+ * base most significant, as Evaluator::seq2int).  fq_kmer_count fills counts[4^keylen];
+ * fq_kmer_find lists where `seed` occurs as (read << 32 | pos), in no particular order, up to
+ * cap entries (*n_out = all occurrences). */
+typedef struct fq_kmer_set fq_kmer_set;
+int fq_kmer_open(int device, const uint8_t* seq, const uint32_t* off, int32_t n, fq_kmer_set** out);
+int fq_kmer_close(fq_kmer_set* s);
+int fq_kmer_count(fq_kmer_set* s, int32_t keylen, int32_t first, int32_t shift_tail, uint32_t* counts);
+int fq_kmer_find(fq_kmer_set* s, int32_t keylen, int32_t first, int32_t shift_tail, uint32_t seed, uint64_t* occ,
+                 size_t cap, size_t* n_out);
+
 /* Kernel timing of the engine's last process_device call (HIP events on the launch stream),
  * in milliseconds; 0 when unavailable. */
 double fq_engine_last_kernel_ms(const fq_engine* e);

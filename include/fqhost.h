@@ -62,6 +62,18 @@ int fqh_session_add_acc(fqh_session* s, const uint64_t* acc, int max_cycles);
 char* fqh_session_finish(fqh_session* s);
 void fqh_session_close(fqh_session* s);
 
+/* The adapter-detection pre-pass's k-mer work (fq_kmer_* signatures, include/fqengine.h).  By
+ * default it runs on the GPU; a host without a device (the CPU test suite) registers another
+ * implementation here (NULL restores the GPU). */
+typedef struct fqh_kmer_backend {
+    int (*open)(int device, const uint8_t* seq, const uint32_t* off, int32_t n, void** out);
+    int (*close)(void* set);
+    int (*count)(void* set, int32_t keylen, int32_t first, int32_t shift_tail, uint32_t* counts);
+    int (*find)(void* set, int32_t keylen, int32_t first, int32_t shift_tail, uint32_t seed, uint64_t* occ, size_t cap,
+                size_t* n_out);
+} fqh_kmer_backend;
+void fqh_set_kmer_backend(const fqh_kmer_backend* b);
+
 /* Records of a FASTQ file as the tool's pack reader parses them (bulk = 1: the zero-copy pack
  * reader, packs of `pack_n` records; bulk = 0: the line-by-line FqReader), with read buffers of
  * `buf_size` bytes instead of the reference's 1 MiB (tests cross-check both readers on buffer

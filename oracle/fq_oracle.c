@@ -718,6 +718,92 @@ void orc_dup_stat(const orc_dup* d, int hist_size, uint64_t* hist, uint64_t* gc_
 }
 
 /* ------------------------------------------------------------------------------------ *
+ * Adapter-detection k-mers, src/evaluator.cpp:3-47 (seq2int), :265-279, :392-405
+ * ------------------------------------------------------------------------------------ */
+typedef struct orc_kmer_set {
+    const uint8_t* seq;
+    const uint32_t* off;
+    int32_t n;
+} orc_kmer_set;
+
+/* Evaluator::seq2int: the key of [pos, pos + keylen) from the previous window's key, or -1 */
+static int kmer_seq2int(const uint8_t* s, int pos, int keylen, int last) {
+    if (last >= 0) {
+        const int mask = (1 << (keylen * 2)) - 1;
+        int key = (last << 2) & mask;
+        switch (s[pos + keylen - 1]) {
+            case 'A': return key + 0;
+            case 'T': return key + 1;
+            case 'C': return key + 2;
+            case 'G': return key + 3;
+            default: return -1;
+        }
+    }
+    int key = 0;
+    for (int i = pos; i < pos + keylen; ++i) {
+        key <<= 2;
+        switch (s[i]) {
+            case 'A': break;
+            case 'T': key += 1; break;
+            case 'C': key += 2; break;
+            case 'G': key += 3; break;
+            default: return -1;
+        }
+    }
+    return key;
+}
+
+int orc_kmer_open(int device, const uint8_t* seq, const uint32_t* off, int32_t n, void** out) {
+    (void)device;
+    orc_kmer_set* k = (orc_kmer_set*)calloc(1, sizeof *k);
+    k->seq = seq; /* the caller keeps the reads alive while the set is open */
+    k->off = off;
+    k->n = n;
+    *out = k;
+    return FQ_OK;
+}
+
+int orc_kmer_close(void* set) {
+    free(set);
+    return FQ_OK;
+}
+
+int orc_kmer_count(void* set, int32_t keylen, int32_t first, int32_t shift_tail, uint32_t* counts) {
+    const orc_kmer_set* k = (const orc_kmer_set*)set;
+    memset(counts, 0, ((size_t)1 << (2 * keylen)) * 4);
+    for (int r = 0; r < k->n; ++r) {
+        const uint8_t* s = k->seq + k->off[r];
+        const int len = (int)(k->off[r + 1] - k->off[r]);
+        int key = -1;
+        for (int pos = first; pos <= len - keylen - shift_tail; ++pos) {
+            key = kmer_seq2int(s, pos, keylen, key);
+            if (key >= 0) ++counts[key];
+        }
+    }
+    return FQ_OK;
+}
+
+int orc_kmer_find(void* set, int32_t keylen, int32_t first, int32_t shift_tail, uint32_t seed, uint64_t* occ,
+                  size_t cap, size_t* n_out) {
+    const orc_kmer_set* k = (const orc_kmer_set*)set;
+    size_t n = 0;
+    for (int r = 0; r < k->n; ++r) {
+        const uint8_t* s = k->seq + k->off[r];
+        const int len = (int)(k->off[r + 1] - k->off[r]);
+        int key = -1;
+        for (int pos = first; pos <= len - keylen - shift_tail; ++pos) {
+            key = kmer_seq2int(s, pos, keylen, key);
+            if (key >= 0 && (uint32_t)key == seed) {
+                if (n < cap) occ[n] = ((uint64_t)r << 32) | (uint32_t)pos;
+                ++n;
+            }
+        }
+    }
+    *n_out = n;
+    return FQ_OK;
+}
+
+/* ------------------------------------------------------------------------------------ *
  * Synthetic workload, host twin of the engine's fq_synth_fill_device.
  * Integer-only (no libm) so host and device agree bit for bit.
  * ------------------------------------------------------------------------------------ */

@@ -67,6 +67,14 @@ void orc_dup_destroy(orc_dup* d);
 void orc_dup_add_batch(orc_dup* d, const fq_batch* b, int paired);
 void orc_dup_stat(const orc_dup* d, int hist_size, uint64_t* hist, uint64_t* gc_sum, uint64_t* totals);
 
+/* Evaluator::evaluateAdapterSeq's k-mer loops (src/evaluator.cpp:265-279, :392-405) with the
+ * fq_kmer_* signatures (include/fqengine.h): the CPU suite's backend for fqh_set_kmer_backend. */
+int orc_kmer_open(int device, const uint8_t* seq, const uint32_t* off, int32_t n, void** out);
+int orc_kmer_close(void* set);
+int orc_kmer_count(void* set, int32_t keylen, int32_t first, int32_t shift_tail, uint32_t* counts);
+int orc_kmer_find(void* set, int32_t keylen, int32_t first, int32_t shift_tail, uint32_t seed, uint64_t* occ,
+                  size_t cap, size_t* n_out);
+
 /* Synthetic workload generator (host twin of fq_synth_fill_device, bit-identical output). */
 void orc_synth_fill(const fq_batch* b, uint64_t seed, uint64_t first_index, int read_len);
 

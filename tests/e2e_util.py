@@ -136,6 +136,18 @@ def oracle_process(orc):
     return process
 
 
+class KmerBackend(ctypes.Structure):  # fqh_kmer_backend (include/fqhost.h)
+    _fields_ = [("open", ctypes.c_void_p), ("close", ctypes.c_void_p), ("count", ctypes.c_void_p),
+                ("find", ctypes.c_void_p)]
+
+
+def oracle_kmer_backend(orc):
+    """The oracle's restatement of the detection k-mer loops as an fqh_kmer_backend."""
+    addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value
+    return KmerBackend(addr(orc.orc_kmer_open), addr(orc.orc_kmer_close), addr(orc.orc_kmer_count),
+                       addr(orc.orc_kmer_find))
+
+
 class OracleDup:
     """Duplicate (-d) on the CPU restatement, standing in for the engine's fq_dup table."""
 

@@ -43,6 +43,11 @@ def load_oracle():
     lib.orc_dup_destroy.argtypes = [vp]
     lib.orc_dup_add_batch.argtypes = [vp, ctypes.POINTER(abi.FqBatch), ci]
     lib.orc_dup_stat.argtypes = [vp, ci, vp, vp, vp]
+    lib.orc_kmer_open.argtypes = [ci, vp, vp, ctypes.c_int32, ctypes.POINTER(vp)]
+    lib.orc_kmer_close.argtypes = [vp]
+    lib.orc_kmer_count.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp]
+    lib.orc_kmer_find.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, vp, ctypes.c_size_t,
+                                  ctypes.POINTER(ctypes.c_size_t)]
     lib.orc_sizeof_params.restype = ctypes.c_size_t
     lib.orc_sizeof_result.restype = ctypes.c_size_t
     assert lib.orc_sizeof_params() == ctypes.sizeof(abi.FqParams), "fq_params ABI mismatch"

@@ -6,6 +6,7 @@ the libfqhost session API with the CPU oracle standing in for the engine, and th
 behaviour (exit status + message) of the real binary, which fails before touching a device.
 GPU: the real `fqtool` binary, engine on MI355X, byte-identical outputs and JSON.
 """
+import ctypes
 import os
 import subprocess
 
@@ -16,10 +17,16 @@ from fqtool_amd import abi
 
 
 @pytest.fixture(scope="module")
-def host():
+def host(oracle):
+    """libfqhost with the adapter-detection k-mer work on the CPU restatement (the tool itself
+    runs it on the GPU; the CPU suite has no device)."""
     if not (os.path.exists(abi.HOST_LIB) and os.path.exists(abi.FQTOOL_BIN)):
         subprocess.run(["make", "-s", "-C", abi.REPO_DIR, "host"], check=True)
-    return abi.load_host()
+    lib = abi.load_host()
+    backend = E.oracle_kmer_backend(oracle)
+    lib.fqh_set_kmer_backend(ctypes.addressof(backend))
+    yield lib
+    lib.fqh_set_kmer_backend(None)
 
 
 @pytest.mark.parametrize("case", E.ok_cases())
