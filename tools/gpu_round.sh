@@ -18,7 +18,7 @@ run() {
 for s in $STEPS; do
     case $s in
     pytest)
-        run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf; rc=$?
+        run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread; rc=$?
         if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
