@@ -86,6 +86,20 @@ struct PtrQual {
 struct LdsQual {  // quality byte i (signed, as the reference's char) of a row packed 4 per LDS word
     const uint32_t* row;
     __device__ __forceinline__ int operator()(int i) const { return (int)(int8_t)(row[i >> 2] >> ((i & 3) * 8)); }
+    __device__ __forceinline__ uint32_t word(int wi) const { return row[wi]; }
+};
+// Quality byte i of a batch row read straight from HBM/L2 (chunk-interleaved tile layout), with
+// dword access for the word-wise window scan; words past the row's stride are clamped.
+struct RowQual {
+    const uint8_t* q;  // the row's chunk 0
+    int nwords;        // stride / 4
+    __device__ __forceinline__ int operator()(int i) const {
+        return (int)(int8_t)q[(i >> 4) * (FQ_TILE_READS * FQ_CHUNK) + (i & 15)];
+    }
+    __device__ __forceinline__ uint32_t word(int wi) const {
+        wi = min(wi, nwords - 1);
+        return *reinterpret_cast<const uint32_t*>(q + (wi >> 2) * (FQ_TILE_READS * FQ_CHUNK) + 4 * (wi & 3));
+    }
 };
 template <class P>
 struct Bytes {
@@ -145,21 +159,20 @@ __device__ inline int window_scan(QQ qual, int s0, int send, int w, int T) {
 // The same scan over an LDS row, 4 positions per step: the added (q[s+w-1]) and removed (q[s-1])
 // bytes arrive as words realigned with v_alignbyte, one LDS word per stream per step, prefetched
 // one step ahead (the byte loop waits out the LDS latency at every position).
-template <bool WANT>
-__device__ inline int window_scan(LdsQual qual, int s0, int send, int w, int T) {
+// (the row's dwords: LdsQual from its LDS row, RowQual from HBM/L2)
+template <bool WANT, class WQ>
+__device__ inline int window_scan_words(WQ qual, int s0, int send, int w, int T) {
     if (s0 >= send) return send;
     const int TW = T * w;
     int tot = 0;
     for (int i = 0; i < w; ++i) tot += qual(s0 + i);
     if ((tot >= TW) == WANT) return s0;
-    const uint32_t* row = qual.row;
     int oa = s0 + w, orr = s0;  // byte offsets of q[s+w-1] and q[s-1] for s = s0 + 1
     const uint32_t sha = oa & 3, shr = orr & 3;
-    const uint32_t* pa = row + (oa >> 2);
-    const uint32_t* pr = row + (orr >> 2);
-    uint32_t alo = pa[0], ahi = pa[1], rlo = pr[0], rhi = pr[1];
+    int pa = oa >> 2, pr = orr >> 2;  // dword indices
+    uint32_t alo = qual.word(pa), ahi = qual.word(pa + 1), rlo = qual.word(pr), rhi = qual.word(pr + 1);
     for (int s = s0 + 1; s < send; s += 4) {
-        const uint32_t an = pa[2], rn = pr[2];
+        const uint32_t an = qual.word(pa + 2), rn = qual.word(pr + 2);
         const uint32_t aw = __builtin_amdgcn_alignbyte(ahi, alo, sha);
         const uint32_t rw = __builtin_amdgcn_alignbyte(rhi, rlo, shr);
 #pragma unroll
@@ -175,6 +188,14 @@ __device__ inline int window_scan(LdsQual qual, int s0, int send, int w, int T) 
         ++pr;
     }
     return send;
+}
+template <bool WANT>
+__device__ inline int window_scan(LdsQual qual, int s0, int send, int w, int T) {
+    return window_scan_words<WANT>(qual, s0, send, w, T);
+}
+template <bool WANT>
+__device__ inline int window_scan(RowQual qual, int s0, int send, int w, int T) {
+    return window_scan_words<WANT>(qual, s0, send, w, T);
 }
 
 // cut_right's scan (src/filter.cpp:124-152) restricted to the windows that can be low: a window

@@ -83,10 +83,11 @@ constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
 // len1 + len2) and gives up a wave for it.
 template <bool LEAN, bool MERGE = false>
 struct Layout {
-    static constexpr int kBlocksPerCU = LEAN ? 2 : 1;
+    static constexpr bool kQLds = MERGE;  // quality rows staged in LDS (merge variant only)
+    static constexpr int kBlocksPerCU = kQLds ? 1 : 2;
     static constexpr int kWaves = MERGE ? 7 : 8;
     static constexpr int kThreads = 64 * kWaves;
-    static constexpr int kWaveW = kCodeW + (LEAN ? 0 : 64 * kQS);
+    static constexpr int kWaveW = kCodeW + (kQLds ? 64 * kQS : 0);
     // [pre1, pre2, post1 (x2 with MERGE), post2] (+ MERGE: read 2's merged parts, cycles 0..319,
     // in removed mode, which uses blocks 0-3 as the kept/removed rows of the two mates)
     static constexpr int kHists = MERGE ? 6 : 4;
@@ -478,7 +479,7 @@ __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) &
 // reverse-complemented for the overlap scan); single-end: a tile is 64 reads, one per lane, with
 // SingleEndProcessor::processSingleEnd's order (src/seprocessor.cpp:290-360).
 template <bool LEAN, bool PAIRED, bool MERGE>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 * Layout<LEAN>::kBlocksPerCU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 * Layout<LEAN, MERGE>::kBlocksPerCU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -566,7 +567,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         const uint8_t* Q = (mate ? b.qual2 : b.qual1) + roff;
         // quality chunk F of this lane's row: from the LDS row (full) or the row in L2 (LEAN)
         auto qchunk = [&](int F) -> uint4 {
-            if (LEAN) return *reinterpret_cast<const uint4*>(Q + cst * F);
+            if (!LY::kQLds) return *reinterpret_cast<const uint4*>(Q + cst * F);
             return make_uint4(qrow[4 * F], qrow[4 * F + 1], qrow[4 * F + 2], qrow[4 * F + 3]);
         };
         // (merge: a merged read, at most len1 + len2 long, must fit max_cycles as well)
@@ -629,7 +630,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 // common case, no byte masks).
                 auto dword = [&](int j, auto full_c) {
                     constexpr bool FULL = decltype(full_c)::value;
-                    if (!LEAN) qrow[4 * k + j] = qw[j];
+                    if (LY::kQLds) qrow[4 * k + j] = qw[j];
                     const uint32_t bm = FULL ? 0xFFFFFFFFu : bytemask(Lk - 4 * j);
                     const uint32_t kk = (sw[j] >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
@@ -710,7 +711,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             nn = valid;
             n = L;
         } else {
-            nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n, lowr_ok ? lowr : ~0u);
+            if constexpr (LY::kQLds)
+                nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n, lowr_ok ? lowr : ~0u);
+            else
+                nn = valid && trim_and_cut_t(p, seq, RowQual{Q, b.stride >> 2}, L, front, tail, st, n, lowr_ok ? lowr : ~0u);
         }
         // the shuffle must run in every lane: ds_bpermute from a lane that is switched off returns
         // whatever its register held before (e.g. the previous tile's value)
