@@ -64,6 +64,7 @@ def log(msg):
 
 def config_params(abi, name, max_cycles=256):
     """Engine parameters of a BASELINE config (what the tool derives from its command line)."""
+    max_cycles = max(max_cycles, READ_LEN)
     p = abi.default_params(paired=name != "C2", max_cycles=max_cycles)
     p.qual_filter_enabled = 1
     if name in ("C3", "C4", "C5"):
@@ -73,7 +74,7 @@ def config_params(abi, name, max_cycles=256):
         p.cut_right = 1
     if name == "C4":
         p.merge_enabled = 1
-        p.max_cycles = max(max_cycles, 320)  # merged reads reach len1 + len2
+        p.max_cycles = max(max_cycles, 2 * READ_LEN, 320)  # merged reads reach len1 + len2
     if name == "C5":
         p.polyx_enabled = 1
     return p
@@ -416,7 +417,15 @@ def free_port():
         return s.getsockname()[1]
 
 
+def set_read_len(args):
+    """--read-len: synthetic mates of this length (rows padded to a multiple of 16)."""
+    global READ_LEN, STRIDE
+    READ_LEN = int(getattr(args, "read_len", 150))
+    STRIDE = (READ_LEN + 15) // 16 * 16
+
+
 def run_rank(args):
+    set_read_len(args)
     """One rank: shard, warm up, time exactly `steps` passes between barriers + device syncs,
     max over ranks, RCCL sum of the accumulator block, parity sample, rank 0 prints the line."""
     import hashlib
@@ -589,12 +598,18 @@ def main():
                     help="pairs per host pack of the PCIe-inclusive engine leg (0: off)")
     ap.add_argument("--config", default="C3", choices=sorted(WORKLOADS),
                     help="workload (BASELINE.json configs); the headline metric is C3")
+    ap.add_argument("--read-len", type=int, default=150,
+                    help="synthetic read length (default 150, the BASELINE configs); longer reads exercise "
+                         "the long-read kernel variant")
     ap.add_argument("--runner", default="hip", help=argparse.SUPPRESS)  # tests: CPU rehearsal of the ranks
     args = ap.parse_args()
     if args.pairs is None:
         args.pairs = 125_000_000 if args.config == "C5" else 100_000_000
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
+    if not 1 <= args.read_len <= 1000:
+        raise SystemExit("--read-len must be in 1..1000")
+    set_read_len(args)
     launch(args)
 
 

@@ -36,7 +36,7 @@ FQ_ACC_TAIL_WORDS = 16
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-ENGINE_LIB = os.path.join(PKG_DIR, "lib", "libfqengine.so")
+ENGINE_LIB = os.environ.get("FQ_ENGINE_LIB") or os.path.join(PKG_DIR, "lib", "libfqengine.so")  # (override: profiling A/B builds)
 HOST_LIB = os.path.join(PKG_DIR, "lib", "libfqhost.so")
 FQTOOL_BIN = os.path.join(PKG_DIR, "bin", "fqtool")
 

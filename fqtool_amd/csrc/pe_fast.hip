@@ -39,7 +39,11 @@
 
 using namespace fqdev;
 
+#if FQ_MAXLEN_BUILD_LONG
+namespace long320 {  // (kernel names tell the two builds apart in profiles)
+#else
 namespace {
+#endif
 
 #ifndef FQ_ABLATE_STAGE
 #define FQ_ABLATE_STAGE 0
@@ -53,12 +57,20 @@ namespace {
 #ifndef FQ_SCHED_PIN
 #define FQ_SCHED_PIN 1
 #endif
+#ifndef FQ_MERGE_QLDS
+#define FQ_MERGE_QLDS 1
+#endif
 #ifndef FQ_AHEAD
 #define FQ_AHEAD 3
 #endif
 constexpr int kAhead = FQ_AHEAD;  // staging: row chunks requested this many chunks ahead of their use
 constexpr int kBlock = 512;  // launch bound: 8 waves (7 in the merge variant)
-constexpr int kMaxLen = 160;
+#ifndef FQ_MAXLEN
+#define FQ_MAXLEN 160  // pe_fast_long.hip builds this file again for reads up to 320 bp
+#endif
+constexpr int kMaxLen = FQ_MAXLEN;
+static_assert(kMaxLen % 32 == 0 && kMaxLen <= 320, "reads per column: a multiple of 32, at most 320");
+constexpr int kOvBlocks = kMaxLen / 32;           // 32-offset blocks of the overlap candidate scan
 constexpr int kChunks = kMaxLen / 16;             // 16-position chunks per read
 constexpr int kFC = 0;                            // column fields (words): 2-bit codes,
 constexpr int kFN = kChunks;                      //   spaced N mask,
@@ -72,10 +84,11 @@ constexpr int kSlots = 6;
 constexpr int kDummySlot = 5;
 constexpr int kHistW = kChunks * kSlots * 32;
 __host__ __device__ constexpr int cell(int c, int slot) { return ((c >> 4) * kSlots + slot) * 32 + 2 * (c & 15); }
-constexpr int kSmallU64 = FQ_ACC_INSERT + 512 + 1;
+constexpr int kSmallU64 = FQ_ACC_INSERT;                 // FilterResult / adapter / polyX / merged counters
 constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
-constexpr int kScalCopies = 16;  // per-read scalars are spread over 16 copies (lane & 15)
-constexpr int kScalW = 2 * 16 * kScalCopies;  // [copy][4 stats][reads, length_sum, q20, q30] u64
+constexpr int kInsW = (512 + 1 + 1) & ~1;                 // insert-size histogram, u32 per workgroup
+// per-read scalars are spread over kScalCopies LDS copies (lane % copies), each
+// [4 stats][reads, length_sum, q20, q30] u64; the merge variant keeps 8 (LDS budget)
 constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
 // LEAN keeps qualities in HBM/L2 (2 workgroups = 16 waves per CU); the full variant, whose
 // trimming windows read qualities at random, stages them in LDS rows (1 workgroup per CU).  The
@@ -83,9 +96,11 @@ constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
 // len1 + len2) and gives up a wave for it.
 template <bool LEAN, bool MERGE = false>
 struct Layout {
-    static constexpr bool kQLds = MERGE;  // quality rows staged in LDS (merge variant only)
-    static constexpr int kBlocksPerCU = kQLds ? 1 : 2;
-    static constexpr int kWaves = MERGE ? 7 : 8;
+    // quality rows staged in LDS (off: rows are re-read from L2); profiling switch for the merge variant
+    static constexpr bool kQLds = MERGE && FQ_MERGE_QLDS;
+    static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160) ? 1 : 2;
+    static constexpr int kWaves = MERGE ? (kQLds ? 7 : 6) : 8;
+    static constexpr int kWavesPerEU = (kWaves * kBlocksPerCU + 3) / 4;
     static constexpr int kThreads = 64 * kWaves;
     static constexpr int kWaveW = kCodeW + (kQLds ? 64 * kQS : 0);
     // [pre1, pre2, post1 (x2 with MERGE), post2] (+ MERGE: read 2's merged parts, cycles 0..319,
@@ -93,7 +108,9 @@ struct Layout {
     static constexpr int kHists = MERGE ? 6 : 4;
     static constexpr int kXtraW = MERGE ? kSlots * 32 : 0;  // one more cycle row: dummy positions up to 335
     static constexpr int kColsW = kWaves * kWaveW;
-    static constexpr int kLdsW = kColsW + kHists * kHistW + kXtraW + kSmallW + kScalW + kAdW;
+    static constexpr int kScalCopies = MERGE ? 8 : 16;
+    static constexpr int kScalW = 2 * 16 * kScalCopies;
+    static constexpr int kLdsW = kColsW + kHists * kHistW + kXtraW + kSmallW + kInsW + kScalW + kAdW;
     static_assert(kLdsW * 4 * kBlocksPerCU <= 160 * 1024, "LDS budget");
     static_assert((kColsW & 1) == 0 && (kHistW & 1) == 0, "u64 cells must stay 8-byte aligned");
     static_assert(kThreads <= kBlock, "launch bound");
@@ -324,7 +341,7 @@ __device__ __forceinline__ void csa(uint32_t& hi, uint32_t& lo, uint32_t a, uint
 // offsets of a block is ((H >> j) ^ FH_j) | ((L >> j) ^ FL_j) (FH_j, FL_j = the bits of fixed[j]
 // spread over a word), and the 16 vectors are summed per offset with carry-save adders.
 __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint32_t fixed, int K, int cnt,
-                                     uint32_t cand[5]) {
+                                     uint32_t cand[kOvBlocks]) {
     // planes of the 32 positions from mpos + 32 * i (i = block): low-bit plane, high-bit plane
     auto planes = [&](int i, uint32_t& lp, uint32_t& hp) {
         const uint32_t u0 = unzip2(field_window(col, kFC, cm, mpos + 32 * i));
@@ -335,11 +352,16 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
     uint32_t L0, H0, L1, H1;
     planes(0, L0, H0);
     const uint32_t fu = unzip2(fixed);
-    const int nblk = __any(cnt > 128) ? 5 : __any(cnt > 96) ? 4 : __any(cnt > 64) ? 3 : 2;  // wave-uniform
-    for (int bk = nblk; bk < 5; ++bk) cand[bk] = 0u;
+    int nblk = 2;  // blocks holding some lane's offsets (wave-uniform)
+#pragma unroll
+    for (int k = 2; k < kOvBlocks; ++k)
+        if (__any(cnt > 32 * k)) nblk = k + 1;
+#pragma unroll
+    for (int bk = 0; bk < kOvBlocks; ++bk)
+        if (bk >= nblk) cand[bk] = 0u;
 #pragma unroll 1
     for (int bk = 0; bk < nblk; ++bk) {
-        if (bk < 4) planes(bk + 1, L1, H1);
+        if (bk < kOvBlocks - 1) planes(bk + 1, L1, H1);
         else L1 = H1 = 0u;
         // mismatch vector of compared position j over the block's 32 offsets
         auto m = [&](int j) -> uint32_t {
@@ -391,53 +413,61 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
     }
 }
 
-__device__ __forceinline__ uint32_t gmask(const Fwd& f) { return ~fold2(~f.c) & ~f.n & 0x55555555u; }
 
-// PolyX::trimPolyG (src/polyx.cpp:14-38) on the code columns.  The scan from the 3' end changes
-// its state only at non-G bases (with maxMM >= 0 the allowance never shrinks, so a G never
-// breaks it), so it visits just those, with find-last-set over 16-position chunks.
-// allowed(j) = min(maxMM, max(1, (j+1)/per)); (j+1)/per = ((j+1)*inv) >> 16 with
-// inv = ceil(65536/per) is exact for j+1 <= 161 and per <= 256 (inv = 0 for per > 256, where the
-// quotient is 0 anyway).  The two chunks at the 3' end are fetched up front; they hold the whole
-// scan for almost every read.  Returns the new window length; bases < 0: not recorded.
-__device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int L, int st, int n, int maxMM, int inv,
+// PolyX::trimPolyG (src/polyx.cpp:14-38) on the code columns, one pass over 16-position groups
+// of scan indices (scan index i = forward position e - i, e = the window's last base).  A group
+// is one field_window of the column: read 2's column is the reverse complement, so its scan order
+// is the column order and a forward G is a stored C; read 1's group is the forward window
+// reversed.  The scan changes state only at non-G bases (with maxMM >= 0 the allowance never
+// shrinks, so a G never breaks it); a group whose non-G count cannot exceed the allowance at its
+// first index is passed over with one popcount, otherwise its non-G bases are visited in order
+// with find-first-set.  allowed(i) = min(maxMM, max(1, (i+1)/per)); (i+1)/per = ((i+1)*inv) >> 16
+// with inv = ceil(65536/per) is exact for i+1 <= 161 and per <= 256 (inv = 0 for per > 256, where
+// the quotient is 0 anyway).  firstGpos, the lowest G position the scan saw, is the highest G scan
+// index below the break, tracked per group.  Returns the new window length; bases < 0: not recorded.
+__device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, int n, int maxMM, int inv, int per,
                                  int compareReq, int& bases) {
+    auto allowed = [&](int x) { return min(maxMM, max(1, inv ? (x * inv) >> 16 : x / per)); };  // x = i + 1
     const int e = st + n - 1;  // last forward position of the window
-    const int Fe = e >> 4, Fs = st >> 4;
-    const uint32_t g0 = gmask(fwd_chunk(col, c, Fe, rc));
-    const uint32_t g1 = gmask(fwd_chunk(col, c, Fe - 1, rc));
-    int mism = 0, iend = n;  // iend: scan index of the break, or rlen when the scan ran through
-    if (maxMM < 0) iend = 0;  // mismatch 0 > allowed at the very first base
-    for (int F = Fe; F >= Fs && iend == n; --F) {
-        const uint32_t g = F == Fe ? g0 : F == Fe - 1 ? g1 : gmask(fwd_chunk(col, c, F, rc));
-        uint32_t m = ~g & 0x55555555u & posmask(e - 16 * F + 1) & ~posmask(st - 16 * F);
-        while (m) {
-            const int b = 31 - __clz(m);
-            const int j = e - (16 * F + (b >> 1));
-            ++mism;
-            if (mism > min(maxMM, max(1, ((j + 1) * inv) >> 16))) {
-                iend = j;
-                break;
+    int iend = n;              // scan index of the break, or rlen when the scan ran through
+    int lastG = -1;            // highest scan index holding a G before the break
+    if (maxMM < 0) {
+        iend = 0;  // mismatch 0 > allowed at the very first base
+    } else {
+        int cum = 0;  // non-G bases before the current group
+        for (int g = 0; 16 * g < n && iend == n; ++g) {
+            const int pos0 = rc ? kMaxLen - 1 - e + 16 * g : e - 16 * g - 15;
+            const uint32_t cw = field_window(col, kFC, c, pos0), nw = field_window(col, kFN, c, pos0);
+            uint32_t x = fold2(cw ^ (rc ? 0x55555555u : 0xFFFFFFFFu)) | nw;  // non-G (N included), spaced
+            if (!rc) x = __builtin_bitreverse32(x) >> 1;                        // forward window -> scan order
+            const uint32_t valid = posmask(n - 16 * g);
+            x &= valid;
+            uint32_t gm = ~x & valid;  // G bases of the group
+            const int a0 = allowed(16 * g + 1);  // allowance at the group start
+            if (cum + __popc(x) > a0) {
+                uint32_t m = x;
+                while (m) {
+                    const int t = (__ffs(m) - 1) >> 1;
+                    const int i = 16 * g + t;
+                    ++cum;
+                    if (cum > allowed(i + 1)) {
+                        iend = i;
+                        gm &= posmask(t);  // G bases before the break
+                        break;
+                    }
+                    m &= m - 1;
+                }
+            } else {
+                cum += __popc(x);
             }
-            m ^= 1u << b;
+            if (gm) lastG = 16 * g + ((31 - __clz(gm)) >> 1);
         }
     }
     bases = -1;
     if (iend + 1 < compareReq) return n;
-    // firstG: the lowest scanned position holding a G, i.e. the lowest G in [e-iend+1, e]
-    // (the reference's default is rlen-1)
-    int firstG = n - 1;
-    const int lo = e - iend + 1;
-    for (int F = lo >> 4; F <= Fe; ++F) {
-        uint32_t g = F == Fe ? g0 : F == Fe - 1 ? g1 : gmask(fwd_chunk(col, c, F, rc));
-        g &= posmask(e - 16 * F + 1) & ~posmask(lo - 16 * F);
-        if (g) {
-            firstG = 16 * F + ((__ffs(g) - 1) >> 1) - st;
-            break;
-        }
-    }
+    const int firstG = lastG >= 0 ? e - lastG - st : n - 1;  // (the reference's default is rlen-1)
     bases = n - firstG;
-    return firstG;  // n >= 1 here, so 0 <= firstG <= n-1 (Read::resize keeps it)
+    return firstG < 0 ? n : firstG;  // (empty window: firstGpos -1, Read::resize(-1) is a no-op)
 }
 
 __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
@@ -479,7 +509,7 @@ __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) &
 // reverse-complemented for the overlap scan); single-end: a tile is 64 reads, one per lane, with
 // SingleEndProcessor::processSingleEnd's order (src/seprocessor.cpp:290-360).
 template <bool LEAN, bool PAIRED, bool MERGE>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 * Layout<LEAN, MERGE>::kBlocksPerCU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -490,9 +520,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     uint32_t* qrows = col + kCodeW;           // full variant: quality rows, row = lane
     uint32_t* hist = lds + LY::kColsW;        // [pre1, pre2, post1, post2] x kHistW (post1 x2 with MERGE)
     unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + LY::kHists * kHistW + LY::kXtraW);
-    unsigned long long* scal = small + kSmallW / 2;
-    uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16 * kScalCopies);
-    for (int i = threadIdx.x; i < LY::kHists * kHistW + LY::kXtraW + kSmallW + kScalW; i += kThreads) hist[i] = 0;
+    unsigned int* ins = reinterpret_cast<unsigned int*>(small + kSmallW / 2);
+    unsigned long long* scal = reinterpret_cast<unsigned long long*>(ins + kInsW);
+    uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16 * LY::kScalCopies);
+    for (int i = threadIdx.x; i < LY::kHists * kHistW + LY::kXtraW + kSmallW + kInsW + LY::kScalW; i += kThreads) hist[i] = 0;
     for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kThreads)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
     __syncthreads();
@@ -520,7 +551,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     // pre = kept + removed and post = kept.
     const bool removed_mode = LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front);
     const int g_per = max(p.polyg_one_mismatch_per, 1);
-    const int g_inv = g_per > 256 ? 0 : (65536 + g_per - 1) / g_per;
+    // (i+1)/per as ((i+1)*inv) >> 16, exact while per * (kMaxLen + 1) < 65536; else inv = 0: division
+    const int g_inv = g_per * (kMaxLen + 1) < 65536 ? (65536 + g_per - 1) / g_per : 0;
 #ifdef FQ_PHASE_STAMPS
     const bool stamps = p.reserved[1] != 0;
     unsigned long long ph[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -729,9 +761,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         // ---------------- polyG (src/peprocessor.cpp:295-299) ----------------
         if (both && p.polyg_enabled && !(abl & 8)) {
             int bases;
-            n = polyg_bits(col, lane, rc, L, st, n, p.polyg_max_mismatch, g_inv, p.polyg_compare_req, bases);
+            n = polyg_bits(col, lane, rc, st, n, p.polyg_max_mismatch, g_inv, g_per, p.polyg_compare_req, bases);
             if (bases >= 0 && !(abl & 32))  // (reads << 32 | bases) into the lane's scalar copy
-                sadd(&scal[16 * (lane_x & 15) + 4 * mate + 2], (1ull << 32) | (unsigned long long)bases);
+                sadd(&scal[16 * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 2], (1ull << 32) | (unsigned long long)bases);
         }
 
         FQ_STAMP(2)
@@ -752,7 +784,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     n = pos;
                 }
                 rr.ad_len = (uint16_t)ad_len;
-                if (ad_len > 0) sadd(&scal[16 * (lane_x & 15) + 4 * mate + 3], (1ull << 32) | (unsigned long long)ad_len);
+                if (ad_len > 0) sadd(&scal[16 * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 3], (1ull << 32) | (unsigned long long)ad_len);
             }
         };
         // OverlapAnalysis::analyze (src/overlapanalysis.cpp:7-72) of the pair's current windows;
@@ -775,12 +807,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
             // bit-plane candidates when every lane compares full 16-position windows
             const bool planes = req >= 16 && !__any(olB < 16) && !(abl & 128);
             if (planes) {
-                uint32_t cand[5];
+                uint32_t cand[kOvBlocks];
                 ov_candidates(col, cm, mpos, fixed, K, cnt, cand);
                 for (;;) {  // candidates in offset order until one passes the exact test
                     int o = -1;
 #pragma unroll
-                    for (int bk = 4; bk >= 0; --bk)
+                    for (int bk = kOvBlocks - 1; bk >= 0; --bk)
                         if (cand[bk]) o = 32 * bk + __ffs(cand[bk]) - 1;
                     if (o < 0) break;
                     cand[o >> 5] &= cand[o >> 5] - 1u;
@@ -832,7 +864,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 int isize = p.insert_size_max;
                 if (ov.overlapped) isize = ov.offset > 0 ? n1 + n2 - ov.len : ov.len;
                 if (isize > p.insert_size_max) isize = p.insert_size_max;
-                sadd(&small[FQ_ACC_INSERT + isize], 1ull);
+                atomicAdd(&ins[isize], 1u);
             }
             if (p.adapter_trimming) {
                 const int ol = ov.len;  // AdapterTrimmer::trimByOverlapAnalysis, src/adaptertrimmer.cpp:14-27
@@ -842,7 +874,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     rr.ad_pos = (uint16_t)(st + ol);
                     rr.ad_len = (uint16_t)(n - ol);
                     if (mate == 0)
-                        sadd(&scal[16 * (lane_x & 15) + 3], (2ull << 32) | (unsigned long long)((n1 - ol) + (n2 - ol)));
+                        sadd(&scal[16 * (lane_x & (LY::kScalCopies - 1)) + 3], (2ull << 32) | (unsigned long long)((n1 - ol) + (n2 - ol)));
                     n = ol;
                 } else if (!LEAN && my_alen > 0) {
                     by_sequence();
@@ -903,18 +935,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         int low = 0, tq = 0, nb = 0;
         if (nn && wn > 0) {
             // window sums = whole-read sums (from staging) minus the trimmed head [0, ws) and
-            // tail [ws+wn, L): the trimmed parts are usually a few bases
-            low = (int)lowf;
-            tq = (int)tqf;
-            nb = (int)nbf;
-            w20 = q20;
-            w30 = q30;
+            // tail [ws+wn, L): the trimmed parts are usually a few bases.  (FULL: a window
+            // shorter than half the read, e.g. read 2's part of a merged read, is summed directly:
+            // "subtracted" from 0 and negated.)
+            const bool direct = !LEAN && 2 * wn < L;
+            low = direct ? 0 : (int)lowf;
+            tq = direct ? 0 : (int)tqf;
+            nb = direct ? 0 : (int)nbf;
+            w20 = direct ? 0u : q20;
+            w30 = direct ? 0u : q30;
             if (!(abl & 2)) {
                 const int end = ws + wn;
                 const bool need_tq = p.avg_qual_limit > 0;  // the total quality only feeds -e
 #pragma unroll
                 for (int part = 0; part < 2; ++part) {
-                    const int a0 = part ? end : 0, a1 = part ? L : ws;  // forward range [a0, a1)
+                    // forward range [a0, a1)
+                    const int a0 = direct ? (part ? L : ws) : (part ? end : 0);
+                    const int a1 = direct ? (part ? L : end) : (part ? L : ws);
                     const int F0 = a0 >> 4, F1 = (a1 + 15) >> 4;
                     // subtract the bytes of row chunk F inside [a0, a1)
                     auto sub = [&](const uint4 cur, int F) {
@@ -933,7 +970,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                             if (need_tq) tq -= (int)__builtin_amdgcn_sad_u8(wq[j] & ((rf >> 7) * 0xFFu), 0u, 0u);
                         }
                     };
-                    if (part == 1) {
+                    if (part == 1 && a0 < a1) {
                         // the tail, from the 3' end: its last two chunks are requested together
                         // (one L2 round trip for most reads), longer adapter tails loop
                         uint4 qa[2];
@@ -958,6 +995,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                         const uint32_t w = col[(kFN + c) * 64 + lane_x];
                         nb -= __popc(w & posmask(s1 - 16 * c) & ~posmask(s0 - 16 * c));
                     }
+                }
+                if (direct) {
+                    low = -low;
+                    tq = -tq;
+                    nb = -nb;
+                    w20 = 0u - w20;
+                    w30 = 0u - w30;
                 }
             }
             if (!(MERGE && merged))
@@ -1112,16 +1156,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                 const int c = m1 + t;
                 rb[t] = xb + (uint32_t)((((c >> 4) * kSlots) * 32 + 2 * (c & 15)) * 4);
             }
+            // quality dwords of forward positions [hi - 15, hi], hi = pos_hi - 16J: words
+            // wl0 - 4J .. wl0 - 4J + 4; the next group's four new words are requested one group ahead
+            const int wl0 = (pos_hi - 15) >> 2, sh = (pos_hi - 15) & 3;  // (negative only for dummies)
+            auto qword = [&](int wi) -> uint32_t {
+                if constexpr (LY::kQLds) return qrow[min(max(wi, 0), kQS - 1)];
+                else return RowQual{Q, b.stride >> 2}.word(max(wi, 0));
+            };
+            uint32_t qw5[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) qw5[i] = qword(wl0 + i);
             for (int J = 0; 16 * J < wn; ++J) {
                 const uint32_t cw = field_window(col, kFC, lane_x, ci0 + 16 * J);
                 const uint32_t nw = field_window(col, kFN, lane_x, ci0 + 16 * J);
-                // qualities of forward positions [hi - 15, hi], hi = pos_hi - 16J, ascending in
-                // a0..a3, then reversed: qrev[k] byte b = merged t = 4k + b
-                const int lo = pos_hi - 16 * J - 15;
-                const int wl = lo >> 2, sh = lo & 3;  // (lo < 0 only for dummy positions)
-                uint32_t qw5[5];
+                uint32_t qn[4];
 #pragma unroll
-                for (int i = 0; i < 5; ++i) qw5[i] = qrow[min(max(wl + i, 0), kQS - 1)];
+                for (int i = 0; i < 4; ++i) qn[i] = qword(wl0 - 4 * (J + 1) + i);
+                // qualities ascending in qa[0..3], then reversed: qrev[k] byte b = merged t = 4k + b
                 uint32_t qa[4], qrev[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) qa[i] = __builtin_amdgcn_alignbyte(qw5[i + 1], qw5[i], sh);
@@ -1155,6 +1206,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
                     __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + 3u * 128u)), 0ull - v,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+                qw5[4] = qw5[0];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) qw5[i] = qn[i];
             }
         }
         if (valid && !(abl & 4) && !removed_mode) {
@@ -1213,7 +1267,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
         if (valid && !(abl & 4)) {
             // per-read Stats scalars: (reads, length_sum) packed as count << 32 | sum, plus
             // q20 << 32 | q30, into one of 16 LDS copies (lanes l, l + 16 share one)
-            unsigned long long* sc = scal + 16 * (lane_x & 15) + 4 * mate;
+            unsigned long long* sc = scal + 16 * (lane_x & (LY::kScalCopies - 1)) + 4 * mate;
             sadd(&sc[0], (1ull << 32) | (unsigned long long)L);
             sadd(&sc[1], ((unsigned long long)q20 << 32) | q30);
             const bool post_here = (MERGE && merged) ? (post_on && mate == 0) : post_on;
@@ -1253,15 +1307,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     __syncthreads();
 
     // ---------------- flush to the global accumulator ----------------
-    const int nsmall = FQ_ACC_INSERT + p.insert_size_max + 1;
-    for (int i = threadIdx.x; i < nsmall; i += kThreads)
+    for (int i = threadIdx.x; i < FQ_ACC_INSERT; i += kThreads)
         if (small[i]) atomicAdd(&acc[i], small[i]);
+    for (int i = threadIdx.x; i <= p.insert_size_max; i += kThreads)
+        if (ins[i]) atomicAdd(&acc[FQ_ACC_INSERT + i], (unsigned long long)ins[i]);
     const size_t st_base = acc_stats_offset(p.insert_size_max, p.max_cycles, 0);
     const size_t st_words = acc_stats_words(p.max_cycles);
     if (threadIdx.x < 16) {  // stats k: [reads << 32 | length_sum, q20 << 32 | q30] -> the four words
         const int k = threadIdx.x >> 2, f = threadIdx.x & 3;
         unsigned long long v = 0;
-        for (int c = 0; c < kScalCopies; ++c) {
+        for (int c = 0; c < LY::kScalCopies; ++c) {
             const unsigned long long w = scal[16 * c + 4 * k + (f >> 1)];
             v += (f & 1) ? (w & 0xFFFFFFFFull) : (w >> 32);
         }
@@ -1269,7 +1324,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
     } else if (threadIdx.x < 18) {  // polyG (slot 2) and adapter (slot 3) counters: reads << 32 | bases
         const int slot = threadIdx.x - 14;
         unsigned long long rd = 0, bs = 0;
-        for (int c = 0; c < kScalCopies; ++c)
+        for (int c = 0; c < LY::kScalCopies; ++c)
             for (int m = 0; m < 2; ++m) {
                 const unsigned long long w = scal[16 * c + 4 * m + slot];
                 rd += w >> 32;
@@ -1333,7 +1388,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2 *
 }
 
 }  // namespace
+#if FQ_MAXLEN_BUILD_LONG
+using namespace long320;
+#endif
 
+#if FQ_MAXLEN == 160
 bool fq_pe_fast_supported(const fq_params& p) {
     // -c and UMI trims run on the general kernel (fq_pack_kernel)
     return p.insert_size_max <= 512 && p.insert_size_max >= 0 && !p.correction_enabled && p.umi_front1 == 0 &&
@@ -1349,33 +1408,60 @@ extern "C" __attribute__((visibility("default"))) int fq_debug_phase_cycles(unsi
     for (int i = 0; i < n && i < kPhases; ++i) out[i] = h[i];
     return 0;
 }
+#define FQ_PREPARE fq_pe_fast_prepare
+#define FQ_LAUNCH fq_launch_pe_fast
+#else  // the long-read build (pe_fast_long.hip): no merge variant
+#define FQ_PREPARE fq_pe_fast_long_prepare
+#define FQ_LAUNCH fq_launch_pe_fast_long
+#endif
 
-hipError_t fq_pe_fast_prepare() {
+hipError_t FQ_PREPARE() {
+    constexpr int nk = FQ_MAXLEN == 160 ? 5 : 4;
     const void* k[5] = {(const void*)pe_fast_kernel<true, true, false>, (const void*)pe_fast_kernel<false, true, false>,
                         (const void*)pe_fast_kernel<true, false, false>, (const void*)pe_fast_kernel<false, false, false>,
-                        (const void*)pe_fast_kernel<false, true, true>};
-    for (int i = 0; i < 5; ++i) {
-        const int words = i == 4 ? Layout<false, true>::kLdsW : (i & 1) ? Layout<false>::kLdsW : 160 * 1024 / 4;
+#if FQ_MAXLEN == 160
+                        (const void*)pe_fast_kernel<false, true, true>
+#else
+                        nullptr
+#endif
+    };
+    for (int i = 0; i < nk; ++i) {
+        int words = (i & 1) ? Layout<false>::kLdsW : 160 * 1024 / 4;
+#if FQ_MAXLEN == 160
+        if (i == 4) words = Layout<false, true>::kLdsW;
+#endif
         hipError_t e = hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, words * 4);
         if (e != hipSuccess) return e;
     }
+#if FQ_MAXLEN == 160
+    return fq_pe_fast_long_prepare();
+#else
     return hipSuccess;
+#endif
 }
 
-hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
-                             int* slow_tiles, int* slow_count, int grid, hipStream_t stream) {
+hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
+                     int* slow_tiles, int* slow_count, int grid, hipStream_t stream) {
+#if FQ_MAXLEN == 160
+    // rows longer than 160 bytes: the 320-position build (reads beyond 320 bp are handed off per tile)
+    if (b.stride > kMaxLen && !p.merge_enabled)
+        return fq_launch_pe_fast_long(p, b, res, acc, slow_tiles, slow_count, grid, stream);
+#endif
     const bool lean = p.trim_front1 == 0 && p.trim_tail1 == 0 && p.trim_front2 == 0 && p.trim_tail2 == 0 &&
                       !(p.avg_qual_limit > 0) &&
                       !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
                       p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled;
     using LL = Layout<true>;
     using LF = Layout<false>;
-    using LM = Layout<false, true>;
     const dim3 gl(grid * LL::kBlocksPerCU), gf(grid * LF::kBlocksPerCU);
+#if FQ_MAXLEN == 160
+    using LM = Layout<false, true>;
     if (p.merge_enabled)
         hipLaunchKernelGGL((pe_fast_kernel<false, true, true>), dim3(grid * LM::kBlocksPerCU), dim3(LM::kThreads),
                            LM::kLdsW * 4, stream, p, b, res, acc, slow_tiles, slow_count);
-    else if (p.paired && lean)
+    else
+#endif
+    if (p.paired && lean)
         // (fq_params.reserved[2]: extra LDS bytes per workgroup, profiling only -- lowers occupancy)
         hipLaunchKernelGGL((pe_fast_kernel<true, true, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4 + p.reserved[2], stream, p, b,
                            res, acc, slow_tiles, slow_count);
@@ -1390,3 +1476,5 @@ hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_resu
                            res, acc, slow_tiles, slow_count);
     return hipGetLastError();
 }
+#undef FQ_PREPARE
+#undef FQ_LAUNCH

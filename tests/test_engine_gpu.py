@@ -278,3 +278,27 @@ def test_async_submit_poll_pipeline(eng_lib, oracle):
         eng_lib.fq_engine_destroy(h)
         for ptr in pinned:
             eng_lib.fq_host_free(ptr)
+
+
+@pytest.mark.parametrize("name", ALL_CONFIGS)
+@pytest.mark.parametrize("L,stride", [(250, 256), (300, 304)])
+def test_long_read_parity(eng_lib, oracle, name, L, stride):
+    """2x250 / 2x300 rows run on the 320-position build of the fast kernels (pe_fast_long.hip;
+    -m keeps the general kernel for them)."""
+    p = config(name, max_cycles=640)
+    pk = synth_pack(oracle, 3000, bool(p.paired), first=777, L=L, stride=stride)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+@pytest.mark.parametrize("name", ALL_CONFIGS)
+@pytest.mark.parametrize("stride", [320, 336])
+def test_long_edge_parity(eng_lib, oracle, name, stride, mode):
+    """Ragged/hostile reads up to the row stride: tiles with a read beyond 320 bp (stride 336) are
+    handed to the general kernel by the long build."""
+    p = config(name, max_cycles=704)
+    pk = edge_pack(2000, bool(p.paired), stride=stride, seed=(hash(name) + stride) & 0xFFFF)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
