@@ -57,8 +57,14 @@ namespace {
 #ifndef FQ_SCHED_PIN
 #define FQ_SCHED_PIN 1
 #endif
+#ifndef FQ_MERGE_WAVES
+#define FQ_MERGE_WAVES 8  // profiling switches of the merge variant without LDS quality rows
+#endif
+#ifndef FQ_MERGE_BLOCKS
+#define FQ_MERGE_BLOCKS 1
+#endif
 #ifndef FQ_MERGE_QLDS
-#define FQ_MERGE_QLDS 1
+#define FQ_MERGE_QLDS 0
 #endif
 #ifndef FQ_AHEAD
 #define FQ_AHEAD 3
@@ -98,8 +104,8 @@ template <bool LEAN, bool MERGE = false>
 struct Layout {
     // quality rows staged in LDS (off: rows are re-read from L2); profiling switch for the merge variant
     static constexpr bool kQLds = MERGE && FQ_MERGE_QLDS;
-    static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160) ? 1 : 2;
-    static constexpr int kWaves = MERGE ? (kQLds ? 7 : 6) : 8;
+    static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160) ? 1 : MERGE ? FQ_MERGE_BLOCKS : 2;
+    static constexpr int kWaves = MERGE ? (kQLds ? 7 : FQ_MERGE_WAVES) : 8;
     static constexpr int kWavesPerEU = (kWaves * kBlocksPerCU + 3) / 4;
     static constexpr int kThreads = 64 * kWaves;
     static constexpr int kWaveW = kCodeW + (kQLds ? 64 * kQS : 0);
