@@ -33,7 +33,25 @@ const char* line_end(const char* p, size_t n) {
     const char* cr = static_cast<const char*>(std::memchr(p, '\r', upto));
     return cr ? cr : p + upto;
 }
+std::mutex g_gate_mu;
+std::shared_future<void> g_gate;  // invalid: no pre-pass running
 }  // namespace
+
+void set_reader_stderr_gate(std::shared_future<void> gate) {
+    std::lock_guard<std::mutex> l(g_gate_mu);
+    g_gate = std::move(gate);
+}
+
+void reader_stderr(const std::string& s) {
+    if (s.empty()) return;
+    std::shared_future<void> g;
+    {
+        std::lock_guard<std::mutex> l(g_gate_mu);
+        g = g_gate;
+    }
+    if (g.valid()) g.wait();
+    std::cerr << s << std::flush;
+}
 
 ByteBuf& ByteBuf::operator=(ByteBuf&& o) noexcept {
     if (this != &o) {
@@ -288,7 +306,7 @@ void FqBulkReader::read_more() {
             const unsigned ask = (unsigned)std::min<size_t>(want - got, 1u << 30);
             const int r = gzread(gz_, dst + got, ask);
             if (r < 0) {
-                std::cerr << "Error to read gzip file" << std::endl;
+                reader_stderr("Error to read gzip file\n");
                 break;
             }
             got += (size_t)r;
@@ -627,7 +645,7 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
         n = read_mate(r1_, pk, 0, max_n);
         if (n < max_n) {
             done_ = true;
-            if (!r1_.error().empty()) std::cerr << r1_.error();
+            if (!r1_.error().empty()) reader_stderr(r1_.error());
         }
     } else if (interleaved_) {  // FqReaderPair over one file: mate 1, then mate 2
         r1_.begin(pk.text[0]);
@@ -639,8 +657,8 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
             const bool ok_b = r1_.read(b);
             if (!ok_a || !ok_b) {
                 done_ = true;
-                std::cerr << err_a;
-                if (!ok_b) std::cerr << r1_.error();
+                reader_stderr(err_a);
+                if (!ok_b) reader_stderr(r1_.error());
                 break;
             }
             pk.rec[0].push_back(a);
@@ -660,8 +678,8 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
         n = std::min(n1, n2);
         if (n < max_n) {
             done_ = true;
-            if (n1 <= n2) std::cerr << r1_.error();
-            if (n2 <= n1) std::cerr << r2_->error();
+            if (n1 <= n2) reader_stderr(r1_.error());
+            if (n2 <= n1) reader_stderr(r2_->error());
         }
         pk.rec[0].resize(n);
         pk.rec[1].resize(n);

@@ -19,13 +19,22 @@
 #include <cstdio>
 #include <functional>
 #include <memory>
+#include <future>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/fqengine.h"
 
+
 namespace fqhost {
+
+// The pack reader's stderr messages (record errors, gzip read errors) go through a gate: while the
+// adapter-detection pre-pass runs concurrently with the pipeline (run_tool), they wait until the
+// pre-pass has printed its own messages, so stderr keeps the reference's order (the reference
+// runs the pre-pass first, src/main.cpp:139-143).
+void set_reader_stderr_gate(std::shared_future<void> gate);
+void reader_stderr(const std::string& s);
 
 // Growable byte buffer that keeps its capacity when cleared (packs are recycled) and does not
 // zero what it allocates.  A pinned buffer takes page-locked memory from the engine

@@ -11,6 +11,7 @@
 #include <iostream>
 #include <memory>
 #include <mutex>
+#include <future>
 #include <thread>
 
 #include "evaluator.h"
@@ -763,7 +764,46 @@ double since(std::chrono::steady_clock::time_point t) {
 
 }  // namespace
 
-Options prepare_options(int argc, char** argv) {
+// PE adapter detection, Evaluator::evaluateAdapterSeq of both mates (src/main.cpp:139-143).  The
+// two mates' detections run concurrently; their read errors are printed in the reference's order
+// (read 1's first; read 2's only when read 1's detection succeeded).  An interleaved input has no
+// read2 file: opening "" fails as in the reference.
+struct Detection {
+    std::string a1, a2;
+    std::exception_ptr err;
+    double seconds = 0;
+};
+Detection detect_pe_adapters(const Options& o) {
+    const auto t0 = std::chrono::steady_clock::now();
+    Detection d;
+    std::string msg1, msg2;
+    std::exception_ptr e1, e2;
+    const int dev = o.device_list()[0];
+    std::thread t([&] {
+        try {
+            d.a2 = detect_adapter(o.in2, o.tail1, &msg2, dev);
+        } catch (...) {
+            e2 = std::current_exception();
+        }
+    });
+    try {
+        d.a1 = detect_adapter(o.in1, o.tail1, &msg1, dev);
+    } catch (...) {
+        e1 = std::current_exception();
+    }
+    t.join();
+    std::cerr << msg1;
+    if (e1) {
+        d.err = e1;
+    } else {
+        std::cerr << msg2;
+        d.err = e2;
+    }
+    d.seconds = since(t0);
+    return d;
+}
+
+Options prepare_options(int argc, char** argv, bool detect_adapters) {
     Options o = parse_cli(argc, argv);
     try {  // Options::validate failures end in error_exit (src/util.h), exit status 255
         o.update(argc, argv);
@@ -781,32 +821,11 @@ Options prepare_options(int argc, char** argv) {
     }
     if (o.split() && o.paired() && o.out2.empty())  // the reference dereferences a null split writer
         throw std::runtime_error("split output of paired-end reads needs both -o and -O");
-    if (o.detect_pe_adapter) {
-        // the two mates' detections run concurrently; their read errors are printed in the
-        // reference's order (read 1's first; read 2's only when read 1's detection succeeded).
-        // An interleaved input has no read2 file: opening "" fails as in the reference.
-        std::string a1, a2, msg1, msg2;
-        std::exception_ptr e1, e2;
-        const int dev = o.device_list()[0];
-        std::thread t([&] {
-            try {
-                a2 = detect_adapter(o.in2, o.tail1, &msg2, dev);
-            } catch (...) {
-                e2 = std::current_exception();
-            }
-        });
-        try {
-            a1 = detect_adapter(o.in1, o.tail1, &msg1, dev);
-        } catch (...) {
-            e1 = std::current_exception();
-        }
-        t.join();
-        std::cerr << msg1;
-        if (e1) std::rethrow_exception(e1);
-        std::cerr << msg2;
-        if (e2) std::rethrow_exception(e2);
-        o.detected_adapter1 = a1;
-        o.detected_adapter2 = a2;
+    if (detect_adapters && o.detect_pe_adapter) {
+        Detection d = detect_pe_adapters(o);
+        if (d.err) std::rethrow_exception(d.err);
+        o.detected_adapter1 = d.a1;
+        o.detected_adapter2 = d.a2;
     }
     return o;
 }
@@ -815,7 +834,15 @@ int run_tool(int argc, char** argv) {
     Options o;
     const auto t0 = std::chrono::steady_clock::now();
     try {
-        o = prepare_options(argc, argv);
+        // (an interleaved input has no read2 file to detect on: the synchronous pre-pass fails
+        // on it before anything is written, as in the reference)
+        o = prepare_options(argc, argv, false);
+        if (o.detect_pe_adapter && o.in2.empty()) {
+            Detection d = detect_pe_adapters(o);
+            if (d.err) std::rethrow_exception(d.err);
+            o.detected_adapter1 = d.a1;
+            o.detected_adapter2 = d.a2;
+        }
     } catch (const CliError& e) {  // App::exit + FailureMessage::simple (src/CLI.hpp)
         if (e.code == 0) std::cout << e.what() << std::endl;
         else std::cerr << e.what() << "\nRun with --help for more information." << std::endl;
@@ -825,6 +852,25 @@ int run_tool(int argc, char** argv) {
         return 255;
     }
     const double prepass_s = since(t0);
+    // The detected adapters only reach the reports (JSON Read{1,2}AdapterSequence, HTML): trimming
+    // uses --adapter_of_read{1,2} only (src/peprocessor.cpp:319, src/filterresult.cpp:315), so
+    // the detection runs concurrently with the pipeline and is joined before the reports.  The
+    // pack reader's messages wait for its messages (set_reader_stderr_gate).
+    std::promise<void> det_done;
+    std::future<Detection> det;
+    if (o.detect_pe_adapter && !o.in2.empty()) {
+        set_reader_stderr_gate(det_done.get_future().share());
+        det = std::async(std::launch::async, [&o, &det_done] {
+            Detection d;
+            try {
+                d = detect_pe_adapters(o);
+            } catch (...) {
+                d.err = std::current_exception();
+            }
+            det_done.set_value();
+            return d;
+        });
+    }
     try {
         const bool paired = o.paired();
         const size_t pack_n = o.pack_pairs ? o.pack_pairs : std::max<size_t>(o.max_reads_in_pack, 262144);
@@ -957,6 +1003,15 @@ int run_tool(int argc, char** argv) {
             acc.set_dup(hist, gcs, tot[0], tot[1]);
         }
         outs.close();
+        double detect_s = 0;
+        if (det.valid()) {
+            Detection d = det.get();
+            set_reader_stderr_gate(std::shared_future<void>());
+            if (d.err) std::rethrow_exception(d.err);
+            o.detected_adapter1 = d.a1;
+            o.detected_adapter2 = d.a2;
+            detect_s = d.seconds;
+        }
         const Json rep = build_report(o, acc, ac);
         {
             std::ofstream js(o.json_file, std::ios::binary);
@@ -968,10 +1023,11 @@ int run_tool(int argc, char** argv) {
         }
         log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s), wall " +
             std::to_string(since(t0)) + " s, engine submit/wait " + std::to_string(engine_s) + " s; pre-pass " +
-            std::to_string(prepass_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +
+            std::to_string(prepass_s) + " s, adapter detection (concurrent) " + std::to_string(detect_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +
             " s, tiles " + std::to_string(tiles_s) + " s, reader waiting " + std::to_string(spare_wait_s) +
             " s; JSON report " + o.json_file + ", HTML report " + o.html_file);
     } catch (const std::exception& e) {
+        if (det.valid()) det.wait();  // the pre-pass's messages come first, as in the reference
         std::cerr << "ERROR: " << e.what() << std::endl;
         return 255;
     }

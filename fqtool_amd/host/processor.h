@@ -76,7 +76,7 @@ std::string merged_name(const std::string& name, int len1, int len2);
 
 // CLI parse + Options::update/validate + the Evaluator pre-pass (read length estimate,
 // PE adapter detection), src/main.cpp:100-143.  Throws CliError / std::runtime_error.
-Options prepare_options(int argc, char** argv);
+Options prepare_options(int argc, char** argv, bool detect_adapters = true);
 
 // The whole tool: returns the process exit code.
 int run_tool(int argc, char** argv);
