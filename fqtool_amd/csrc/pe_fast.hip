@@ -536,7 +536,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
 
     // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
     // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics,
-    // 32 skip the polyG counters, 64 accept the first scan candidate unchecked, 128 skip the scan
+    // 32 skip the polyG counters, 64 accept the first scan candidate unchecked, 128 skip the scan,
+    // 1024 skip trimAndCut (FULL), 2048 skip polyX
     const int abl = p.reserved[0];
     const int ntiles = PAIRED ? (b.n + 31) >> 5 : (b.n + 63) >> 6;
 #if FQ_FIXED_STRIDE  // profiling only: assume rows of >= 160 bytes
@@ -752,7 +753,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
             if constexpr (LY::kQLds)
                 nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n, lowr_ok ? lowr : ~0u);
             else
-                nn = valid && trim_and_cut_t(p, seq, RowQual{Q, b.stride >> 2}, L, front, tail, st, n, lowr_ok ? lowr : ~0u);
+                nn = valid && ((abl & 1024) ? (n = L, true)
+                                        : trim_and_cut_t(p, seq, RowQual{Q, b.stride >> 2}, L, front, tail, st, n, lowr_ok ? lowr : ~0u));
         }
         // the shuffle must run in every lane: ds_bpermute from a lane that is switched off returns
         // whatever its register held before (e.g. the previous tile's value)
@@ -891,7 +893,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
 
         FQ_STAMP(3)
         // ---------------- polyX, maxLen (src/peprocessor.cpp:335-349) ----------------
-        if (!LEAN && both && p.polyx_enabled) {
+        if (!LEAN && both && p.polyx_enabled && !(abl & 2048)) {
             int poly, bases;
             n = trim_polyx_t(at(seq, st), n, p.polyx_mask, p.polyx_compare_req, p.polyx_max_mismatch,
                              p.polyx_one_mismatch_per, poly, bases);

@@ -197,6 +197,10 @@ def config(name, max_cycles=256):
         p.polyg_enabled = 1
         p.cut_tail = 1
         p.umi_front1 = 12
+    elif name == "PE_cutRF":  # cut_right (w=3, staged scan) after forced front/tail trims
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.cut_right, p.cut_right_window, p.cut_right_quality = 1, 3, 28
+        p.trim_front1, p.trim_tail1, p.trim_front2, p.trim_tail2 = 5, 2, 3, 7
     elif name.startswith("PE_cutR"):  # cut_right alone (removed-mode stats), window w
         w = int(name[7:])
         p.adapter_trimming = p.polyg_enabled = 1
@@ -213,7 +217,7 @@ def config(name, max_cycles=256):
 
 
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
-               "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR5", "PE_merge_q",
+               "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR2", "PE_cutR5", "PE_cutRF", "PE_merge_q",
                "PE_correct", "PE_correct_all", "PE_umi", "SE_umi"]
 
 

@@ -18,7 +18,7 @@ assert lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 0, 150, None) == 0
 res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
 torch.cuda.synchronize()
 bits = {"full": 0, "no_overlap": 1, "no_filter": 2, "no_stats": 4, "no_polyg": 8, "stage_only": 15,
-        "no_ov_exact": 64, "no_ov_scan": 128}
+        "no_ov_exact": 64, "no_ov_scan": 128, "no_trim": 1024, "no_polyx": 2048}
 import bench
 CFG = os.environ.get("CONFIG", "C3")
 for name in os.environ.get("VARIANTS", "full,no_overlap,no_filter,no_stats,no_polyg,stage_only").split(","):
