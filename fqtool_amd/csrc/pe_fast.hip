@@ -67,7 +67,23 @@ namespace {
 #define FQ_MERGE_QLDS 0
 #endif
 #ifndef FQ_AHEAD
-#define FQ_AHEAD 3
+#define FQ_AHEAD 4  // (A/B at 20 M pairs: 3 -> 4 is -1 to -2 % on C3-C5; 5 and 6 are slower)
+#endif
+#ifndef FQ_NFOLD
+#define FQ_NFOLD 1  // removed-mode Stats: N bases by a nibble add (0: the per-N fix-up loop, profiling)
+#endif
+#ifndef FQ_SCAL_PAD
+#define FQ_SCAL_PAD 1  // per-read scalar copies 17 u64 apart: one LDS bank pair per copy (0: 16, profiling)
+#endif
+#ifndef FQ_STAGE_PRIO
+#define FQ_STAGE_PRIO 1  // s_setprio during staging: the loads of staging waves go out first (-2 %)
+#endif
+#ifndef FQ_DESYNC
+#define FQ_DESYNC 0  // profiling: initial s_sleep stagger of co-resident waves
+#endif
+#ifndef FQ_PREFETCH
+#define FQ_PREFETCH 0  // profiling: after staging, pull the first FQ_PREFETCH chunks of the wave's next tile
+                       // toward L2 with LDS-DMA loads (0: off; measured slower at 10)
 #endif
 constexpr int kAhead = FQ_AHEAD;  // staging: row chunks requested this many chunks ahead of their use
 constexpr int kBlock = 512;  // launch bound: 8 waves (7 in the merge variant)
@@ -90,12 +106,22 @@ constexpr int kSlots = 6;
 constexpr int kDummySlot = 5;
 constexpr int kHistW = kChunks * kSlots * 32;
 __host__ __device__ constexpr int cell(int c, int slot) { return ((c >> 4) * kSlots + slot) * 32 + 2 * (c & 15); }
+// Removed-mode Stats rows: [cycle / 16][13 slots][cycle % 16] u64 cells per mate, slot =
+// 4 * kept + code for A C T G (codes 0-3), 8 + 4 * kept for N (the G slot + 5, so an N is one
+// nibble add away from the G that its code 3 reads as), 10 for positions beyond the read.
+constexpr int kRSlots = 13;
+constexpr int kRNSlot = 8;   // removed N; kept N = kRNSlot + 4
+__host__ __device__ constexpr int rcell(int c, int slot) { return ((c >> 4) * kRSlots + slot) * 32 + 2 * (c & 15); }
+constexpr int kRemW = 2 * kRSlots * 32 * kChunks;  // both mates' removed-mode rows
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int kSmallU64 = FQ_ACC_INSERT;                 // FilterResult / adapter / polyX / merged counters
 constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
 constexpr int kInsW = (512 + 1 + 1) & ~1;                 // insert-size histogram, u32 per workgroup
 // per-read scalars are spread over kScalCopies LDS copies (lane % copies), each
 // [4 stats][reads, length_sum, q20, q30] u64; the merge variant keeps 8 (LDS budget)
 constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
+constexpr int kScalStride = FQ_SCAL_PAD ? 17 : 16;  // u64 per scalar copy (17: copies on distinct LDS bank pairs)
+constexpr int kPfW = FQ_PREFETCH ? 64 : 0;             // LDS-DMA prefetch sink (never read)
 // LEAN keeps qualities in HBM/L2 (2 workgroups = 16 waves per CU); the full variant, whose
 // trimming windows read qualities at random, stages them in LDS rows (1 workgroup per CU).  The
 // merge variant adds the post-stats block of read 1's cycles 160..319 (merged reads reach
@@ -113,10 +139,13 @@ struct Layout {
     // in removed mode, which uses blocks 0-3 as the kept/removed rows of the two mates)
     static constexpr int kHists = MERGE ? 6 : 4;
     static constexpr int kXtraW = MERGE ? kSlots * 32 : 0;  // one more cycle row: dummy positions up to 335
+    // removed mode: both mates' kept/removed rows first, then (MERGE) read 2's merged parts
+    static constexpr int kMrgOff = cmax(4 * kHistW, kRemW);
+    static constexpr int kHistRegW = cmax(kHists * kHistW, MERGE ? kMrgOff + 2 * kHistW : kRemW) + kXtraW;
     static constexpr int kColsW = kWaves * kWaveW;
     static constexpr int kScalCopies = MERGE ? 8 : 16;
-    static constexpr int kScalW = 2 * 16 * kScalCopies;
-    static constexpr int kLdsW = kColsW + kHists * kHistW + kXtraW + kSmallW + kInsW + kScalW + kAdW;
+    static constexpr int kScalW = 2 * kScalStride * kScalCopies;
+    static constexpr int kLdsW = kColsW + kHistRegW + kSmallW + kInsW + kScalW + kAdW + kPfW;
     static_assert(kLdsW * 4 * kBlocksPerCU <= 160 * 1024, "LDS budget");
     static_assert((kColsW & 1) == 0 && (kHistW & 1) == 0, "u64 cells must stay 8-byte aligned");
     static_assert(kThreads <= kBlock, "launch bound");
@@ -315,10 +344,6 @@ __device__ __forceinline__ uint32_t spread2to4(uint32_t x) {
     return (x | (x << 2)) & 0x33333333u;
 }
 
-// Removed-mode Stats rows: [cycle / 16][12 slots][cycle % 16] u64 cells per mate, slot =
-// 4 * kept + code for A C T G (codes 0-3), 8 + kept for N, 10 for positions beyond the read.
-constexpr int kRSlots = 12;
-__host__ __device__ constexpr int rcell(int c, int slot) { return ((c >> 4) * kRSlots + slot) * 32 + 2 * (c & 15); }
 
 // Unshuffle: the low bits of the 16 two-bit fields of x to bits 0-15, the high bits to 16-31.
 __device__ __forceinline__ uint32_t unzip2(uint32_t x) {
@@ -476,6 +501,41 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, in
     return firstG < 0 ? n : firstG;  // (empty window: firstGpos -1, Read::resize(-1) is a no-op)
 }
 
+// PolyX::trimPolyX's scan (src/polyx.cpp:51-77) decided on the code column while the allowance
+// keeps its first value, min(maxMM, max(1, cmp/per)) = 1 for scan indices i < 2*per - 1: with a
+// constant allowance of 1 a base b is out for good from its second non-b base on, so the loop
+// breaks at the largest such index over the masked bases (or at 0).  Returns true when that break
+// lies in the decided range and before compareReq, i.e. the read is left as it is (the common
+// case); false when the scalar restatement (trim_polyx_t) has to run.  Scan index i is forward
+// position e - i (e = the window's last base), as in polyg_bits.
+__device__ inline bool polyx_no_trim(const uint32_t* col, int c, bool rc, int st, int n, int mask, int maxMM, int per,
+                                     int compareReq) {
+    if (maxMM < 1 || per < 1 || n <= 0) return false;
+    const int e = st + n - 1;
+    const int pos0 = rc ? kMaxLen - 1 - e : e - 15;
+    const uint32_t cw = field_window(col, kFC, c, pos0), nw = field_window(col, kFN, c, pos0);
+    const int lim = min(min(2 * per - 1, 16), n);  // scan indices [0, lim) are decided here
+    const uint32_t valid = posmask(lim);
+    int brk = 0;
+    // "ATCGN"[b]: forward codes A 0, T 2, C 1, G 3 (read 2's column holds the complements)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+        if (!((mask >> b) & 1)) continue;
+        uint32_t nonb;  // forward-order spaced mask of the positions that are not b
+        if (b < 4) {
+            const uint32_t code = (uint32_t)((0x3120 >> (4 * b)) & 3) ^ (rc ? 2u : 0u);
+            nonb = (fold2(cw ^ (code * 0x55555555u)) | nw) & 0x55555555u;
+        } else {
+            nonb = ~nw & 0x55555555u;
+        }
+        if (!rc) nonb = __builtin_bitreverse32(nonb) >> 1;  // forward window -> scan order
+        nonb &= valid;
+        const uint32_t second = nonb & (nonb - 1u);
+        brk = max(brk, second ? (__ffs(second) - 1) >> 1 : 99);
+    }
+    return brk < lim && brk + 1 < compareReq;
+}
+
 __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
 
 typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // a u64 at an LDS byte address
@@ -525,11 +585,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
     uint32_t* col = lds + wave * LY::kWaveW;  // code / N columns: word field*64 + lane
     uint32_t* qrows = col + kCodeW;           // full variant: quality rows, row = lane
     uint32_t* hist = lds + LY::kColsW;        // [pre1, pre2, post1, post2] x kHistW (post1 x2 with MERGE)
-    unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + LY::kHists * kHistW + LY::kXtraW);
+    unsigned long long* small = reinterpret_cast<unsigned long long*>(hist + LY::kHistRegW);
     unsigned int* ins = reinterpret_cast<unsigned int*>(small + kSmallW / 2);
     unsigned long long* scal = reinterpret_cast<unsigned long long*>(ins + kInsW);
-    uint8_t* adp = reinterpret_cast<uint8_t*>(scal + 16 * LY::kScalCopies);
-    for (int i = threadIdx.x; i < LY::kHists * kHistW + LY::kXtraW + kSmallW + kInsW + LY::kScalW; i += kThreads) hist[i] = 0;
+    uint8_t* adp = reinterpret_cast<uint8_t*>(scal + kScalStride * LY::kScalCopies);
+    for (int i = threadIdx.x; i < LY::kHistRegW + kSmallW + kInsW + LY::kScalW; i += kThreads) hist[i] = 0;
     for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kThreads)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
     __syncthreads();
@@ -574,6 +634,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
 #define FQ_STAMP(i)
 #endif
 
+#if FQ_DESYNC
+    {   // profiling: stagger the waves that share a SIMD (wave w, w + 4 of both workgroups of a CU)
+        const int slot = (wave >> 2) + 2 * (blockIdx.x & 1);
+        for (int i = 0; i < slot * FQ_DESYNC; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
         // Per-lane values are derived from an opaque copy of the lane id inside the loop: left to
         // itself the compiler hoists dozens of them out of the tile loop and spills them.
@@ -596,6 +662,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
         const int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
 
         // ---------------- staging ----------------
+#if FQ_STAGE_PRIO
+        __builtin_amdgcn_s_setprio(FQ_STAGE_PRIO);  // profiling: staging waves issue first
+#endif
         // chunk-interleaved batch tiles (include/fqengine.h): chunk k of this lane's row is 512 B
         // after chunk k-1, so each chunk load of the wave is one (PE: two planes x 32 rows) or
         // two (SE: 64 rows) 512-byte contiguous runs
@@ -618,7 +687,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
         // ten addresses are not kept live across tiles)
         uint32_t* wp = col + lane_x + (rc ? (kChunks - 1) * 64 : 0);
         const int wstep = rc ? -64 : 64;
-        // Row chunks are requested three ahead of their use (software pipelining: one HBM round
+        // Row chunks are requested kAhead ahead of their use (software pipelining: one HBM round
         // trip per tile instead of one per chunk); every row is readable up to its stride, so
         // the look-ahead loads are clamped, never guarded.  Only the chunks that some lane's read
         // does not fill (wave-uniform test) pay for byte masks.
@@ -732,6 +801,38 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if FQ_STAGE_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+#if FQ_PREFETCH
+        // The wave's next tile is one contiguous run of R * stride bytes per plane (R = 32 pairs or
+        // 64 reads; planes span whole 32-read tiles, so the run is clamped to the rows that exist):
+        // one dword per 128-byte line, loaded into a never-read LDS sink, so the next staging finds
+        // its rows in L2 / the Infinity Cache while this tile computes.  The asm loads are outside
+        // hipcc's waitcnt bookkeeping; any later counted vmcnt wait covers them (older loads retire
+        // first), so nothing waits on them before the quality re-reads of the filter / stats.
+        {
+            const int tn = t + gridDim.x * kWaves;
+            if (tn < ntiles) {
+                constexpr int R = PAIRED ? 32 : 64;
+                const int rows = min(R, ((b.n + 31) & ~31) - tn * R);
+                // (PAIRED: the first FQ_PREFETCH chunks of the 32 rows, 512 B each)
+                const int run = PAIRED ? min(rows * b.stride, FQ_PREFETCH * 512) : rows * b.stride;
+                const uint32_t sink = (uint32_t)(LY::kLdsW - kPfW) * 4u;
+                const uint8_t* planes[4] = {b.seq1, b.qual1, b.seq2, b.qual2};
+#pragma unroll
+                for (int pi = 0; pi < (PAIRED ? 4 : 2); ++pi) {
+                    const uint8_t* base = planes[pi] + (size_t)tn * R * b.stride;
+                    for (int off = lane_x * 128; off < run; off += 64 * 128) {
+                        const uint8_t* g = base + off;
+                        unsigned keep;
+                        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                                     : "=&s"(keep) : "v"(g), "s"(sink));
+                    }
+                }
+            }
+        }
+#endif
 #if FQ_ABLATE_STAGE >= 3  // profiling only: staging, then straight to the result store
         if (valid && res)
             *reinterpret_cast<uint4*>(&res[PAIRED ? 2 * (size_t)idx + mate : (size_t)idx]) =
@@ -771,7 +872,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
             int bases;
             n = polyg_bits(col, lane, rc, st, n, p.polyg_max_mismatch, g_inv, g_per, p.polyg_compare_req, bases);
             if (bases >= 0 && !(abl & 32))  // (reads << 32 | bases) into the lane's scalar copy
-                sadd(&scal[16 * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 2], (1ull << 32) | (unsigned long long)bases);
+                sadd(&scal[kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 2], (1ull << 32) | (unsigned long long)bases);
         }
 
         FQ_STAMP(2)
@@ -792,7 +893,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
                     n = pos;
                 }
                 rr.ad_len = (uint16_t)ad_len;
-                if (ad_len > 0) sadd(&scal[16 * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 3], (1ull << 32) | (unsigned long long)ad_len);
+                if (ad_len > 0) sadd(&scal[kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 3], (1ull << 32) | (unsigned long long)ad_len);
             }
         };
         // OverlapAnalysis::analyze (src/overlapanalysis.cpp:7-72) of the pair's current windows;
@@ -882,7 +983,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
                     rr.ad_pos = (uint16_t)(st + ol);
                     rr.ad_len = (uint16_t)(n - ol);
                     if (mate == 0)
-                        sadd(&scal[16 * (lane_x & (LY::kScalCopies - 1)) + 3], (2ull << 32) | (unsigned long long)((n1 - ol) + (n2 - ol)));
+                        sadd(&scal[kScalStride * (lane_x & (LY::kScalCopies - 1)) + 3], (2ull << 32) | (unsigned long long)((n1 - ol) + (n2 - ol)));
                     n = ol;
                 } else if (!LEAN && my_alen > 0) {
                     by_sequence();
@@ -893,7 +994,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
 
         FQ_STAMP(3)
         // ---------------- polyX, maxLen (src/peprocessor.cpp:335-349) ----------------
-        if (!LEAN && both && p.polyx_enabled && !(abl & 2048)) {
+        if (!LEAN && both && p.polyx_enabled && !(abl & 2048) &&
+            !polyx_no_trim(col, lane, rc, st, n, p.polyx_mask, p.polyx_max_mismatch, p.polyx_one_mismatch_per,
+                           p.polyx_compare_req)) {
             int poly, bases;
             n = trim_polyx_t(at(seq, st), n, p.polyx_mask, p.polyx_compare_req, p.polyx_max_mismatch,
                              p.polyx_one_mismatch_per, poly, bases);
@@ -1097,18 +1200,28 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
                     if (F + 2 < kChunks) qb[(F + 2) % 3] = qchunk(min(F + 2, nchunks - 1));
                     if (F + 1 < kChunks) fn = fwd_chunk_in(col, lane_x, min(F + 1, nchunks - 1), rc);
                     const int vl = L - 16 * F;
-                    // slot 4 * kept + code; an N (code 3) is counted as a G here and moved below
+                    // slot 4 * kept + code; an N (code 3) reads as a G here
                     const unsigned long long km = ~(~0ull << min(max(w4 - 64 * F, 0), 63));
                     uint32_t lo = spread2to4(f.c) + ((uint32_t)km & 0x44444444u);
                     uint32_t hi = spread2to4(f.c >> 16) + ((uint32_t)(km >> 32) & 0x44444444u);
+#if FQ_NFOLD
+                    // N bases: their slot kRNSlot + 4 * kept is the G slot + 5, one nibble add (staging
+                    // kept N flags only inside the read)
+                    if (__any(f.n != 0)) {
+                        const uint32_t n0 = spread2to4(f.n), n1 = spread2to4(f.n >> 16);
+                        lo += n0 + (n0 << 2);
+                        hi += n1 + (n1 << 2);
+                    }
+#endif
                     if (__any(vl < 16)) {  // positions beyond the read (kept is 0 there) -> dummy slot 10
                         const unsigned long long vm = ~0ull << min(max(l4 - 64 * F, 0), 63);
                         const uint32_t dlo = (uint32_t)vm, dhi = vl >= 16 ? 0u : (uint32_t)(vm >> 32);
                         lo = (lo & ~dlo) | (dlo & 0xAAAAAAAAu);
                         hi = (hi & ~dhi) | (dhi & 0xAAAAAAAAu);
                     }
-                    // N bases (rare): move each from its G cell (slot 4 * kept + 3) to slot 8 + kept
-                    // (staging kept N flags only inside the read)
+#if !FQ_NFOLD
+                    // N bases (profiling baseline): move each from its G cell (slot 4 * kept + 3) to
+                    // slot kRNSlot + 4 * kept
                     uint32_t nv = f.n;
                     if (__any(nv != 0)) {
                         const uint32_t qs[4] = {q0, q1, q2, q3};
@@ -1119,12 +1232,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
                             const unsigned long long v = kCount1 | (unsigned long long)__builtin_amdgcn_ubfe(qs[t >> 2], 8 * (t & 3), 8);
                             const uint32_t a = (uint32_t)(LY::kColsW + mate * (kRSlots * 32 * kChunks)) * 4u +
                                                (uint32_t)(F * kRSlots * 32 * 4) + 8u * (uint32_t)t;
-                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(8 + kept) * 128u)), v,
+                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(kRNSlot + 4 * kept) * 128u)), v,
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(4 * kept + 3) * 128u)), 0ull - v,
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     }
+#endif
                     // rotate by r positions: rotated position t is 16F + (t + r) % 16
                     const uint32_t xa = rswap ? hi : lo, xb = rswap ? lo : hi;
                     const uint32_t klo = __builtin_amdgcn_alignbit(xb, xa, rr4), khi = __builtin_amdgcn_alignbit(xa, xb, rr4);
@@ -1155,7 +1269,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
             // so merged position j is column index 159 - pos_hi + j (codes already complemented);
             // its quality is read 2's byte at forward position pos_hi - j.  Cells: cycle rows of
             // the extra block, count << 40 | sum(q); N bases are counted as G and moved.
-            const uint32_t xb = (uint32_t)(LY::kColsW + 4 * kHistW) * 4u;
+            const uint32_t xb = (uint32_t)(LY::kColsW + LY::kMrgOff) * 4u;
             const int pos_hi = ws + wn - 1;
             const int ci0 = kMaxLen - 1 - pos_hi;
             uint32_t rb[16];
@@ -1275,7 +1389,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
         if (valid && !(abl & 4)) {
             // per-read Stats scalars: (reads, length_sum) packed as count << 32 | sum, plus
             // q20 << 32 | q30, into one of 16 LDS copies (lanes l, l + 16 share one)
-            unsigned long long* sc = scal + 16 * (lane_x & (LY::kScalCopies - 1)) + 4 * mate;
+            unsigned long long* sc = scal + kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate;
             sadd(&sc[0], (1ull << 32) | (unsigned long long)L);
             sadd(&sc[1], ((unsigned long long)q20 << 32) | q30);
             const bool post_here = (MERGE && merged) ? (post_on && mate == 0) : post_on;
@@ -1325,7 +1439,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
         const int k = threadIdx.x >> 2, f = threadIdx.x & 3;
         unsigned long long v = 0;
         for (int c = 0; c < LY::kScalCopies; ++c) {
-            const unsigned long long w = scal[16 * c + 4 * k + (f >> 1)];
+            const unsigned long long w = scal[kScalStride * c + 4 * k + (f >> 1)];
             v += (f & 1) ? (w & 0xFFFFFFFFull) : (w >> 32);
         }
         if (v) atomicAdd(&acc[st_base + k * st_words + f], v);  // FQ_ST_READS, _LENGTH_SUM, _Q20, _Q30
@@ -1334,7 +1448,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
         unsigned long long rd = 0, bs = 0;
         for (int c = 0; c < LY::kScalCopies; ++c)
             for (int m = 0; m < 2; ++m) {
-                const unsigned long long w = scal[16 * c + 4 * m + slot];
+                const unsigned long long w = scal[kScalStride * c + 4 * m + slot];
                 rd += w >> 32;
                 bs += w & 0xFFFFFFFFull;
             }
@@ -1347,8 +1461,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
             const int k = i / (ncyc * 5), j = i - k * ncyc * 5;
             const int c = j / 5, slot = j - c * 5;  // slots A C T G N
             const uint32_t* hk = hist + k * (kRSlots * 32 * kChunks);
-            const unsigned long long kept = *reinterpret_cast<const unsigned long long*>(hk + rcell(c, slot < 4 ? 4 + slot : 9));
-            const unsigned long long rem = *reinterpret_cast<const unsigned long long*>(hk + rcell(c, slot < 4 ? slot : 8));
+            const unsigned long long kept = *reinterpret_cast<const unsigned long long*>(hk + rcell(c, slot < 4 ? 4 + slot : kRNSlot + 4));
+            const unsigned long long rem = *reinterpret_cast<const unsigned long long*>(hk + rcell(c, slot < 4 ? slot : kRNSlot));
             const int cls = slot_class(slot);
             const unsigned long long vals[2] = {kept + rem, kept};
 #pragma unroll
@@ -1364,7 +1478,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
     }
     if (MERGE && removed_mode) {  // read 2's merged parts: post1 (acc block 2) at cycles < 320
         const int ncyc = min(2 * kMaxLen, p.max_cycles);
-        const uint32_t* hx = hist + 4 * kHistW;
+        const uint32_t* hx = hist + LY::kMrgOff;
         for (int i = threadIdx.x; i < ncyc * 5; i += kThreads) {
             const int c = i / 5, slot = i - c * 5;
             const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hx + cell(c, slot));

@@ -107,6 +107,36 @@ def edge_pack(n, paired, stride=160, seed=7):
     return pk
 
 
+def polyx_pack(n, paired, stride=160, seed=11):
+    """Reads ending in a homopolymer tail (A, T, C, G or N) of 1-24 bases with 0-3 substitutions at
+    random tail positions, ahead of which sits random sequence: polyX scans that break before, at
+    and after the compare requirement and the first allowance step (src/polyx.cpp:45-101)."""
+    rng = random.Random(seed)
+    pk = Pack(n, stride, paired)
+    for i in range(n):
+        for m in ((1, 2) if paired else (1,)):
+            L = rng.choice([8, 12, 16, 30, 75, 100, 149, 150])
+            seq = bytearray(bytes(rng.choice(b"ACGT") for _ in range(L)))
+            x = rng.choice(b"ATCGN")
+            t = min(L, rng.randint(1, 24))
+            for k in range(L - t, L):
+                seq[k] = x
+            for _ in range(rng.choice([0, 0, 1, 1, 2, 3])):
+                k = rng.randint(max(0, L - t - 2), L - 1)
+                seq[k] = rng.choice(b"ACGTN")
+            qual = bytes(33 + rng.randint(20, 40) for _ in range(L))
+            pk.set(i, m, bytes(seq), qual)
+    return pk
+
+
+def polyx_params(paired, mask, max_mm, per, compare_req, max_cycles=512):
+    p = abi.default_params(paired=paired, max_cycles=max_cycles)
+    p.qual_filter_enabled = 1
+    p.polyx_enabled = 1
+    p.polyx_mask, p.polyx_max_mismatch, p.polyx_one_mismatch_per, p.polyx_compare_req = mask, max_mm, per, compare_req
+    return p
+
+
 def config(name, max_cycles=256):
     """Parameter presets: the BASELINE configs plus extra option coverage."""
     paired = name not in ("C2", "SE_adapter", "SE_all", "SE_umi")

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from fqtool_amd import abi
-from batch_util import ALL_CONFIGS, Pack, config, edge_pack, run_oracle, synth_pack
+from batch_util import ALL_CONFIGS, Pack, config, edge_pack, polyx_pack, polyx_params, run_oracle, synth_pack
 
 pytestmark = pytest.mark.gpu
 
@@ -64,6 +64,20 @@ def assert_same(p, res_o, acc_o, res_e, acc_e):
 def test_synthetic_parity(eng_lib, oracle, name, mode):
     p = config(name, max_cycles=512)
     pk = synth_pack(oracle, 6000, bool(p.paired), first=12345)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+@pytest.mark.parametrize("paired", [True, False])
+@pytest.mark.parametrize("mask,max_mm,per,req", [(0b11111, 5, 8, 10), (0b01101, 5, 8, 10), (0b10000, 2, 3, 6),
+                                                 (0b00001, 1, 1, 3), (0b01111, 0, 8, 10), (0b00000, 5, 8, 1),
+                                                 (0b01111, 5, 20, 16)])
+def test_polyx_tails(eng_lib, oracle, paired, mask, max_mm, per, req):
+    """The fast kernels decide most polyX scans on the code column (polyx_no_trim) and run the
+    scalar restatement for the rest: both against the oracle on homopolymer tails."""
+    p = polyx_params(paired, mask, max_mm, per, req)
+    pk = polyx_pack(4000, paired, seed=mask * 131 + max_mm * 7 + per + req)
     res_o, acc_o = run_oracle(oracle, p, pk)
     res_e, acc_e = run_engine(eng_lib, p, pk)
     assert_same(p, res_o, acc_o, res_e, acc_e)

@@ -1,0 +1,34 @@
+"""Profiling aid: median kernel ms of the fast kernel over several launches (after one warm-up)
+for each config in CONFIGS, with the engine library FQ_ENGINE_LIB (A/B builds, tools/ab.sh)."""
+import ctypes, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from fqtool_amd import abi
+import bench
+
+lib = abi.load_engine()
+dev = torch.device("cuda:0")
+n, stride = int(os.environ.get("PAIRS", 20_000_000)), 160
+bufs = [torch.empty(abi.batch_bytes(n, stride), dtype=torch.uint8, device=dev) for _ in range(4)]
+lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
+b = abi.FqBatch(); b.n, b.stride = n, stride
+b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
+b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
+assert lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 0, 150, None) == 0
+res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+torch.cuda.synchronize()
+tag = os.environ.get("TAG", "")
+for cfg in os.environ.get("CONFIGS", "C3").split():
+    p = bench.config_params(abi, cfg)
+    if cfg == "C2":
+        b.seq2 = b.qual2 = None
+    h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
+    ms = []
+    for i in range(int(os.environ.get("LAUNCHES", 6))):
+        lib.fq_engine_process_device(h, ctypes.byref(b), res.data_ptr(), None); lib.fq_engine_sync(h)
+        if i: ms.append(lib.fq_engine_last_kernel_ms(h))
+    lib.fq_engine_destroy(h)
+    ms.sort()
+    print(f"{tag} {cfg} median {ms[len(ms)//2]:.3f} min {ms[0]:.3f}", flush=True)
+    if cfg == "C2":
+        b.seq2, b.qual2 = bufs[2].data_ptr(), bufs[3].data_ptr()
