@@ -81,6 +81,9 @@ namespace {
 #ifndef FQ_DESYNC
 #define FQ_DESYNC 0  // profiling: initial s_sleep stagger of co-resident waves
 #endif
+#ifndef FQ_CUT_W4
+#define FQ_CUT_W4 1  // cut_right windows <= 4 decided per low chunk (0: the word-stream scan, profiling)
+#endif
 #ifndef FQ_PREFETCH
 #define FQ_PREFETCH 0  // profiling: after staging, pull the first FQ_PREFETCH chunks of the wave's next tile
                        // toward L2 with LDS-DMA loads (0: off; measured slower at 10)
@@ -536,6 +539,69 @@ __device__ inline bool polyx_no_trim(const uint32_t* col, int c, bool rc, int st
     return brk < lim && brk + 1 < compareReq;
 }
 
+// The four bit-7 flags of a dword's bytes as a nibble (byte k -> bit k)
+__device__ __forceinline__ uint32_t flags4(uint32_t t) {
+    return ((t >> 7) | (t >> 14) | (t >> 21) | (t >> 28)) & 0xFu;
+}
+
+// Filter::trimAndCut (src/filter.cpp:69-189) when cut_right is its only window option and the
+// window is at most 4 bases (the default is 4): low_window_scan's result, but each chunk that holds a
+// quality below the threshold (bit c of low_chunks, from staging) is decided at once from three
+// 16-byte row chunks c-1, c, c+1 (one L2 round trip instead of one per 4 positions): the windows
+// starting at 16c-3 .. 16c+15 are summed with v_sad_u8 on realigned dwords (exact integer
+// test sum < T*w, win_ge), and the first base below the threshold at or after the first low
+// window (the reference's `while (qual(s) >= thr) ++s`, which stops inside that window) comes from
+// the bytes' below-threshold flags.  limr = (128 - T) per byte (qualities < 128 in these tiles).
+__device__ inline bool cut_right_w4(const fq_params& p, const uint8_t* Q, int nchunks, int l, int front, int tail,
+                                    uint32_t low_chunks, uint32_t limr, int& out_start, int& out_len) {
+    int rlen = l - front - tail;
+    if (rlen < 0) return false;
+    const int w = p.cut_right_window, thr = 33 + p.cut_right_quality;
+    if (l - front - tail - w <= 0) return false;
+    const int send = l - tail - w;  // window starts [front, send) are scanned
+    const uint32_t TW = (uint32_t)(thr * w), wm = bytemask(w);
+    constexpr int cst = FQ_TILE_READS * FQ_CHUNK;
+    int from = front, cut = -1;  // cut: the first base below the threshold from the first low window on
+    uint32_t lc = low_chunks;
+    while (lc) {
+        const int c = __ffs(lc) - 1;
+        lc &= lc - 1u;
+        const int a = max(from, 16 * c - w + 1), bnd = min(send, 16 * c + 16);
+        if (a < bnd) {
+            const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+            const uint4 q0 = c > 0 ? *reinterpret_cast<const uint4*>(Q + cst * (c - 1)) : z;
+            const uint4 q1 = *reinterpret_cast<const uint4*>(Q + cst * c);
+            const uint4 q2 = c + 1 < nchunks ? *reinterpret_cast<const uint4*>(Q + cst * (c + 1)) : z;
+            const uint32_t d[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+            uint32_t win = 0;  // bit j: the window starting at 16c - 3 + j is low
+#pragma unroll
+            for (int j = 0; j < 19; ++j) {
+                const int o = 13 + j;  // its byte offset in d
+                const uint32_t W = (o & 3) ? __builtin_amdgcn_alignbyte(d[(o >> 2) + 1], d[o >> 2], o & 3) : d[o >> 2];
+                win |= (__builtin_amdgcn_sad_u8(W & wm, 0u, 0u) < TW ? 1u : 0u) << j;
+            }
+            const int lo = a - (16 * c - 3), hi = bnd - (16 * c - 3);  // 0 <= lo < hi <= 19
+            win &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+            if (win) {
+                const int j = __ffs(win) - 1;
+                // below-threshold flags of bytes 12..35 of d (bit i: byte 12 + i)
+                uint32_t lowb = 0;
+#pragma unroll
+                for (int k = 3; k < 9; ++k) lowb |= flags4(~(d[k] + limr) & 0x80808080u) << (4 * (k - 3));
+                cut = 16 * c - 3 + j + __ffs(lowb >> (j + 1)) - 1;  // (the window holds such a base)
+                break;
+            }
+        }
+        from = max(from, bnd);
+        if (from >= send) break;
+    }
+    if (cut >= 0) rlen = cut - front;
+    if (rlen <= 0 || front >= l - 1) return false;
+    out_start = front;
+    out_len = min(rlen, l - front);
+    return true;
+}
+
 __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
 
 typedef __attribute__((address_space(3))) unsigned long long LdsU64;  // a u64 at an LDS byte address
@@ -612,6 +678,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
     // cut_right threshold 33 + q, in 0..93 (CLI range): the same SWAR below-threshold test
     const bool lowr_ok = p.cut_right && 33 + p.cut_right_quality >= 1 && 33 + p.cut_right_quality <= 127;
     const uint32_t limr = lowr_ok ? (uint32_t)(0x80 - (33 + p.cut_right_quality)) * 0x01010101u : 0u;
+    // cut_right as the only window option, window <= 4: cut_right_w4
+    const bool cut_w4 = FQ_CUT_W4 && lowr_ok && !p.cut_front && !p.cut_tail && p.cut_right_window >= 1 && p.cut_right_window <= 4;
     // Without front trimming every kept window starts at 0, so each base lands in exactly one of
     // two disjoint blocks: "kept" (inside a passing read's window; the post block) or "removed"
     // (trimmed tails, failed pairs; the pre block), one LDS atomic per base.  At the flush
@@ -855,6 +923,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
                 nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n, lowr_ok ? lowr : ~0u);
             else
                 nn = valid && ((abl & 1024) ? (n = L, true)
+                               : cut_w4 ? cut_right_w4(p, Q, nchunks, L, front, tail, lowr, limr, st, n)
                                         : trim_and_cut_t(p, seq, RowQual{Q, b.stride >> 2}, L, front, tail, st, n, lowr_ok ? lowr : ~0u));
         }
         // the shuffle must run in every lane: ds_bpermute from a lane that is switched off returns

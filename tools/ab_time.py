@@ -20,6 +20,7 @@ torch.cuda.synchronize()
 tag = os.environ.get("TAG", "")
 for cfg in os.environ.get("CONFIGS", "C3").split():
     p = bench.config_params(abi, cfg)
+    p.reserved[0] = int(os.environ.get("ABL", 0))  # ablation bits (pe_fast.hip; results invalid when set)
     if cfg == "C2":
         b.seq2 = b.qual2 = None
     h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
