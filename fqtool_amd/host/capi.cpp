@@ -217,14 +217,16 @@ char* fqh_debug_records(const char* path, int bulk, int buf_size, int pack_n, in
         out.append(a, la).append("\t").append(b, lb).append("\t").append(c, lc).append("\t").append(d, ld).append("\n");
     };
     try {
-        if (bulk) {
+        if (bulk) {  // 2: with the parallel fast path (read_fast on a 3-worker pool) ahead of read()
             FqBulkReader r(path, phred64 != 0, buf_size);
             ByteBuf text;
             Rec rc;
             std::vector<Rec> recs;
+            std::unique_ptr<Pool> pool(bulk == 2 ? new Pool(3) : nullptr);
             for (bool more = true; more;) {
                 r.begin(text);
                 recs.clear();
+                if (pool) r.read_fast(recs, (size_t)pack_n, pool.get());
                 while ((int)recs.size() < pack_n && (more = r.read(rc))) recs.push_back(rc);
                 const char* t = r.end();
                 for (const Rec& x : recs)

@@ -444,6 +444,140 @@ bool FqBulkReader::read(Rec& r) {  // FqReader::read, src/fqreader.cpp:160-195
     return true;
 }
 
+// Parallel record location for a mapped file.  On a "plain" stretch -- every line ends in a single
+// '\n', no line is empty (so no terminator is ever followed by a '\n' and getLine's 1 MiB-buffer
+// folding rule, src/fqreader.cpp:139-140, never applies), every record's first line starts with
+// '@' (so the skip loop of src/fqreader.cpp:169-171 never skips) and quality and sequence lengths
+// agree (no error) -- FqReader::read is "four lines per record", which segments of the mapping can
+// apply independently.  Segment k > 0 starts at its first line that looks like a record start ('@'
+// line, a line, a '+' line, a line as long as the second); its records are kept only when segment
+// k-1's parse ends exactly there (it started at a true record start, so its end is one), so a
+// wrong guess is never used.  The fast path stops at the first segment it cannot take, or at the
+// first irregular record, or where a record is not complete inside the region; read() continues
+// from there with the exact rules.  Phred64 conversion is applied to the kept records only.
+size_t FqBulkReader::read_fast(std::vector<Rec>& out, size_t max_n, Pool* pool) {
+    if (!map_ || !pool || max_n < 1024 || pos_ >= map_size_) return 0;
+    char* d = map_;
+    const size_t r0 = pos_, avg = avg_rec_ ? avg_rec_ : 512;
+    const size_t r1 = std::min(map_size_, r0 + max_n * avg + max_n * avg / 16 + (1u << 16));
+    const size_t words = (r1 - r0 + 63) >> 6;
+    std::vector<uint64_t> bm(words + 1, 0);  // bit i of word w: byte r0 + 64 w + i is '\r' / '\n'
+    const int K = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool->size() * 2, (r1 - r0) >> 20));
+    const __m128i nl = _mm_set1_epi8('\n'), cr = _mm_set1_epi8('\r');
+    pool->run(K, [&](int k) {
+        const size_t w0 = words * k / K, w1 = words * (k + 1) / K;
+        for (size_t w = w0; w < w1; ++w) {
+            const size_t base = r0 + (w << 6);
+            uint64_t m = 0;
+            if (base + 64 <= r1) {
+                for (int j = 0; j < 4; ++j) {
+                    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(d + base + 16 * j));
+                    m |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(v, nl), _mm_cmpeq_epi8(v, cr)))
+                         << (16 * j);
+                }
+            } else {
+                for (size_t i = base; i < r1; ++i)
+                    if (d[i] == '\n' || d[i] == '\r') m |= 1ull << (i - base);
+            }
+            bm[w] = m;
+        }
+    });
+    // first terminator at or after byte x (absolute), or r1
+    auto term = [&](size_t x) -> size_t {
+        if (x >= r1) return r1;
+        size_t w = (x - r0) >> 6;
+        uint64_t bits = bm[w] & (~0ull << ((x - r0) & 63));
+        while (!bits) {
+            if (++w >= words) return r1;
+            bits = bm[w];
+        }
+        return std::min(r1, r0 + (w << 6) + (size_t)__builtin_ctzll(bits));
+    };
+    struct Seg {
+        size_t start = SIZE_MAX, stop = SIZE_MAX;  // first record; where the parse ended
+        bool clean = false;                        // ended at the segment's end (not at a problem)
+        std::vector<Rec> recs;
+    };
+    std::vector<Seg> segs((size_t)K);
+    auto bound = [&](int k) { return k >= K ? r1 : r0 + (r1 - r0) * (size_t)k / (size_t)K; };
+    pool->run(K, [&](int k) {
+        Seg& sg = segs[(size_t)k];
+        size_t x;
+        if (k == 0) {
+            x = r0;
+        } else {  // the first record-like line at or after the segment's start
+            x = term(bound(k) - 1) + 1;
+            for (int tries = 0;; ++tries) {
+                if (tries == 16 || x >= bound(k + 1)) return;
+                const size_t a = term(x), b = term(a + 1), c = term(b + 1), e = term(c + 1);
+                if (e >= r1) return;
+                if (d[x] == '@' && b + 1 < r1 && d[b + 1] == '+' && e - c == b - a) break;
+                x = a + 1;
+            }
+        }
+        sg.start = x;
+        const size_t lim = bound(k + 1);
+        sg.recs.reserve((lim - x) / avg + 16);
+        while (x < lim) {
+            const size_t t0 = term(x), t1 = term(t0 + 1), t2 = term(t1 + 1), t3 = term(t2 + 1);
+            if (t3 >= r1 || d[x] != '@' || d[t0] != '\n' || d[t1] != '\n' || d[t2] != '\n' || d[t3] != '\n' ||
+                t0 == x || t1 == t0 + 1 || t2 == t1 + 1 || t3 == t2 + 1 || t3 - t2 != t1 - t0)
+                break;  // not plain (or incomplete in the region): the exact reader takes over here
+            Rec r;
+            r.off = x;
+            r.name_len = (uint32_t)(t0 - x);
+            r.len = (uint32_t)(t1 - t0 - 1);
+            r.strand_len = (uint32_t)(t2 - t1 - 1);
+            r.gap[0] = r.gap[1] = r.gap[2] = 1;
+            sg.recs.push_back(r);
+            x = t3 + 1;
+        }
+        sg.stop = x;
+        sg.clean = x >= lim;
+    });
+    // stitch: segment k is taken while it starts where segment k-1 ended
+    size_t x = r0, got = 0;
+    std::vector<std::pair<int, size_t>> taken;  // (segment, records taken)
+    for (int k = 0; k < K && got < max_n; ++k) {
+        const Seg& sg = segs[(size_t)k];
+        if (sg.start != x) break;
+        const size_t take = std::min(sg.recs.size(), max_n - got);
+        if (take) {
+            taken.emplace_back(k, take);
+            got += take;
+            const Rec& last = sg.recs[take - 1];
+            x = last.qual_off() + last.len + 1;
+        }
+        if (take < sg.recs.size() || !sg.clean) {
+            if (take == sg.recs.size()) x = sg.stop;
+            break;
+        }
+    }
+    if (!got) return 0;
+    const size_t o0 = out.size();
+    out.resize(o0 + got);
+    std::vector<size_t> at(taken.size());
+    for (size_t i = 0, a = o0; i < taken.size(); ++i) {
+        at[i] = a;
+        a += taken[i].second;
+    }
+    pool->run((int)taken.size(), [&](int i) {
+        const Seg& sg = segs[(size_t)taken[(size_t)i].first];
+        const size_t cnt = taken[(size_t)i].second;
+        std::memcpy(out.data() + at[(size_t)i], sg.recs.data(), cnt * sizeof(Rec));
+        if (phred64_)  // Read::convertPhread64To33, src/read.h:71-75 (char arithmetic)
+            for (size_t j = 0; j < cnt; ++j) {
+                char* q = d + sg.recs[j].qual_off();
+                for (uint32_t b = 0; b < sg.recs[j].len; ++b) q[b] = (char)std::max(33, (int)q[b] - (64 - 33));
+            }
+    });
+    avg_rec_ = std::max<size_t>(16, (x - r0) / got);
+    pos_ = x;
+    tbase_ = pos_ >> 6;  // read() indexes afresh from here
+    indexed_ = tbase_ << 6;
+    return got;
+}
+
 // ---- Pool ----
 struct Pool::Impl {
     struct Job {
@@ -621,11 +755,11 @@ PackReader::PackReader(const std::string& in1, const std::string& in2, bool inte
 }
 
 namespace {
-size_t read_mate(FqBulkReader& r, Pack& pk, int m, size_t max_n) {
+size_t read_mate(FqBulkReader& r, Pack& pk, int m, size_t max_n, Pool* pool) {
     r.begin(pk.text[m]);
     Rec rc;
-    size_t k = 0;
     pk.rec[m].reserve(max_n);
+    size_t k = r.read_fast(pk.rec[m], max_n, pool);  // (mapped input: the plain stretch in parallel)
     while (k < max_n && r.read(rc)) {
         pk.rec[m].push_back(rc);
         ++k;
@@ -642,7 +776,7 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     pk.paired = paired_;
     size_t n = 0;
     if (!paired_) {
-        n = read_mate(r1_, pk, 0, max_n);
+        n = read_mate(r1_, pk, 0, max_n, pool);
         if (n < max_n) {
             done_ = true;
             if (!r1_.error().empty()) reader_stderr(r1_.error());
@@ -672,8 +806,8 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
         // and a mate reports its error only if its failure is at that index (both do, read 1
         // first, when they fail at the same index).
         size_t n2 = 0;
-        std::thread t([&] { n2 = read_mate(*r2_, pk, 1, max_n); });
-        const size_t n1 = read_mate(r1_, pk, 0, max_n);
+        std::thread t([&] { n2 = read_mate(*r2_, pk, 1, max_n, pool); });
+        const size_t n1 = read_mate(r1_, pk, 0, max_n, pool);
         t.join();
         n = std::min(n1, n2);
         if (n < max_n) {

@@ -145,6 +145,8 @@ class FqReader {
 // (src/fqreader.cpp:90-150), so reads stay aligned to buf_size multiples of the stream and the
 // rule is evaluated on stream offsets.  Bytes read past the last record of a pack are carried
 // into the next pack's arena.
+class Pool;
+
 class FqBulkReader {
    public:
     FqBulkReader(const std::string& path, bool phred64, int buf_size = 1 << 20);
@@ -156,6 +158,10 @@ class FqBulkReader {
     // next record into the arena given to begin(); false at end of input or on a
     // quality/sequence length mismatch (message in error())
     bool read(Rec& r);
+    // Parallel fast path of read() for a mapped regular file: appends up to max_n records to `out`
+    // from the "plain" stretch at the read position (see fastq.cpp) and returns their count;
+    // read() then continues exactly where it stopped.  0 when the input is not mapped.
+    size_t read_fast(std::vector<Rec>& out, size_t max_n, Pool* pool);
     // the arena is done: unconsumed bytes are carried to the next begin(); returns the base
     // the records' offsets refer to (the arena, or the file mapping)
     const char* end();
@@ -185,6 +191,7 @@ class FqBulkReader {
     size_t tbase_ = 0, indexed_ = 0;
     char* map_ = nullptr;  // a regular file is read through a private mapping (zero copy)
     size_t map_size_ = 0;
+    size_t avg_rec_ = 0;   // mean record bytes seen by read_fast (sizes its next region)
     std::string err_;
 };
 

@@ -68,3 +68,51 @@ def test_bulk_reader_exact_multiple_of_buffer(host, tmp_path):
         assert records(host, str(path), 1, buf, 7) == want, buf
     # with 1 MiB buffers every record parses
     assert records(host, str(path), 1, 1 << 20, 7).count("\n") == 50
+
+
+def plain_with_hazards(rng, n_rec, hazards):
+    """Mostly plain FASTQ (several MiB, so the fast path splits it into segments) with a few hostile
+    spots: CRLF or CR records, blank lines, garbage lines, qualities starting with '@' or '+',
+    an empty sequence, a length mismatch (the input's last record)."""
+    out = []
+    spots = set(rng.sample(range(n_rec), hazards))
+    for i in range(n_rec):
+        L = rng.choice([36, 100, 150, 151, 250])
+        seq = bytes(rng.choice(b"ACGTN") for _ in range(L))
+        qual = bytearray(rng.randint(59, 104) for _ in range(L))
+        if rng.random() < 0.02:
+            qual[0] = ord(rng.choice("@+"))  # record-start look-alikes for the segment guess
+        nl = b"\n"
+        if i in spots:
+            kind = rng.randrange(6)
+            if kind == 5 and i < n_rec * 9 // 10:
+                kind = 0  # (the mismatch only near the end: reading stops there)
+            if kind == 0:
+                nl = b"\r\n"
+            elif kind == 1:
+                out.append(b"\n")
+            elif kind == 2:
+                out.append(b"garbage\n")
+            elif kind == 3:
+                nl = b"\r"
+            elif kind == 4:
+                seq, qual = b"", bytearray()
+            else:
+                out.append(b"@x\nACGT\n+\nIII\n")  # length mismatch: reading stops here
+        out.append(b"@r%d extra" % i + nl + seq + nl + b"+" + nl + bytes(qual) + nl)
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_parallel_fast_path_equals_line_reader(host, tmp_path, seed):
+    rng = random.Random(100 + seed)
+    text = plain_with_hazards(rng, 30000 if seed < 4 else 45000, [0, 1, 3, 8, 20, 0][seed])
+    if seed == 5:
+        text = text.rstrip(b"\n")  # unterminated last line
+    path = tmp_path / "big.fq"
+    path.write_bytes(text)
+    want = records(host, str(path), 0, 1 << 20, phred64=seed % 2)
+    assert want.count("\n") > 1000
+    for pack_n in (1500, 7000, 100000):
+        got = records(host, str(path), 2, 1 << 20, pack_n, phred64=seed % 2)
+        assert got == want, pack_n
