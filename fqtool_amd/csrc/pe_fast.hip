@@ -1,12 +1,13 @@
-// pe_fast.hip -- hot path for paired-end packs on gfx950 (everything except -m merge).
+// pe_fast.hip -- hot path for paired-end and single-end packs on gfx950 (incl. -m merge).
 //
 // Mapping: one workgroup = 8 waves, one wave = a tile of 32 pairs, one LANE = one READ
 // (lanes 0-31 read 1, lanes 32-63 read 2 of the same pairs), so every per-read operation of
 // PairEndProcessor::processPairEnd (reference src/peprocessor.cpp:261-508) keeps all 64 lanes
 // busy and the two mates of a pair are lanes l and l^32 of the same wave.
 //
-// Occupancy: 2 workgroups (16 waves) per CU; the only per-wave LDS is the 2-bit code / N-mask
-// column block (5 KB), and the workgroup's Stats histograms are shared by its 8 waves.
+// Occupancy: 16 waves per CU (2 workgroups of 8, the merge variant 1 of 16); the only per-wave
+// LDS is the 2-bit code / N-mask column block (5 KB), and a workgroup's Stats histograms are
+// shared by its waves.
 //
 // Staging: each lane streams its seq and qual rows from HBM with 16-byte loads (the batch's
 // chunk-interleaved tiles make each wave-wide chunk load contiguous).  Sequence bytes
@@ -58,7 +59,7 @@ namespace {
 #define FQ_SCHED_PIN 1
 #endif
 #ifndef FQ_MERGE_WAVES
-#define FQ_MERGE_WAVES 8  // profiling switches of the merge variant without LDS quality rows
+#define FQ_MERGE_WAVES 16  // merge variant: one workgroup of 16 waves per CU (8: 10.8, 12: 9.4, 16: 9.0 ms per 20 M pairs)
 #endif
 #ifndef FQ_MERGE_BLOCKS
 #define FQ_MERGE_BLOCKS 1
@@ -84,12 +85,15 @@ namespace {
 #ifndef FQ_CUT_W4
 #define FQ_CUT_W4 1  // cut_right windows <= 4 decided per low chunk (0: the word-stream scan, profiling)
 #endif
+#ifndef FQ_FILTER_BATCH
+#define FQ_FILTER_BATCH 1  // passFilter's trimmed / direct ranges: row chunks loaded four at a time
+#endif
 #ifndef FQ_PREFETCH
 #define FQ_PREFETCH 0  // profiling: after staging, pull the first FQ_PREFETCH chunks of the wave's next tile
                        // toward L2 with LDS-DMA loads (0: off; measured slower at 10)
 #endif
 constexpr int kAhead = FQ_AHEAD;  // staging: row chunks requested this many chunks ahead of their use
-constexpr int kBlock = 512;  // launch bound: 8 waves (7 in the merge variant)
+constexpr int kBlock = 1024;  // largest workgroup (the launch bound of each variant is its own size)
 #ifndef FQ_MAXLEN
 #define FQ_MAXLEN 160  // pe_fast_long.hip builds this file again for reads up to 320 bp
 #endif
@@ -125,10 +129,10 @@ constexpr int kInsW = (512 + 1 + 1) & ~1;                 // insert-size histogr
 constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
 constexpr int kScalStride = FQ_SCAL_PAD ? 17 : 16;  // u64 per scalar copy (17: copies on distinct LDS bank pairs)
 constexpr int kPfW = FQ_PREFETCH ? 64 : 0;             // LDS-DMA prefetch sink (never read)
-// LEAN keeps qualities in HBM/L2 (2 workgroups = 16 waves per CU); the full variant, whose
-// trimming windows read qualities at random, stages them in LDS rows (1 workgroup per CU).  The
-// merge variant adds the post-stats block of read 1's cycles 160..319 (merged reads reach
-// len1 + len2) and gives up a wave for it.
+// Every variant re-reads qualities from the rows in L2 (no LDS quality rows) and runs 16 waves
+// per CU: LEAN and FULL as 2 workgroups of 8 waves (128 VGPRs), the merge variant, whose Stats
+// blocks are larger (read 2's merged parts land at read 1's post cycles up to 319), as one
+// workgroup of 16 waves.  The long-read build (320-position columns) fits one 8-wave workgroup.
 template <bool LEAN, bool MERGE = false>
 struct Layout {
     // quality rows staged in LDS (off: rows are re-read from L2); profiling switch for the merge variant
@@ -641,7 +645,7 @@ __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) &
 // reverse-complemented for the overlap scan); single-end: a tile is 64 reads, one per lane, with
 // SingleEndProcessor::processSingleEnd's order (src/seprocessor.cpp:290-360).
 template <bool LEAN, bool PAIRED, bool MERGE>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
+__global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1150,6 +1154,28 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
                             if (need_tq) tq -= (int)__builtin_amdgcn_sad_u8(wq[j] & ((rf >> 7) * 0xFFu), 0u, 0u);
                         }
                     };
+#if FQ_FILTER_BATCH
+                    if (!LEAN && a0 < a1) {
+                        // (FULL) the range's row chunks from L2, four requested together per round
+                        // trip (LEAN, whose ranges are the trimmed tails only, is faster as below)
+                        for (int Fb = F0; Fb < F1; Fb += 4) {
+                            uint4 qa[4];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) qa[i] = qchunk(min(Fb + i, nchunks - 1));
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+                                if (Fb + i < F1) sub(qa[i], Fb + i);
+                        }
+                    } else if (LEAN && part == 1 && a0 < a1) {
+                        uint4 qa[2];
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) qa[i] = qchunk(max(F1 - 1 - i, 0));
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+                            if (F1 - 1 - i >= F0) sub(qa[i], F1 - 1 - i);
+                        for (int F = F1 - 3; F >= F0; --F) sub(qchunk(F), F);
+                    }
+#else
                     if (part == 1 && a0 < a1) {
                         // the tail, from the 3' end: its last two chunks are requested together
                         // (one L2 round trip for most reads), longer adapter tails loop
@@ -1169,6 +1195,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(Lay
                             cur = nxt;
                         }
                     }
+#endif
                     // N bits of the same range (read 2's column is reverse-complemented)
                     const int s0 = rc ? kMaxLen - a1 : a0, s1 = rc ? kMaxLen - a0 : a1;
                     for (int c = s0 >> 4; c < ((s1 + 15) >> 4); ++c) {
