@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 out=build/alt/$name; mkdir -p $out
 HIPFLAGS="-std=c++17 -O3 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result"
-/opt/rocm/bin/hipcc $HIPFLAGS "$@" -c fqtool_amd/csrc/pe_fast.hip -o $out/pe_fast.o &
+/opt/rocm/bin/hipcc $HIPFLAGS "$@" -c fqtool_amd/csrc/${PE_FAST_SRC:-pe_fast.hip} -o $out/pe_fast.o &
 /opt/rocm/bin/hipcc $HIPFLAGS "$@" -c fqtool_amd/csrc/pe_fast_long.hip -o $out/pe_fast_long.o &
 wait
 objs=""
