@@ -88,6 +88,9 @@ namespace {
 #ifndef FQ_FILTER_BATCH
 #define FQ_FILTER_BATCH 1  // passFilter's trimmed / direct ranges: row chunks loaded four at a time
 #endif
+#ifndef FQ_STATS_AHEAD
+#define FQ_STATS_AHEAD 2  // removed-mode Stats: quality chunks requested this many chunks ahead
+#endif
 #ifndef FQ_PREFETCH
 #define FQ_PREFETCH 0  // profiling: after staging, pull the first FQ_PREFETCH chunks of the wave's next tile
                        // toward L2 with LDS-DMA loads (0: off; measured slower at 10)
@@ -1280,10 +1283,11 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 rwb[t] = blk0 + 8u * (uint32_t)((t + r) & 15);
                 asm volatile("" : "+v"(rwb[t]));  // kept whole (not re-split into base + offset per use)
             }
-            // quality chunks rotate through three registers (requested two chunks ahead)
-            uint4 qb[3];
-            qb[0] = qchunk(0);
-            qb[1] = qchunk(min(1, nchunks - 1));
+            // quality chunks rotate through kSA + 1 registers (requested kSA chunks ahead)
+            constexpr int kSA = FQ_STATS_AHEAD;
+            uint4 qb[kSA + 1];
+#pragma unroll
+            for (int i = 0; i < kSA; ++i) qb[i] = qchunk(min(i, nchunks - 1));
             Fwd fn = fwd_chunk_in(col, lane_x, 0, rc);
             // nibble prefix masks from one 64-bit shift: ~(~0 << 4 * clamp(len, 0, 16)), the
             // 64th bit never needed (nibble 15's top bit is 0 in 0x4444... and 0xAAAA... masks)
@@ -1292,8 +1296,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             for (int F = 0; F < kChunks; ++F) {
                 if (F < nch) {  // wave-uniform; positions >= L are dummies
                     const Fwd f = fn;
-                    const uint32_t q0 = qb[F % 3].x, q1 = qb[F % 3].y, q2 = qb[F % 3].z, q3 = qb[F % 3].w;
-                    if (F + 2 < kChunks) qb[(F + 2) % 3] = qchunk(min(F + 2, nchunks - 1));
+                    const uint32_t q0 = qb[F % (kSA + 1)].x, q1 = qb[F % (kSA + 1)].y, q2 = qb[F % (kSA + 1)].z,
+                                   q3 = qb[F % (kSA + 1)].w;
+                    if (F + kSA < kChunks) qb[(F + kSA) % (kSA + 1)] = qchunk(min(F + kSA, nchunks - 1));
                     if (F + 1 < kChunks) fn = fwd_chunk_in(col, lane_x, min(F + 1, nchunks - 1), rc);
                     const int vl = L - 16 * F;
                     // slot 4 * kept + code; an N (code 3) reads as a G here
