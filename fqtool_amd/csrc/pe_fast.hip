@@ -1363,15 +1363,20 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 }
             }
         }
-        if (MERGE && removed_mode && valid && !(abl & 4) && merged && mate && post_on) {
+        // read 2's merged-part start, known to both lanes of the pair (all lanes swap)
+        const int ws2 = MERGE ? (mate ? ws : xor32(ws)) : 0;
+        if (MERGE && removed_mode && valid && !(abl & 4) && merged && post_on) {
             // Read 2's part of the merged read, rc(r2)[ol, ol + m2) at merged cycles m1 .. m1+m2-1
             // (OverlapAnalysis::merge src/overlapanalysis.cpp:74-104, then Stats::statRead of the
             // merged read, src/peprocessor.cpp:361): read 2's column holds the reverse complement,
             // so merged position j is column index 159 - pos_hi + j (codes already complemented);
             // its quality is read 2's byte at forward position pos_hi - j.  Cells: cycle rows of
-            // the extra block, count << 40 | sum(q); N bases are counted as G and moved.
+            // the extra block, count << 40 | sum(q); N bases are counted as G and moved.  Both
+            // lanes of the pair share the part (m1, m2 are pair-uniform): 16-position group J goes
+            // to the lane of mate J % 2, so no lane of a merged pair idles here.
             const uint32_t xb = (uint32_t)(LY::kColsW + LY::kMrgOff) * 4u;
-            const int pos_hi = ws + wn - 1;
+            const int c2 = lane_x | 32;  // read 2's column
+            const int pos_hi = ws2 + m2 - 1;
             const int ci0 = kMaxLen - 1 - pos_hi;
             uint32_t rb[16];
 #pragma unroll
@@ -1380,21 +1385,23 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 rb[t] = xb + (uint32_t)((((c >> 4) * kSlots) * 32 + 2 * (c & 15)) * 4);
             }
             // quality dwords of forward positions [hi - 15, hi], hi = pos_hi - 16J: words
-            // wl0 - 4J .. wl0 - 4J + 4; the next group's four new words are requested one group ahead
+            // wl0 - 4J .. wl0 - 4J + 4; the lane's next group (J + 2) is requested one group ahead
             const int wl0 = (pos_hi - 15) >> 2, sh = (pos_hi - 15) & 3;  // (negative only for dummies)
+            const uint8_t* Q2 = b.qual2 + roff;
+            const uint32_t* qrow2 = qrows + c2 * kQS;
             auto qword = [&](int wi) -> uint32_t {
-                if constexpr (LY::kQLds) return qrow[min(max(wi, 0), kQS - 1)];
-                else return RowQual{Q, b.stride >> 2}.word(max(wi, 0));
+                if constexpr (LY::kQLds) return qrow2[min(max(wi, 0), kQS - 1)];
+                else return RowQual{Q2, b.stride >> 2}.word(max(wi, 0));
             };
             uint32_t qw5[5];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) qw5[i] = qword(wl0 + i);
-            for (int J = 0; 16 * J < wn; ++J) {
-                const uint32_t cw = field_window(col, kFC, lane_x, ci0 + 16 * J);
-                const uint32_t nw = field_window(col, kFN, lane_x, ci0 + 16 * J);
-                uint32_t qn[4];
+            for (int i = 0; i < 5; ++i) qw5[i] = qword(wl0 - 4 * mate + i);
+            for (int J = mate; 16 * J < m2; J += 2) {
+                const uint32_t cw = field_window(col, kFC, c2, ci0 + 16 * J);
+                const uint32_t nw = field_window(col, kFN, c2, ci0 + 16 * J);
+                uint32_t qn[5];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) qn[i] = qword(wl0 - 4 * (J + 1) + i);
+                for (int i = 0; i < 5; ++i) qn[i] = qword(wl0 - 4 * (J + 2) + i);
                 // qualities ascending in qa[0..3], then reversed: qrev[k] byte b = merged t = 4k + b
                 uint32_t qa[4], qrev[4];
 #pragma unroll
@@ -1402,7 +1409,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
 #pragma unroll
                 for (int i = 0; i < 4; ++i) qrev[i] = __builtin_amdgcn_perm(0u, qa[3 - i], 0x00010203u);
                 // slot nibbles: code, or the dummy slot beyond the part
-                const int rem = wn - 16 * J;
+                const int rem = m2 - 16 * J;
                 const unsigned long long dm = ~0ull << min(4 * max(rem, 0), 63);
                 uint32_t nlo = spread2to4(cw), nhi = spread2to4(cw >> 16);
                 const uint32_t dlo = (uint32_t)dm, dhi = rem >= 16 ? 0u : (uint32_t)(dm >> 32);
@@ -1429,9 +1436,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                     __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + 3u * 128u)), 0ull - v,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                qw5[4] = qw5[0];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) qw5[i] = qn[i];
+                for (int i = 0; i < 5; ++i) qw5[i] = qn[i];
             }
         }
         if (valid && !(abl & 4) && !removed_mode) {
