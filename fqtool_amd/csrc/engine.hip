@@ -238,8 +238,8 @@ static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStr
     }
     // per-pair flags (index filter) run on the general kernel
     if (e->fast && !db.flags) {
-        const size_t ntiles = ((size_t)db.n + 31) / 32 + 1;  // single-end 64-read tiles enter as two
-        int rc = ensure_scratch(e, sc, ntiles, sync_device_on_grow);
+        const size_t nitems = (size_t)db.n + 1;  // hand-off list: one pair / read index per item
+        int rc = ensure_scratch(e, sc, nitems, sync_device_on_grow);
         if (rc != FQ_OK) return rc;
         HIP_TRY(e, hipMemsetAsync(sc.slow_count, 0, sizeof(int), s));
         if (timed) HIP_TRY(e, hipEventRecord(e->ev0, s));

@@ -7,12 +7,13 @@
 
 size_t fq_pack_kernel_lds_bytes(const fq_params& p);
 hipError_t fq_pack_kernel_set_lds(const fq_params& p);
-// General kernel (any bytes, any length <= max_cycles, merge): all pairs, or only the 32-pair
-// tiles listed in tiles[0 .. *ntiles) when tiles != nullptr.
+// General kernel (any bytes, any length <= max_cycles, merge): all pairs, or only the pairs
+// (single-end: reads) whose indices are listed in tiles[0 .. *ntiles) when tiles != nullptr.
 hipError_t fq_launch_pack_kernel(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
                                  int* err, int grid, hipStream_t stream, const int* tiles = nullptr,
                                  const int* ntiles = nullptr);
-// Fast paired-end kernel (pe_fast.hip); tiles it cannot take are appended to slow_tiles.
+// Fast kernels (pe_fast.hip); the indices of pairs / reads they cannot take are appended to
+// slow_tiles (room for one per pair / read).
 bool fq_pe_fast_supported(const fq_params& p);
 hipError_t fq_pe_fast_prepare();
 hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,

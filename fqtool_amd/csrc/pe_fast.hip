@@ -733,8 +733,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         const int r = lane_x & 15;  // stats rotation within a chunk
         uint32_t* qrow = qrows + lane_x * kQS;
         const int idx = PAIRED ? t * 32 + pl : t * 64 + lane_x;
-        const bool valid = idx < b.n;
-        const int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
+        bool valid = idx < b.n;  // (both cleared below for a pair handed to the general kernel)
+        int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
 
         // ---------------- staging ----------------
 #if FQ_STAGE_PRIO
@@ -861,17 +861,24 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             wp[kFN * 64] = 0u;
             wp += wstep;
         }
+        // Pairs (single-end: reads) this kernel cannot take -- a read longer than the columns or
+        // max_cycles, a byte outside ACGTN, a quality >= 128 -- are handed to the general kernel
+        // one by one (item list: pair / read indices); the rest of the tile stays here, the
+        // handed-over lanes continuing as empty lanes (valid false, length 0).
         if (__any(bad)) {
-            if (lane == 0) {  // the general kernel takes 32-read (single-end) / 32-pair tiles
-                if (PAIRED) {
-                    slow_tiles[atomicAdd(slow_count, 1)] = t;
-                } else {
-                    const int k = atomicAdd(slow_count, 2);
-                    slow_tiles[k] = 2 * t;
-                    slow_tiles[k + 1] = 2 * t + 1;
-                }
+            // bit i of hm: pair (single-end: read) i of the tile goes over
+            const unsigned long long bm = __ballot(bad);
+            const unsigned long long hm = PAIRED ? ((bm | (bm >> 32)) & 0xFFFFFFFFull) : bm;
+            const int me = PAIRED ? pl : lane_x;
+            const bool pbad = (hm >> me) & 1ull;
+            int base = 0;
+            if (lane == 0) base = atomicAdd(slow_count, (int)__popcll(hm));
+            base = __shfl(base, 0);
+            if (pbad && mate == 0) slow_tiles[base + (int)__popcll(hm & ((1ull << me) - 1ull))] = idx;
+            if (pbad) {
+                valid = false;
+                L = 0;
             }
-            continue;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

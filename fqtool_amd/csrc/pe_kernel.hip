@@ -223,10 +223,11 @@ __global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, f
     __syncthreads();
 
     const int skew = threadIdx.x & 63;
-    // all pairs of the pack, or (tile-list mode) the 32-pair tiles the fast kernel handed over
-    const int total = tiles ? *ntiles * 32 : b.n;
+    // all pairs of the pack, or (item-list mode) the pairs / single-end reads the fast kernel
+    // handed over, one index each
+    const int total = tiles ? *ntiles : b.n;
     for (int item = blockIdx.x * blockDim.x + threadIdx.x; item < total; item += gridDim.x * blockDim.x) {
-        const int idx = tiles ? tiles[item >> 5] * 32 + (item & 31) : item;
+        const int idx = tiles ? tiles[item] : item;
         if (idx >= b.n) continue;
         const Row s1 = batch_row(b.seq1, b.stride, idx);
         const Row q1 = batch_row(b.qual1, b.stride, idx);

@@ -323,8 +323,9 @@ int fq_engine_process(fq_engine* e, const fq_batch* host_batch, fq_read_result* 
 /* Device-resident pack (inputs already in HBM): enqueues the kernels on `stream`
  * (a hipStream_t; NULL = the HIP default stream) and returns without synchronising.
  * `device_results` may be NULL when the caller needs only the accumulators.
- * The engine's hand-off tile list is shared by these calls: use one stream at a time per
- * engine (concurrent streams need one engine each). */
+ * The engine's hand-off list (pairs / reads the fast kernels pass to the general kernel) is
+ * shared by these calls: use one stream at a time per engine (concurrent streams need one
+ * engine each). */
 int fq_engine_process_device(fq_engine* e, const fq_batch* device_batch,
                              fq_read_result* device_results, void* stream);
 

@@ -21,8 +21,8 @@ def eng_lib():
 
 @pytest.fixture(params=["fast", "general"])
 def mode(request, monkeypatch):
-    """Run each parity case through the default dispatch (gfx950 fast kernels, falling back per
-    tile) and through the general kernel only."""
+    """Run each parity case through the default dispatch (gfx950 fast kernels, handing single
+    pairs / reads to the general kernel) and through the general kernel only."""
     monkeypatch.setenv("FQ_ENGINE_GENERAL_ONLY", "1" if request.param == "general" else "0")
     return request.param
 
@@ -95,7 +95,7 @@ def test_edge_case_parity(eng_lib, oracle, name, mode):
 @pytest.mark.parametrize("name", ["C3", "C3b", "C4", "C5", "PE_all", "C2", "SE_all"])
 def test_mixed_fast_and_handoff_tiles(eng_lib, oracle, name):
     """Mostly clean synthetic tiles plus scattered tiles with IUPAC bases, quality bytes >= 128
-    and over-long reads: the fast kernel hands those tiles to the general kernel."""
+    and over-long reads: the fast kernel hands those pairs to the general kernel."""
     p = config(name, max_cycles=512)
     paired = bool(p.paired)
     n = 8001 if paired else 8033  # a ragged last tile
@@ -112,6 +112,43 @@ def test_mixed_fast_and_handoff_tiles(eng_lib, oracle, name):
             m2[0][i, 150:170] = ord("A")
             m2[1][i, 150:170] = ord("I")
             m2[2][i] = 170
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+@pytest.mark.parametrize("stride", [160, 336])
+@pytest.mark.parametrize("name", ["C3", "C4", "C5", "PE_all", "C2", "SE_all"])
+def test_dense_per_pair_handoff(eng_lib, oracle, name, stride):
+    """The fast kernels hand over single pairs (single-end: reads), not whole tiles: ~12 % of the
+    pairs hold a lowercase base, an IUPAC code, a quality byte >= 128 or an over-long read in
+    either mate or both, one whole tile goes over, and the last tile is ragged.  The pairs kept on
+    the fast path share their tiles (and LDS statistics) with the handed-over ones.  Stride 160
+    runs the 160-position build, stride 336 the 320-position build (reads of 330 bases go over)."""
+    p = config(name, max_cycles=512)
+    paired = bool(p.paired)
+    n = 12_345
+    pk = synth_pack(oracle, n, paired, first=97, stride=stride)
+    rng = np.random.default_rng(29)
+    mates = [(pk.seq1, pk.qual1, pk.len1)] + ([(pk.seq2, pk.qual2, pk.len2)] if paired else [])
+    picks = rng.choice(n, n // 8, replace=False)
+    picks = np.concatenate([picks, np.arange(64 * 3, 64 * 4)])  # one whole tile (both layouts)
+    for k, i in enumerate(picks):
+        which = [mates[k % len(mates)]] if k % 5 else mates  # every fifth: both mates
+        for s, q, ln in which:
+            kind = (k // 2) % 4
+            if kind == 0:
+                s[i, rng.integers(0, 150)] = ord("a") + 2 * (k % 3)  # a, c, e
+            elif kind == 1:
+                s[i, rng.integers(0, 150)] = ord("Y")
+            elif kind == 2:
+                q[i, rng.integers(0, 150)] = 129 + k % 100
+            elif stride == 160:
+                s[i, rng.integers(0, 150)] = ord("n")
+            else:
+                s[i, 150:330] = ord("G")
+                q[i, 150:330] = ord("F")
+                ln[i] = 330
     res_o, acc_o = run_oracle(oracle, p, pk)
     res_e, acc_e = run_engine(eng_lib, p, pk)
     assert_same(p, res_o, acc_o, res_e, acc_e)

@@ -16,6 +16,11 @@ b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
 b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
 assert lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 0, 150, None) == 0
 res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+ev = int(os.environ.get("EXOTIC_EVERY", 0))
+if ev:  # every ev-th pair gets a lowercase base in read 1 (position 5): a hand-off to the general kernel
+    i = torch.arange(0, n, ev, device=dev, dtype=torch.int64)
+    off = (i // 32) * 32 * stride + (i % 32) * 16 + 5
+    bufs[0][off] = ord("a")
 torch.cuda.synchronize()
 tag = os.environ.get("TAG", "")
 for cfg in os.environ.get("CONFIGS", "C3").split():
