@@ -647,7 +647,103 @@ __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) &
 // PAIRED: a tile is 32 pairs, lanes l and l+32 holding the two mates of a pair (read 2's column
 // reverse-complemented for the overlap scan); single-end: a tile is 64 reads, one per lane, with
 // SingleEndProcessor::processSingleEnd's order (src/seprocessor.cpp:290-360).
-template <bool LEAN, bool PAIRED, bool MERGE>
+// BaseCorrector::correctByOverlapAnalysis (src/basecorrector.cpp:14-70) for one pair with
+// 0 < diff <= 5, run by both lanes of the pair (the decisions are pair-uniform; each lane applies
+// its own read's corrections).  A mismatch of the overlap (as OverlapAnalysis counts it: N == N,
+// N != base) where one side is >= Q30 and the other <= Q14 takes the good side's base
+// (complemented) and quality.  Each correction is applied where the later steps read the read: the
+// lane's code column (read 2's column holds the reverse complement, so the new code is the other
+// column's code as stored), its quality row in HBM (rewritten in place, as the general kernel
+// does), and the whole-read sums that passFilter and the post statistics derive their window sums
+// from.  The pre-trimming statistics must see the original read (src/peprocessor.cpp:276-277):
+// the removed-mode Stats pass counts the corrected base, so the removed block gets
+// (original - corrected) at the base's cycle (pre = kept + removed), and the per-read pre Q20/Q30
+// scalar gets the negated deltas.  Host side: the FASTQ text is corrected from the read-2 record's
+// (offset, overlap length, window length), flags FQ_RF_CORRECTED.
+__device__ inline void correct_pair_fast(const fq_params& p, uint32_t* col, uint32_t* lds, const fq_batch& b, size_t roff,
+                                         int mate, int lane_x, int mlane, int st1, int st2, int n2, const Overlap& ov,
+                                         const uint8_t* Q, fq_read_result& rr, uint32_t& q20, uint32_t& q30,
+                                         uint32_t& lowf, uint32_t& tqf, uint32_t& nbf, uint32_t limq,
+                                         unsigned long long* pre_q, int rem_block, unsigned long long* acc) {
+    const int ol = ov.len;
+    const int start1 = max(0, ov.offset), start2 = n2 - max(0, -ov.offset) - 1;
+    const int a0 = st1 + start1;                  // read 1's forward position at overlap index 0
+    const int b0 = kMaxLen - 1 - (st2 + start2);  // read 2's column (reverse complement) index at 0
+    const int c1 = mate ? mlane : lane_x, c2 = mate ? lane_x : mlane;
+    const RowQual Q1{b.qual1 + roff, b.stride >> 2}, Q2{b.qual2 + roff, b.stride >> 2};
+    uint8_t* myq = const_cast<uint8_t*>(Q);
+    const int good = 33 + 30, bad = 33 + 14;  // util::num2qual(30), util::num2qual(14)
+    int corrected = 0;
+    bool cr1 = false, cr2 = false;
+    int d20 = 0, d30 = 0;
+    // the whole-read sums' per-byte terms (staging's SWAR tests on one byte)
+    auto f20 = [](uint32_t q) { return (int)(((q + 0x4Au) >> 7) & 1u); };
+    auto f30 = [](uint32_t q) { return (int)(((q + 0x40u) >> 7) & 1u); };
+    auto flow = [&](uint32_t q) { return (int)((~(q + (limq & 0xFFu)) >> 7) & 1u); };
+    for (int j = 0; 16 * j < ol; ++j) {
+        const uint32_t a = field_window(col, kFC, c1, a0 + 16 * j), wa = field_window(col, kFN, c1, a0 + 16 * j);
+        const uint32_t bb = field_window(col, kFC, c2, b0 + 16 * j), wb = field_window(col, kFN, c2, b0 + 16 * j);
+        uint32_t mism = ((fold2(a ^ bb) & ~(wa | wb)) | (wa ^ wb)) & posmask(ol - 16 * j);
+        while (mism) {
+            const int t = (__ffs(mism) - 1) >> 1;
+            mism &= mism - 1u;
+            const int i = 16 * j + t;
+            const int p1 = a0 + i, p2 = st2 + start2 - i;
+            const uint32_t x1 = (uint32_t)Q1(p1), x2 = (uint32_t)Q2(p2);
+            // read 1's forward code / N flag; read 2's column code (its complement) / N flag
+            const uint32_t k1 = (a >> (2 * t)) & 3u, n1 = (wa >> (2 * t)) & 1u;
+            const uint32_t k2 = (bb >> (2 * t)) & 3u, nb2 = (wb >> (2 * t)) & 1u;
+            int side;  // the read that takes the other's base: 1, 2, or 0 (none)
+            if ((int)x1 >= good && (int)x2 <= bad) side = 2;
+            else if ((int)x2 >= good && (int)x1 <= bad) side = 1;
+            else continue;
+            ++corrected;
+            if (side == 1) cr1 = true;
+            else cr2 = true;
+            if (side != mate + 1) continue;
+            // this lane's read: forward position P, column index ci, new column code / N flag
+            const int P = mate ? p2 : p1, ci = mate ? b0 + i : p1;
+            const uint32_t ncode = mate ? k1 : k2, nN = mate ? n1 : nb2;
+            const uint32_t ocode = mate ? k2 : k1, oN = mate ? nb2 : n1;
+            const uint32_t xo = mate ? x2 : x1, xn = mate ? x1 : x2;
+            const int w = ci >> 4, sh = 2 * (ci & 15);
+            uint32_t& cw = col[(kFC + w) * 64 + lane_x];
+            uint32_t& nw = col[(kFN + w) * 64 + lane_x];
+            cw = (cw & ~(3u << sh)) | (ncode << sh);
+            nw = (nw & ~(1u << sh)) | (nN << sh);
+            myq[(P >> 4) * (FQ_TILE_READS * FQ_CHUNK) + (P & 15)] = (uint8_t)xn;
+            const int e20 = f20(xn) - f20(xo), e30 = f30(xn) - f30(xo);
+            d20 += e20;
+            d30 += e30;
+            q20 += (uint32_t)e20;
+            q30 += (uint32_t)e30;
+            lowf += (uint32_t)(flow(xn) - flow(xo));
+            tqf += xn - xo;
+            nbf += nN - oN;
+            // forward codes (read 2's column holds complements; N stays code 3) -> removed slots
+            const uint32_t fo = mate && !oN ? ocode ^ 2u : ocode, fn = mate && !nN ? ncode ^ 2u : ncode;
+            const int so = oN ? kRNSlot : (int)fo, sn = nN ? kRNSlot : (int)fn;
+            atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + rcell(P, so)), kCount1 | (unsigned long long)xo);
+            atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + rcell(P, sn)), 0ull - (kCount1 | (unsigned long long)xn));
+        }
+    }
+    if (!corrected) return;
+    if (d20 | d30) atomicAdd(pre_q, 0ull - (unsigned long long)((long long)d20 * 4294967296LL + (long long)d30));
+    if (mate ? cr2 : cr1) rr.flags |= FQ_RF_CORRECTED;
+    if (mate) {  // what the host needs to correct the text (as fq_pack_kernel's correct_pair)
+        rr.m_len1 = (uint16_t)(int16_t)ov.offset;
+        rr.m_len2 = (uint16_t)ol;
+        rr.reserved = (uint16_t)n2;
+    } else {
+        unsigned long long* tail = acc + acc_stats_offset(p.insert_size_max, p.max_cycles, 4);
+        atomicAdd(&tail[FQ_ACC_TAIL_CORRECTED_READS], (cr1 && cr2) ? 2ull : 1ull);
+        atomicAdd(&tail[FQ_ACC_TAIL_CORRECTED_BASES], (unsigned long long)corrected);
+    }
+}
+
+// CORR: the -c instantiation of the full paired-end variant (kept apart so the other variants'
+// register allocation does not carry the correction code)
+template <bool LEAN, bool PAIRED, bool MERGE, bool CORR = false>
 __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
@@ -1057,6 +1153,16 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 if (ov.overlapped) isize = ov.offset > 0 ? n1 + n2 - ov.len : ov.len;
                 if (isize > p.insert_size_max) isize = p.insert_size_max;
                 atomicAdd(&ins[isize], 1u);
+            }
+            if constexpr (CORR) {
+                // BaseCorrector::correctByOverlapAnalysis (src/basecorrector.cpp:14-70), pair-uniform
+                if (ov.diff > 0 && ov.diff <= 5) {
+                    const int st_o = xor32(st);
+                    correct_pair_fast(p, col, lds, b, roff, mate, lane_x, mlane, mate ? st_o : st, mate ? st : st_o, n2,
+                                      ov, Q, rr, q20, q30, lowf, tqf, nbf, limq,
+                                      scal + kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 1,
+                                      LY::kColsW + mate * (kRSlots * 32 * kChunks), acc);
+                }
             }
             if (p.adapter_trimming) {
                 const int ol = ov.len;  // AdapterTrimmer::trimByOverlapAnalysis, src/adaptertrimmer.cpp:14-27
@@ -1630,8 +1736,11 @@ using namespace long320;
 
 #if FQ_MAXLEN == 160
 bool fq_pe_fast_supported(const fq_params& p) {
-    // -c and UMI trims run on the general kernel (fq_pack_kernel)
-    return p.insert_size_max <= 512 && p.insert_size_max >= 0 && !p.correction_enabled && p.umi_front1 == 0 &&
+    // UMI trims (and -c with -m or front trimming) run on the general kernel (fq_pack_kernel)
+    // -c: paired, no merge, no front trimming (its Stats fix-up is the removed-mode block's)
+    const bool corr_ok = !p.correction_enabled || (p.paired && !p.merge_enabled && p.trim_front1 == 0 &&
+                                                   p.trim_front2 == 0 && !p.cut_front);
+    return p.insert_size_max <= 512 && p.insert_size_max >= 0 && corr_ok && p.umi_front1 == 0 &&
            p.umi_front2 == 0 && (!p.merge_enabled || (p.paired && !p.complexity_enabled));
 }
 
@@ -1669,6 +1778,11 @@ hipError_t FQ_PREPARE() {
         hipError_t e = hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, words * 4);
         if (e != hipSuccess) return e;
     }
+    {  // the -c instantiation of the full paired-end variant
+        hipError_t e = hipFuncSetAttribute((const void*)pe_fast_kernel<false, true, false, true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, Layout<false>::kLdsW * 4);
+        if (e != hipSuccess) return e;
+    }
 #if FQ_MAXLEN == 160
     return fq_pe_fast_long_prepare();
 #else
@@ -1686,7 +1800,8 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
     const bool lean = p.trim_front1 == 0 && p.trim_tail1 == 0 && p.trim_front2 == 0 && p.trim_tail2 == 0 &&
                       !(p.avg_qual_limit > 0) &&
                       !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
-                      p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled;
+                      p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled &&
+                      !p.correction_enabled;
     using LL = Layout<true>;
     using LF = Layout<false>;
     const dim3 gl(grid * LL::kBlocksPerCU), gf(grid * LF::kBlocksPerCU);
@@ -1700,6 +1815,9 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
     if (p.paired && lean)
         // (fq_params.reserved[2]: extra LDS bytes per workgroup, profiling only -- lowers occupancy)
         hipLaunchKernelGGL((pe_fast_kernel<true, true, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4 + p.reserved[2], stream, p, b,
+                           res, acc, slow_tiles, slow_count);
+    else if (p.paired && p.correction_enabled)
+        hipLaunchKernelGGL((pe_fast_kernel<false, true, false, true>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
                            res, acc, slow_tiles, slow_count);
     else if (p.paired)
         hipLaunchKernelGGL((pe_fast_kernel<false, true, false>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,

@@ -219,6 +219,11 @@ def config(name, max_cycles=256):
         p.correction_enabled = 1
         p.merge_enabled = 1
         p.cut_right = 1
+    elif name == "PE_correct_x":  # -c with the config-5 options (the fast kernels' -c variant)
+        p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
+        abi.set_adapter(p, 1, AD1)
+        p.cut_right = 1
+        p.correction_enabled = 1
     elif name == "PE_umi":  # UMI in both reads (trimFront after the pre-filter stats)
         p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
         p.cut_front = 1
@@ -248,7 +253,7 @@ def config(name, max_cycles=256):
 
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
                "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR2", "PE_cutR5", "PE_cutRF", "PE_merge_q",
-               "PE_correct", "PE_correct_all", "PE_umi", "SE_umi"]
+               "PE_correct", "PE_correct_all", "PE_correct_x", "PE_umi", "SE_umi"]
 
 
 def run_oracle(oracle, p, pk):

@@ -40,7 +40,8 @@ def synth_device(lib, torch, n, paired, first):
 
 
 @pytest.mark.parametrize("name,n", [("C2", 20_000_017), ("C3", 20_000_017), ("C3", 100_000_000), ("C4", 20_000_017),
-                                    ("C5", 20_000_017), ("C3b", 4_000_005), ("PE_all", 4_000_005)])
+                                    ("C5", 20_000_017), ("C3b", 4_000_005), ("PE_all", 4_000_005),
+                                    ("PE_correct", 4_000_005), ("PE_correct_x", 4_000_005)])
 def test_fullsize_parity(eng_lib, oracle, name, n):
     import torch
 
@@ -48,8 +49,10 @@ def test_fullsize_parity(eng_lib, oracle, name, n):
     paired = bool(p.paired)
     t0 = time.time()
     planes, lens = synth_device(eng_lib, torch, n, paired, first=3 * 10**9)
-    eres, eacc = engine_run(eng_lib, torch, p, planes, lens, n, STRIDE, paired, 0)
+    # (inputs copied first: -c rewrites corrected bases and qualities in place, as the reference's
+    # BaseCorrector does to its Read objects)
     hp, l1, l2 = host_copy(torch, planes, lens, paired)
+    eres, eacc = engine_run(eng_lib, torch, p, planes, lens, n, STRIDE, paired, 0)
     got = eres.cpu().numpy().view(np.dtype(abi.RESULT_DTYPE_FIELDS))
     del planes, lens, eres
     torch.cuda.empty_cache()

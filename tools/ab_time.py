@@ -25,6 +25,7 @@ torch.cuda.synchronize()
 tag = os.environ.get("TAG", "")
 for cfg in os.environ.get("CONFIGS", "C3").split():
     p = bench.config_params(abi, cfg)
+    p.correction_enabled = int(os.environ.get("CORRECT", 0))  # -c on top of the config
     p.reserved[0] = int(os.environ.get("ABL", 0))  # ablation bits (pe_fast.hip; results invalid when set)
     if cfg == "C2":
         b.seq2 = b.qual2 = None
