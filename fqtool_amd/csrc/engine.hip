@@ -236,8 +236,8 @@ static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStr
         const int rc = fq_dup_pack(e->dup, db, e->p.paired, order, s);
         if (rc != FQ_OK) return fail(e, rc, std::string("duplication analysis: ") + fq_dup_error(e->dup));
     }
-    // per-pair flags (index filter) run on the general kernel
-    if (e->fast && !db.flags) {
+    // (index-filtered pairs are handed to the general kernel one by one)
+    if (e->fast) {
         const size_t nitems = (size_t)db.n + 1;  // hand-off list: one pair / read index per item
         int rc = ensure_scratch(e, sc, nitems, sync_device_on_grow);
         if (rc != FQ_OK) return rc;

@@ -741,9 +741,9 @@ __device__ inline void correct_pair_fast(const fq_params& p, uint32_t* col, uint
     }
 }
 
-// CORR: the -c instantiation of the full paired-end variant (kept apart so the other variants'
-// register allocation does not carry the correction code)
-template <bool LEAN, bool PAIRED, bool MERGE, bool CORR = false>
+// XTRA: the -c / UMI instantiation of the full variants (kept apart so the other variants'
+// register allocation does not carry that code)
+template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA = false>
 __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
@@ -782,12 +782,16 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
     const bool lowr_ok = p.cut_right && 33 + p.cut_right_quality >= 1 && 33 + p.cut_right_quality <= 127;
     const uint32_t limr = lowr_ok ? (uint32_t)(0x80 - (33 + p.cut_right_quality)) * 0x01010101u : 0u;
     // cut_right as the only window option, window <= 4: cut_right_w4
-    const bool cut_w4 = FQ_CUT_W4 && lowr_ok && !p.cut_front && !p.cut_tail && p.cut_right_window >= 1 && p.cut_right_window <= 4;
+    // UMI in the reads (src/umiprocessor.cpp:10-89, trimFront before trimAndCut): trimAndCut runs on
+    // the read from umi_cut(umi_front, len) on (the general path of trim_and_cut_t)
+    const bool umi = XTRA && (p.umi_front1 > 0 || p.umi_front2 > 0);
+    const bool cut_w4 = FQ_CUT_W4 && lowr_ok && !umi && !p.cut_front && !p.cut_tail && p.cut_right_window >= 1 &&
+                        p.cut_right_window <= 4;
     // Without front trimming every kept window starts at 0, so each base lands in exactly one of
     // two disjoint blocks: "kept" (inside a passing read's window; the post block) or "removed"
     // (trimmed tails, failed pairs; the pre block), one LDS atomic per base.  At the flush
     // pre = kept + removed and post = kept.
-    const bool removed_mode = LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front);
+    const bool removed_mode = LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front && !umi);
     const int g_per = max(p.polyg_one_mismatch_per, 1);
     // (i+1)/per as ((i+1)*inv) >> 16, exact while per * (kMaxLen + 1) < 65536; else inv = 0: division
     const int g_inv = g_per * (kMaxLen + 1) < 65536 ? (65536 + g_per - 1) / g_per : 0;
@@ -951,16 +955,20 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 wp += wstep;
             }
         }
-        const bool bad = odd || exo != 0 || (qhi & 0x80808080u) != 0;
+        // (index filter: a pair the host dropped counts only in the pre-filter Stats,
+        // src/peprocessor.cpp:283-286 -- rare, so it goes over too)
+        const bool bad = odd || exo != 0 || (qhi & 0x80808080u) != 0 ||
+                         (b.flags && valid && (b.flags[idx] & FQ_BF_INDEX_FILTERED));
         for (int k = nch; k < kChunks; ++k) {  // unused tail of the row
             wp[kFC * 64] = 0u;
             wp[kFN * 64] = 0u;
             wp += wstep;
         }
         // Pairs (single-end: reads) this kernel cannot take -- a read longer than the columns or
-        // max_cycles, a byte outside ACGTN, a quality >= 128 -- are handed to the general kernel
-        // one by one (item list: pair / read indices); the rest of the tile stays here, the
-        // handed-over lanes continuing as empty lanes (valid false, length 0).
+        // max_cycles, a byte outside ACGTN, a quality >= 128, an index-filtered pair -- are
+        // handed to the general kernel one by one (item list: pair / read indices); the rest of
+        // the tile stays here, the handed-over lanes continuing as empty lanes (valid false,
+        // length 0).
         if (__any(bad)) {
             // bit i of hm: pair (single-end: read) i of the tile goes over
             const unsigned long long bm = __ballot(bad);
@@ -1031,7 +1039,17 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         } else {
             if constexpr (LY::kQLds)
                 nn = valid && trim_and_cut_t(p, seq, qual, L, front, tail, st, n, lowr_ok ? lowr : ~0u);
-            else
+            else if (XTRA && umi) {
+                // UmiProcessor::process cuts min(umi_front, len - 1) bases (a read of length 0 keeps
+                // them), src/peprocessor.cpp:288-290 / src/seprocessor.cpp:309-311
+                const int uf = mate ? p.umi_front2 : p.umi_front1;
+                const int u = (uf > 0 && L > 0) ? min(uf, L - 1) : 0;
+                // (cut_right's low-chunk hint in the cut read's chunks: chunk c spans row chunks
+                // c + u/16 and c + (u+15)/16, so the union of their bits is a safe superset)
+                const uint32_t lowu = lowr_ok ? ((lowr >> (u >> 4)) | (lowr >> ((u + 15) >> 4))) : ~0u;
+                nn = valid && trim_and_cut_t(p, at(seq, u), at(RowQual{Q, b.stride >> 2}, u), L - u, front, tail, st, n, lowu);
+                st += u;
+            } else
                 nn = valid && ((abl & 1024) ? (n = L, true)
                                : cut_w4 ? cut_right_w4(p, Q, nchunks, L, front, tail, lowr, limr, st, n)
                                         : trim_and_cut_t(p, seq, RowQual{Q, b.stride >> 2}, L, front, tail, st, n, lowr_ok ? lowr : ~0u));
@@ -1154,9 +1172,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 if (isize > p.insert_size_max) isize = p.insert_size_max;
                 atomicAdd(&ins[isize], 1u);
             }
-            if constexpr (CORR) {
+            if constexpr (XTRA) {
                 // BaseCorrector::correctByOverlapAnalysis (src/basecorrector.cpp:14-70), pair-uniform
-                if (ov.diff > 0 && ov.diff <= 5) {
+                if (p.correction_enabled && ov.diff > 0 && ov.diff <= 5) {
                     const int st_o = xor32(st);
                     correct_pair_fast(p, col, lds, b, roff, mate, lane_x, mlane, mate ? st_o : st, mate ? st : st_o, n2,
                                       ov, Q, rr, q20, q30, lowf, tqf, nbf, limq,
@@ -1736,12 +1754,15 @@ using namespace long320;
 
 #if FQ_MAXLEN == 160
 bool fq_pe_fast_supported(const fq_params& p) {
-    // UMI trims (and -c with -m or front trimming) run on the general kernel (fq_pack_kernel)
+    // -c with -m, front trimming or UMI, and UMI with -m run on the general kernel (fq_pack_kernel)
     // -c: paired, no merge, no front trimming (its Stats fix-up is the removed-mode block's)
     const bool corr_ok = !p.correction_enabled || (p.paired && !p.merge_enabled && p.trim_front1 == 0 &&
-                                                   p.trim_front2 == 0 && !p.cut_front);
-    return p.insert_size_max <= 512 && p.insert_size_max >= 0 && corr_ok && p.umi_front1 == 0 &&
-           p.umi_front2 == 0 && (!p.merge_enabled || (p.paired && !p.complexity_enabled));
+                                                   p.trim_front2 == 0 && !p.cut_front && p.umi_front1 <= 0 &&
+                                                   p.umi_front2 <= 0);
+    // UMI trims with -m stay on the general kernel (the merge variant assumes reads from 0)
+    const bool umi_ok = (p.umi_front1 <= 0 && p.umi_front2 <= 0) || !p.merge_enabled;
+    return p.insert_size_max <= 512 && p.insert_size_max >= 0 && corr_ok && umi_ok &&
+           (!p.merge_enabled || (p.paired && !p.complexity_enabled));
 }
 
 // profiling aid (tools/ablate.py --phases): read and clear the per-phase cycle totals
@@ -1778,9 +1799,9 @@ hipError_t FQ_PREPARE() {
         hipError_t e = hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, words * 4);
         if (e != hipSuccess) return e;
     }
-    {  // the -c instantiation of the full paired-end variant
-        hipError_t e = hipFuncSetAttribute((const void*)pe_fast_kernel<false, true, false, true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, Layout<false>::kLdsW * 4);
+    // the -c / UMI instantiations of the full variants
+    for (const void* kx : {(const void*)pe_fast_kernel<false, true, false, true>, (const void*)pe_fast_kernel<false, false, false, true>}) {
+        hipError_t e = hipFuncSetAttribute(kx, hipFuncAttributeMaxDynamicSharedMemorySize, Layout<false>::kLdsW * 4);
         if (e != hipSuccess) return e;
     }
 #if FQ_MAXLEN == 160
@@ -1801,9 +1822,10 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
                       !(p.avg_qual_limit > 0) &&
                       !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
                       p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled &&
-                      !p.correction_enabled;
+                      !p.correction_enabled && p.umi_front1 <= 0 && p.umi_front2 <= 0;
     using LL = Layout<true>;
     using LF = Layout<false>;
+    const bool xtra = p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0;  // (lean is false then)
     const dim3 gl(grid * LL::kBlocksPerCU), gf(grid * LF::kBlocksPerCU);
 #if FQ_MAXLEN == 160
     using LM = Layout<false, true>;
@@ -1816,7 +1838,7 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
         // (fq_params.reserved[2]: extra LDS bytes per workgroup, profiling only -- lowers occupancy)
         hipLaunchKernelGGL((pe_fast_kernel<true, true, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4 + p.reserved[2], stream, p, b,
                            res, acc, slow_tiles, slow_count);
-    else if (p.paired && p.correction_enabled)
+    else if (p.paired && xtra)
         hipLaunchKernelGGL((pe_fast_kernel<false, true, false, true>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
                            res, acc, slow_tiles, slow_count);
     else if (p.paired)
@@ -1824,6 +1846,9 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
                            res, acc, slow_tiles, slow_count);
     else if (lean)
         hipLaunchKernelGGL((pe_fast_kernel<true, false, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4, stream, p, b,
+                           res, acc, slow_tiles, slow_count);
+    else if (xtra)
+        hipLaunchKernelGGL((pe_fast_kernel<false, false, false, true>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
                            res, acc, slow_tiles, slow_count);
     else
         hipLaunchKernelGGL((pe_fast_kernel<false, false, false>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,

@@ -228,6 +228,11 @@ def config(name, max_cycles=256):
         p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
         p.cut_front = 1
         p.umi_front1, p.umi_front2 = 10, 7
+    elif name == "PE_umi_x":  # UMI in both reads with the config-5 options (cut_right scan on the cut read)
+        p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
+        abi.set_adapter(p, 2, AD2)
+        p.cut_right = 1
+        p.umi_front1, p.umi_front2 = 8, 12
     elif name == "SE_umi":
         p.polyg_enabled = 1
         p.cut_tail = 1
@@ -253,7 +258,7 @@ def config(name, max_cycles=256):
 
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
                "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR2", "PE_cutR5", "PE_cutRF", "PE_merge_q",
-               "PE_correct", "PE_correct_all", "PE_correct_x", "PE_umi", "SE_umi"]
+               "PE_correct", "PE_correct_all", "PE_correct_x", "PE_umi", "PE_umi_x", "SE_umi"]
 
 
 def run_oracle(oracle, p, pk):

@@ -16,6 +16,11 @@ b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
 b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
 assert lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 0, 150, None) == 0
 res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+fe = int(os.environ.get("INDEX_EVERY", 0))
+if fe:  # every fe-th pair dropped by the host's index filter (fq_batch.flags)
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    flags[::fe] = abi.FQ_BF_INDEX_FILTERED
+    b.flags = flags.data_ptr()
 ev = int(os.environ.get("EXOTIC_EVERY", 0))
 if ev:  # every ev-th pair gets a lowercase base in read 1 (position 5): a hand-off to the general kernel
     i = torch.arange(0, n, ev, device=dev, dtype=torch.int64)
@@ -26,6 +31,7 @@ tag = os.environ.get("TAG", "")
 for cfg in os.environ.get("CONFIGS", "C3").split():
     p = bench.config_params(abi, cfg)
     p.correction_enabled = int(os.environ.get("CORRECT", 0))  # -c on top of the config
+    p.umi_front1 = p.umi_front2 = int(os.environ.get("UMI", 0))  # UMI cut from both reads
     p.reserved[0] = int(os.environ.get("ABL", 0))  # ablation bits (pe_fast.hip; results invalid when set)
     if cfg == "C2":
         b.seq2 = b.qual2 = None
