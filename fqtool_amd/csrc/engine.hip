@@ -244,7 +244,10 @@ static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStr
         HIP_TRY(e, hipMemsetAsync(sc.slow_count, 0, sizeof(int), s));
         if (timed) HIP_TRY(e, hipEventRecord(e->ev0, s));
         HIP_TRY(e, fq_launch_pe_fast(e->p, db, dres, e->acc, sc.slow_tiles, sc.slow_count, e->cus, s));
-        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, e->cus, s, sc.slow_tiles, sc.slow_count));
+        // (the hand-off list's length is known on the device only: as many workgroups as the
+        // batch could need, at the occupancy the kernel's LDS allows; empty ones exit at once)
+        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, grid_for(e, db.n), s, sc.slow_tiles,
+                                         sc.slow_count));
     } else {
         if (timed) HIP_TRY(e, hipEventRecord(e->ev0, s));
         HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, grid_for(e, db.n), s));
