@@ -741,7 +741,7 @@ __device__ inline void correct_pair_fast(const fq_params& p, uint32_t* col, uint
     }
 }
 
-// XTRA: the -c / UMI instantiation of the full variants (kept apart so the other variants'
+// XTRA: the -c / UMI / -e instantiation of the full variants (kept apart so the other variants'
 // register allocation does not carry that code)
 template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA = false>
 __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
@@ -927,7 +927,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                     q20 += __popc((qm + 0x4A4A4A4Au) & (0x80808080u & bm));  // q > '5'
                     q30 += __popc((qm + 0x40404040u) & (0x80808080u & bm));  // q > '?'
                     lowf += __popc(~(qm + limq) & (0x80808080u & bm));        // q < limit
-                    if (!LEAN) tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);    // (LEAN excludes -e)
+                    // whole-read quality total: only -e reads it (passFilter's mean quality),
+                    // which runs on the XTRA instantiation (and the merge variant)
+                    if (!LEAN && (XTRA || MERGE)) tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);
                     if (!LEAN) lr |= ~(qm + limr) & (0x80808080u & bm);         // q < cut_right threshold
                     cc |= (kk & 0x03030303u) << (2 * j);
                     nn4 |= ((kk >> 2) & 0x01010101u) << (2 * j);
@@ -1825,7 +1827,8 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
                       !p.correction_enabled && p.umi_front1 <= 0 && p.umi_front2 <= 0;
     using LL = Layout<true>;
     using LF = Layout<false>;
-    const bool xtra = p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0;  // (lean is false then)
+    // -c, UMI and -e (the whole-read quality total) run on the XTRA instantiations (lean is false then)
+    const bool xtra = p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0 || p.avg_qual_limit > 0;
     const dim3 gl(grid * LL::kBlocksPerCU), gf(grid * LF::kBlocksPerCU);
 #if FQ_MAXLEN == 160
     using LM = Layout<false, true>;
