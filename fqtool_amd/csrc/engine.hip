@@ -238,7 +238,9 @@ static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStr
     }
     // (index-filtered pairs are handed to the general kernel one by one)
     if (e->fast) {
-        const size_t nitems = (size_t)db.n + 1;  // hand-off list: one pair / read index per item
+        // hand-off list: pair / read indices, reserved a tile's worth (<= 64) at a time, at most
+        // one reservation per tile, so at most n + 64 slots (holes included)
+        const size_t nitems = (size_t)db.n + 64 + 1;
         int rc = ensure_scratch(e, sc, nitems, sync_device_on_grow);
         if (rc != FQ_OK) return rc;
         HIP_TRY(e, hipMemsetAsync(sc.slow_count, 0, sizeof(int), s));

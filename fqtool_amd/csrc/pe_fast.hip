@@ -155,7 +155,8 @@ struct Layout {
     static constexpr int kColsW = kWaves * kWaveW;
     static constexpr int kScalCopies = MERGE ? 8 : 16;
     static constexpr int kScalW = 2 * kScalStride * kScalCopies;
-    static constexpr int kLdsW = kColsW + kHistRegW + kSmallW + kInsW + kScalW + kAdW + kPfW;
+    static constexpr int kHrW = 2 * kWaves;  // per wave: hand-off list reservation (next slot, slots left)
+    static constexpr int kLdsW = kColsW + kHistRegW + kSmallW + kInsW + kScalW + kAdW + kHrW + kPfW;
     static_assert(kLdsW * 4 * kBlocksPerCU <= 160 * 1024, "LDS budget");
     static_assert((kColsW & 1) == 0 && (kHistW & 1) == 0, "u64 cells must stay 8-byte aligned");
     static_assert(kThreads <= kBlock, "launch bound");
@@ -758,6 +759,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
     unsigned int* ins = reinterpret_cast<unsigned int*>(small + kSmallW / 2);
     unsigned long long* scal = reinterpret_cast<unsigned long long*>(ins + kInsW);
     uint8_t* adp = reinterpret_cast<uint8_t*>(scal + kScalStride * LY::kScalCopies);
+    int* hres = reinterpret_cast<int*>(adp) + kAdW;  // [wave][next slot, slots left]
+    for (int i = threadIdx.x; i < LY::kHrW; i += kThreads) hres[i] = 0;
     for (int i = threadIdx.x; i < LY::kHistRegW + kSmallW + kInsW + LY::kScalW; i += kThreads) hist[i] = 0;
     for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kThreads)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
@@ -815,6 +818,10 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         for (int i = 0; i < slot * FQ_DESYNC; ++i) __builtin_amdgcn_s_sleep(127);
     }
 #endif
+    // hand-off list: a wave reserves kItems slots at a time (its reservation lives in LDS, hres,
+    // read only on the rare hand-off path)
+    constexpr int kItems = PAIRED ? 32 : 64;
+    constexpr int kHole = 0x7FFFFFFF;
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
         // Per-lane values are derived from an opaque copy of the lane id inside the loop: left to
         // itself the compiler hoists dozens of them out of the tile loop and spills them.
@@ -977,10 +984,23 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             const unsigned long long hm = PAIRED ? ((bm | (bm >> 32)) & 0xFFFFFFFFull) : bm;
             const int me = PAIRED ? pl : lane_x;
             const bool pbad = (hm >> me) & 1ull;
-            int base = 0;
-            if (lane == 0) base = atomicAdd(slow_count, (int)__popcll(hm));
-            base = __shfl(base, 0);
-            if (pbad && mate == 0) slow_tiles[base + (int)__popcll(hm & ((1ull << me) - 1ull))] = idx;
+            // slots come from the wave's reservation of one tile's worth (kItems), so one
+            // same-address atomic serves many tiles; an outgrown reservation's rest becomes holes
+            // (kHole >= n: the general kernel skips them), as does the last one's at the end
+            const int k = (int)__popcll(hm);
+            int hb = hres[2 * wave], hl = hres[2 * wave + 1];
+            if (k > hl) {
+                if (lane_x < hl) slow_tiles[hb + lane_x] = kHole;
+                int base = 0;
+                if (lane == 0) base = atomicAdd(slow_count, kItems);
+                hb = __shfl(base, 0);
+                hl = kItems;
+            }
+            if (pbad && mate == 0) slow_tiles[hb + (int)__popcll(hm & ((1ull << me) - 1ull))] = idx;
+            if (lane == 0) {
+                hres[2 * wave] = hb + k;
+                hres[2 * wave + 1] = hl - k;
+            }
             if (pbad) {
                 valid = false;
                 L = 0;
@@ -1659,6 +1679,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             if (res) *reinterpret_cast<uint4*>(&res[PAIRED ? 2 * (size_t)idx + mate : (size_t)idx]) = w;
         }
     }
+    if (lane < hres[2 * wave + 1]) slow_tiles[hres[2 * wave] + lane] = kHole;  // the rest of the last reservation
 
     FQ_STAMP(7)
 #ifdef FQ_PHASE_STAMPS
