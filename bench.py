@@ -389,6 +389,53 @@ class HipRunner:
                 if not isinstance(x, tuple):
                     lib.fq_host_free(x)
 
+    def paths_leg(self, pairs):
+        """Off the BASELINE configs: C3's options with UMI (8 + 8), with -c, and with 1 % of the
+        pairs holding a lowercase base (handed to the general kernel one by one), on the first
+        `pairs` pairs of the resident shard; kernel ms per launch from HIP events on the launch
+        stream (median of 3 after a warm-up).  Runs after every check: -c rewrites corrected
+        bases in place and the lowercase bases are written into the shard."""
+        abi, lib, torch = self.abi, self.lib, self.torch
+        n = min(pairs, self.n) // abi.TILE_READS * abi.TILE_READS
+        b = abi.FqBatch()
+        for f, _ in abi.FqBatch._fields_:
+            setattr(b, f, getattr(self.batch, f))
+        b.n = n
+        out = {"pairs": n, "unit": "Mreads/s (kernels, HBM-resident)"}
+
+        def timed(p, label):
+            h = ctypes.c_void_p()
+            if lib.fq_engine_create(ctypes.byref(p), self.local, 0, 0, ctypes.byref(h)) != 0:
+                raise RuntimeError(lib.fq_engine_last_error(None).decode())
+            try:
+                ms = []
+                for i in range(4):
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record(self.stream)
+                    if lib.fq_engine_process_device(h, ctypes.byref(b), self.results.data_ptr(),
+                                                    ctypes.c_void_p(self.stream.cuda_stream)) != 0:
+                        raise RuntimeError(lib.fq_engine_last_error(h).decode())
+                    ev[1].record(self.stream)
+                    torch.cuda.synchronize(self.dev)
+                    if i:
+                        ms.append(ev[0].elapsed_time(ev[1]))
+                ms.sort()
+                out[label] = {"ms": round(ms[1], 3), "value": round(2 * n / ms[1] / 1e3, 1)}
+            finally:
+                lib.fq_engine_destroy(h)
+
+        timed(config_params(abi, "C3"), "c3")
+        p = config_params(abi, "C3")
+        p.umi_front1 = p.umi_front2 = 8
+        timed(p, "c3_umi8")
+        p = config_params(abi, "C3")
+        p.correction_enabled = 1
+        timed(p, "c3_correct")
+        i = torch.arange(0, n, 100, device=self.dev, dtype=torch.int64)
+        self.planes[0][(i // abi.TILE_READS) * abi.TILE_READS * STRIDE + (i % abi.TILE_READS) * 16 + 5] = ord("a")
+        timed(config_params(abi, "C3"), "c3_lowercase_1pct")
+        return out
+
     def host_legs(self, cpu_pairs, e2e_pairs, workers):
         del self.planes, self.lens, self.results
         self.torch.cuda.empty_cache()
@@ -510,6 +557,14 @@ def run_rank(args):
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             engine["value_all_ranks"] = round(float(t.item()), 2)
 
+    paths = None
+    if rank == 0 and world == 1 and args.config == "C3" and args.paths_pairs > 0 and hasattr(runner, "paths_leg"):
+        try:
+            paths = runner.paths_leg(args.paths_pairs)
+            log(f"paths {paths}")
+        except Exception as ex:  # a side leg: report, never fail the bench line
+            paths = {"error": str(ex)}
+
     value = reads * args.steps / elapsed / 1e6
     traffic, traffic_src = pmc_traffic(args.config, args.pairs) if world == 1 else (None, None)
     bytes_per_pair = (2 if paired else 1) * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result per read
@@ -539,6 +594,7 @@ def run_rank(args):
         "cpu_baseline": None,
         "engine_mreads_s": engine["value"] if engine else None,
         "engine": engine,
+        "paths": paths,
         "e2e": None,
         "acc_sha256": acc_digest,
         "parity_sample": sample,
@@ -592,6 +648,8 @@ def main():
     ap.add_argument("--cpu-pairs", type=int, default=1_000_000, help="CPU-baseline sample size (pairs)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip both host legs (e2e and CPU baseline)")
     ap.add_argument("--e2e-pairs", type=int, default=10_000_000, help="pairs of the end-to-end tool leg (0: off)")
+    ap.add_argument("--paths-pairs", type=int, default=20_000_000,
+                    help="pairs of the off-baseline path leg (C3 + UMI / -c / 1 %% lowercase; 0: off)")
     ap.add_argument("--sample-pairs", type=int, default=1_000_000,
                     help="per-rank parity sample checked against the oracle after the timed region (0: off)")
     ap.add_argument("--engine-pairs", type=int, default=1_048_576,
