@@ -223,7 +223,7 @@ static int grid_for(const fq_engine* e, int n) {
     if (per_cu < 1) per_cu = 1;
     if (per_cu > 8) per_cu = 8;
     const int cap = e->cus * per_cu;
-    const int need = (n + 255) / 256;
+    const int need = (n + kPackThreads - 1) / kPackThreads;
     return need < cap ? (need > 0 ? need : 1) : cap;
 }
 

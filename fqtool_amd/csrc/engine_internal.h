@@ -5,6 +5,9 @@
 
 #include "../../include/fqengine.h"
 
+// General kernel workgroup: 8 waves (one LDS histogram copy per workgroup, 2 workgroups per CU
+// at <= 160 cycles: 16 waves per CU; it uses ~70 VGPRs, so registers allow more)
+constexpr int kPackThreads = 512;
 size_t fq_pack_kernel_lds_bytes(const fq_params& p);
 hipError_t fq_pack_kernel_set_lds(const fq_params& p);
 // General kernel (any bytes, any length <= max_cycles, merge): all pairs, or only the pairs

@@ -204,7 +204,7 @@ __device__ __forceinline__ fq_read_result index_filtered_result() {
 }
 
 template <bool PAIRED>
-__global__ void __launch_bounds__(256) fq_pack_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
+__global__ void __launch_bounds__(kPackThreads) fq_pack_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                       unsigned long long* __restrict__ acc, int* __restrict__ err,
                                                       const int* __restrict__ tiles, const int* __restrict__ ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -478,9 +478,9 @@ hipError_t fq_launch_pack_kernel(const fq_params& p, const fq_batch& b, fq_read_
                                  int* err, int grid, hipStream_t stream, const int* tiles, const int* ntiles) {
     const size_t lds = fq_pack_kernel_lds_bytes(p);
     if (p.paired)
-        hipLaunchKernelGGL(fq_pack_kernel<true>, dim3(grid), dim3(256), lds, stream, p, b, res, acc, err, tiles, ntiles);
+        hipLaunchKernelGGL(fq_pack_kernel<true>, dim3(grid), dim3(kPackThreads), lds, stream, p, b, res, acc, err, tiles, ntiles);
     else
-        hipLaunchKernelGGL(fq_pack_kernel<false>, dim3(grid), dim3(256), lds, stream, p, b, res, acc, err, tiles,
+        hipLaunchKernelGGL(fq_pack_kernel<false>, dim3(grid), dim3(kPackThreads), lds, stream, p, b, res, acc, err, tiles,
                            ntiles);
     return hipGetLastError();
 }
