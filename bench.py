@@ -235,6 +235,9 @@ class HipRunner:
         from fqtool_amd import abi
 
         self.torch, self.abi, self.args = torch, abi, args
+        ndev = torch.cuda.device_count()
+        if local >= ndev:  # each rank checks its own device (the launcher never touches the GPU)
+            raise SystemExit(f"bench: rank needs cuda:{local} but only {ndev} GPUs are visible")
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
         self.local = local
@@ -487,13 +490,21 @@ def run_rank(args):
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     runner = make_runner(args.runner, args, local)
-    if world > 1:
+    if world > 1 or args.pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         kw = {"device_id": runner.dev} if runner.backend == "nccl" else {}
         dist.init_process_group(runner.backend, **kw)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
-    first, n = shard(rank, world, args.pairs)
+    shard_rank, shard_world = rank, world
+    if args.shard:  # rehearse one rank of a larger job: its index range, on this one process
+        if world != 1:
+            raise SystemExit("bench: --shard is for a single process")
+        shard_rank, shard_world = (int(x) for x in args.shard.split("/"))
+    first, n = shard(shard_rank, shard_world, args.pairs)
     runner.alloc(first, n)
 
     def step(timed):
@@ -583,6 +594,7 @@ def run_rank(args):
         "dtype": "u8",
         "data": "synthetic (seeded counter-based generator in HBM, SURVEY.md 8(d))",
         "config": {"workload": WORKLOADS[args.config], ("pairs_per_gpu" if paired else "reads_per_gpu"): n,
+                   "first_index": first,
                    "read_len": READ_LEN, "row_stride": STRIDE,
                    "parallelism": f"dp{world} (pairs sharded, RCCL sum of the accumulator block)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
@@ -608,8 +620,10 @@ def run_rank(args):
     runner.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
+        out_pg = dist.get_backend()
         dist.destroy_process_group()
+        log(f"rank {rank}: process group ({out_pg}) closed")
     if sample is not None and not sample.get("all_ranks_ok", sample["ok"]):
         raise SystemExit("bench: parity sample FAILED (the engine's records/accumulator differ from the oracle)")
 
@@ -626,15 +640,20 @@ def launch(args):
     if "WORLD_SIZE" in os.environ or args.gpus == 1:
         run_rank(args)
         return
-    if args.runner == "hip":
-        import torch
+    # No torch.cuda / HIP call here: this process only forks+execs the ranks (a GPU-initialised
+    # process must never replace its program on this pool); each rank checks its own device.
+    import multiprocessing as mp
 
-        ndev = torch.cuda.device_count()  # counts devices without initialising HIP in this process
-        if ndev < args.gpus:
-            raise SystemExit(f"bench: --gpus {args.gpus} but only {ndev} GPUs are visible")
-    import torch.multiprocessing as mp
-
-    mp.start_processes(_spawned_rank, args=(args, free_port()), nprocs=args.gpus, join=True, start_method="spawn")
+    ctx = mp.get_context("spawn")
+    port = free_port()
+    procs = [ctx.Process(target=_spawned_rank, args=(i, args, port)) for i in range(args.gpus)]
+    for p_ in procs:
+        p_.start()
+    for p_ in procs:
+        p_.join()
+    bad = [(i, p_.exitcode) for i, p_ in enumerate(procs) if p_.exitcode != 0]
+    if bad:
+        raise SystemExit(f"bench: rank(s) failed: {bad}")
 
 
 def main():
@@ -660,6 +679,12 @@ def main():
                     help="synthetic read length (default 150, the BASELINE configs); longer reads exercise "
                          "the long-read kernel variant")
     ap.add_argument("--runner", default="hip", help=argparse.SUPPRESS)  # tests: CPU rehearsal of the ranks
+    ap.add_argument("--shard", default=None,
+                    help="R/W: process rank R's index range of a W-rank job on this single process "
+                         "(e.g. 7/8 with --config C5: the last shard of config 5)")
+    ap.add_argument("--pg", action="store_true",
+                    help="create the process group (RCCL on the GPU) and run the accumulator all-reduce "
+                         "even with one rank")
     args = ap.parse_args()
     if args.pairs is None:
         args.pairs = 125_000_000 if args.config == "C5" else 100_000_000

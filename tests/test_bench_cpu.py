@@ -48,3 +48,37 @@ def test_bench_refuses_world_size_mismatch():
     r = run_bench("--gpus", "2", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_gpus4_c5_rehearsal_equals_oracle_over_union(oracle):
+    """Config 5's shape (C5 options, N ranks each owning a contiguous index range, one SUM of the
+    accumulator block) at 4 ranks on gloo: the reduced block is one oracle run over the union."""
+    import bench
+    from fqtool_amd import abi
+
+    r = run_bench("--gpus", "4", "--config", "C5", "--pairs", "1000")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 4 and out["config"]["pairs_per_gpu"] == 1000 and out["config"]["first_index"] == 0
+    p = bench.config_params(abi, "C5")
+    pk = synth_pack(oracle, 4000, True, first=0)
+    _, acc = run_oracle(oracle, p, pk)
+    assert out["acc_sha256"] == hashlib.sha256(acc.tobytes()).hexdigest()
+
+
+def test_bench_shard_option_runs_one_rank_of_a_larger_job(oracle):
+    """--shard 3/4 --pg: one process takes rank 3's index range and still runs the collective
+    (a world-1 process group), the rehearsal the GPU suite runs for config 5's rank 7 of 8."""
+    import bench
+    from fqtool_amd import abi
+
+    r = run_bench("--config", "C5", "--pairs", "1000", "--shard", "3/4", "--pg",
+                  env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(bench.free_port())})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["config"]["first_index"] == 3000
+    assert "process group (gloo) closed" in r.stderr
+    p = bench.config_params(abi, "C5")
+    pk = synth_pack(oracle, 1000, True, first=3000)
+    _, acc = run_oracle(oracle, p, pk)
+    assert out["acc_sha256"] == hashlib.sha256(acc.tobytes()).hexdigest()

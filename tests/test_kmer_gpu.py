@@ -22,7 +22,7 @@ def eng_lib():
     return abi.load_engine()
 
 
-def testdata_reads():
+def _testdata_reads():
     with gzip.open(os.path.join(INPUTS, "r2.fq.gz")) as f:
         lines = f.read().split(b"\n")
     return [lines[i] for i in range(1, len(lines), 4)]
@@ -43,7 +43,7 @@ def readset(reads):
 @pytest.mark.parametrize("source", ["testdata", "edge"])
 @pytest.mark.parametrize("tail", [1, 4])
 def test_kmer_histogram_and_seeds(eng_lib, oracle, source, tail):
-    reads = testdata_reads() if source == "testdata" else edge_reads()
+    reads = _testdata_reads() if source == "testdata" else edge_reads()
     seq, off = readset(reads)
     n = len(reads)
     k, first = 10, 20
