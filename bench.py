@@ -30,6 +30,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+SIMDS = 1024  # 256 CUs x 4 SIMD-32
+CLOCK_HZ = 2.4e9  # MI355X max shader clock
 PCIE_PEAK_GBS = 64.0  # PCIe 5.0 x16, one direction (host <-> MI355X)
 READ_LEN = 150
 STRIDE = 160
@@ -56,6 +58,21 @@ def pmc_traffic(cfg, pairs):
     if int(d.get("pairs", -1)) != pairs:
         return None, None
     return int(d["traffic_bytes"]), os.path.relpath(paths[-1], REPO)
+
+
+def sq_profile(cfg, pairs):
+    """VALU wave-instructions per launch of the fast kernel for this workload, from the latest
+    committed SQ counter profile (tools/pmc_sq.sh + tools/pmc_sq_summary.py: rocprofv3 --pmc
+    SQ_INSTS_VALU ... passes of this bench command); (None, None) when no profile matches."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_sq_{cfg}.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    if int(d.get("pairs", d.get("reads", -1))) != pairs:
+        return None, None
+    return d, os.path.relpath(paths[-1], REPO)
 
 
 def log(msg):
@@ -578,6 +595,18 @@ def run_rank(args):
 
     value = reads * args.steps / elapsed / 1e6
     traffic, traffic_src = pmc_traffic(args.config, args.pairs) if world == 1 else (None, None)
+    sq, sq_src = sq_profile(args.config, args.pairs) if world == 1 else (None, None)
+    valu = None
+    if sq and kavg and sq.get("counters_per_launch", {}).get("SQ_INSTS_VALU"):
+        # VALU issue fraction: each wave64 VALU instruction holds a SIMD-32 for 2 cycles
+        # (MI355X_MICROARCH.md); peak = 1024 SIMDs x 2.4 GHz; the instruction count is the committed
+        # PMC profile's, the time is this run's HIP-event kernel time
+        n_valu = sq["counters_per_launch"]["SQ_INSTS_VALU"]
+        valu = {"insts_per_launch": n_valu, "per_tile": sq.get("valu_per_tile"),
+                "frac": round(n_valu * 2 / (SIMDS * CLOCK_HZ * kavg / 1e3), 4),
+                "frac_at_profiled_clock": sq.get("valu_issue_frac"), "src": sq_src,
+                "wait_frac": sq.get("wait_frac"), "inst_stall_frac": sq.get("inst_stall_frac"),
+                "active_frac": sq.get("active_frac")}
     bytes_per_pair = (2 if paired else 1) * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result per read
     achieved = n * bytes_per_pair / (kavg / 1e3) / 1e9 if kavg else None
     out = {
@@ -602,7 +631,8 @@ def run_rank(args):
                      "traffic": traffic, "traffic_unit": "bytes per launch (PMC)", "traffic_src": traffic_src,
                      "algorithmic_bytes": n * bytes_per_pair,
                      "kernel_ms_avg": round(kavg, 3) if kavg else None,
-                     ("bytes_per_pair" if paired else "bytes_per_read"): bytes_per_pair},
+                     ("bytes_per_pair" if paired else "bytes_per_read"): bytes_per_pair,
+                     "valu": valu},
         "cpu_baseline": None,
         "engine_mreads_s": engine["value"] if engine else None,
         "engine": engine,
