@@ -64,6 +64,12 @@ namespace {
 #ifndef FQ_MERGE_BLOCKS
 #define FQ_MERGE_BLOCKS 1
 #endif
+#ifndef FQ_LEAN_WAVES
+#define FQ_LEAN_WAVES 8  // profiling: waves per workgroup of the LEAN variant
+#endif
+#ifndef FQ_LEAN_BLOCKS
+#define FQ_LEAN_BLOCKS 2  // profiling: workgroups per CU of the LEAN variant
+#endif
 #ifndef FQ_MERGE_QLDS
 #define FQ_MERGE_QLDS 0
 #endif
@@ -140,8 +146,8 @@ template <bool LEAN, bool MERGE = false>
 struct Layout {
     // quality rows staged in LDS (off: rows are re-read from L2); profiling switch for the merge variant
     static constexpr bool kQLds = MERGE && FQ_MERGE_QLDS;
-    static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160) ? 1 : MERGE ? FQ_MERGE_BLOCKS : 2;
-    static constexpr int kWaves = MERGE ? (kQLds ? 7 : FQ_MERGE_WAVES) : 8;
+    static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160) ? 1 : MERGE ? FQ_MERGE_BLOCKS : LEAN ? FQ_LEAN_BLOCKS : 2;
+    static constexpr int kWaves = MERGE ? (kQLds ? 7 : FQ_MERGE_WAVES) : (LEAN && kMaxLen <= 160) ? FQ_LEAN_WAVES : 8;
     static constexpr int kWavesPerEU = (kWaves * kBlocksPerCU + 3) / 4;
     static constexpr int kThreads = 64 * kWaves;
     static constexpr int kWaveW = kCodeW + (kQLds ? 64 * kQS : 0);
@@ -839,7 +845,12 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         uint32_t* my_post = hist + (2 + (MERGE ? 2 : 1) * mate) * kHistW;  // post block, or the "removed" block
         const int r = lane_x & 15;  // stats rotation within a chunk
         uint32_t* qrow = qrows + lane_x * kQS;
+#ifdef FQ_SAME_TILE  // profiling only: every wave re-reads a few L2-resident tiles (results invalid)
+        const int tt = t & (FQ_SAME_TILE - 1);
+        const int idx = PAIRED ? tt * 32 + pl : tt * 64 + lane_x;
+#else
         const int idx = PAIRED ? t * 32 + pl : t * 64 + lane_x;
+#endif
         bool valid = idx < b.n;  // (both cleared below for a pair handed to the general kernel)
         int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
 
