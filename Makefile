@@ -21,9 +21,6 @@ endif
 ifneq ($(SCHED_PIN),)
 HIPFLAGS   += -DFQ_SCHED_PIN=$(SCHED_PIN)
 endif
-ifneq ($(FIXED_STRIDE),)
-HIPFLAGS   += -DFQ_FIXED_STRIDE=1
-endif
 ifneq ($(AHEAD),)
 HIPFLAGS   += -DFQ_AHEAD=$(AHEAD)
 endif

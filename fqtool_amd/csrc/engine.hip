@@ -28,7 +28,8 @@ struct Slot {
     fq_read_result* d_res = nullptr;
     Scratch scratch;
     hipEvent_t ev_in = nullptr, ev_kern = nullptr, ev_done = nullptr;
-    int* h_err = nullptr;  // pinned: the device error flag as of this pack's kernels
+    int* d_err = nullptr;  // this pack's device error word (cleared at submit, set by its kernels)
+    int* h_err = nullptr;  // pinned: d_err as of this pack's kernels
     bool busy = false;      // events recorded and not yet waited for
 };
 
@@ -85,7 +86,7 @@ static int hip_fail(fq_engine* e, hipError_t err, const char* what) {
     } while (0)
 
 static int validate_params(const fq_params* p, std::string& why) {
-    if (p->max_cycles < 1 || p->max_cycles > 4096) return why = "max_cycles must be in [1, 4096]", FQ_E_INVALID;
+    if (p->max_cycles < 1 || p->max_cycles > FQ_MAX_CYCLES_LIMIT) return why = "max_cycles must be in [1, 4096]", FQ_E_INVALID;
     if (p->insert_size_max < 0 || p->insert_size_max > 100000) return why = "bad insert_size_max", FQ_E_INVALID;
     if (p->cut_front && p->cut_front_window < 1) return why = "cut_front window must be >= 1", FQ_E_INVALID;
     if (p->cut_right && p->cut_right_window < 1) return why = "cut_right window must be >= 1", FQ_E_INVALID;
@@ -122,6 +123,7 @@ static void free_slot(Slot& s) {
     if (s.d_lens) (void)hipFree(s.d_lens);
     if (s.d_flags) (void)hipFree(s.d_flags);
     if (s.d_res) (void)hipFree(s.d_res);
+    if (s.d_err) (void)hipFree(s.d_err);
     if (s.h_err) (void)hipHostFree(s.h_err);
     if (s.ev_in) (void)hipEventDestroy(s.ev_in);
     if (s.ev_kern) (void)hipEventDestroy(s.ev_kern);
@@ -137,6 +139,7 @@ static int alloc_slot(fq_engine* e, Slot& s) {
     HIP_TRY(e, hipMalloc(&s.d_lens, (size_t)2 * e->max_batch * sizeof(uint16_t)));
     HIP_TRY(e, hipMalloc(&s.d_flags, (size_t)e->max_batch + 1));
     HIP_TRY(e, hipMalloc(&s.d_res, (size_t)2 * e->max_batch * sizeof(fq_read_result)));
+    HIP_TRY(e, hipMalloc(&s.d_err, sizeof(int)));
     HIP_TRY(e, hipHostMalloc((void**)&s.h_err, sizeof(int), hipHostMallocDefault));
     *s.h_err = 0;
     HIP_TRY(e, hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
@@ -230,7 +233,7 @@ static int grid_for(const fq_engine* e, int n) {
 // Enqueues the kernels of one batch on stream s.  `sc` is the hand-off list of this launch; it
 // must not be shared with a launch that can run concurrently (different stream).
 static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStream_t s, Scratch& sc, bool timed,
-                  bool sync_device_on_grow, uint64_t order) {
+                  bool sync_device_on_grow, uint64_t order, int* derr) {
     if (db.n <= 0) return FQ_OK;
     if (e->dup) {  // Duplicate::statPair / statRead run on the untrimmed reads (src/peprocessor.cpp:279-281)
         const int rc = fq_dup_pack(e->dup, db, e->p.paired, order, s);
@@ -248,11 +251,11 @@ static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStr
         HIP_TRY(e, fq_launch_pe_fast(e->p, db, dres, e->acc, sc.slow_tiles, sc.slow_count, e->cus, s));
         // (the hand-off list's length is known on the device only: as many workgroups as the
         // batch could need, at the occupancy the kernel's LDS allows; empty ones exit at once)
-        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, grid_for(e, db.n), s, sc.slow_tiles,
+        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, derr, grid_for(e, db.n), s, sc.slow_tiles,
                                          sc.slow_count));
     } else {
         if (timed) HIP_TRY(e, hipEventRecord(e->ev0, s));
-        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, e->err, grid_for(e, db.n), s));
+        HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, derr, grid_for(e, db.n), s));
     }
     if (timed) {
         HIP_TRY(e, hipEventRecord(e->ev1, s));
@@ -291,11 +294,8 @@ static int validate_host_batch(fq_engine* e, const fq_batch* hb) {
         return fail(e, FQ_E_INVALID, "batch exceeds the engine's max_batch/max_stride (or stride % 16 != 0)");
     if (!hb->seq1 || !hb->qual1 || !hb->len1 || (pe && (!hb->seq2 || !hb->qual2 || !hb->len2)))
         return fail(e, FQ_E_INVALID, "missing batch arrays");
-    for (int i = 0; i < hb->n; ++i) {
-        if (hb->len1[i] > e->p.max_cycles || hb->len1[i] > hb->stride ||
-            (pe && (hb->len2[i] > e->p.max_cycles || hb->len2[i] > hb->stride)))
-            return fail(e, FQ_E_TOO_LONG, "read longer than max_cycles / stride");
-    }
+    // (read lengths are checked on the device: a read longer than max_cycles or the stride sets
+    // the pack's error word, which fq_engine_poll reports as FQ_E_TOO_LONG)
     return FQ_OK;
 }
 
@@ -346,14 +346,15 @@ int fq_engine_submit(fq_engine* e, const fq_batch* hb, fq_read_result* results, 
     HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
     // kernels on the compute stream (one accumulator: the packs' kernels run in order)
     HIP_TRY(e, hipStreamWaitEvent(e->stream, s.ev_in, 0));
-    if ((rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false, seq_no)) != FQ_OK) return rc;
+    HIP_TRY(e, hipMemsetAsync(s.d_err, 0, sizeof(int), e->stream));
+    if ((rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false, seq_no, s.d_err)) != FQ_OK) return rc;
     HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
     // D2H of the records (and of the error flag) on the copy-out stream
     HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
     const size_t nres = (size_t)hb->n * (pe ? 2 : 1);
     if (nres)
         HIP_TRY(e, hipMemcpyAsync(results, s.d_res, nres * sizeof(fq_read_result), hipMemcpyDeviceToHost, e->s_out));
-    HIP_TRY(e, hipMemcpyAsync(s.h_err, e->err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
+    HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
     HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
     s.busy = true;
     e->pending.push_back(Pending{seq_no, k, false, 0});
@@ -378,11 +379,7 @@ int fq_engine_poll(fq_engine* e, int wait, uint64_t* seq_no) {
     const Pending done = q;
     e->pending.pop_front();
     if (seq_no) *seq_no = done.seq_no;
-    if (done.err) {
-        HIP_TRY(e, hipMemsetAsync(e->err, 0, sizeof(int), e->stream));
-        HIP_TRY(e, hipStreamSynchronize(e->stream));
-        return fail(e, FQ_E_TOO_LONG, "a read is longer than max_cycles or the row stride");
-    }
+    if (done.err) return fail(e, FQ_E_TOO_LONG, "a read is longer than max_cycles or the row stride");
     return 1;
 }
 
@@ -404,7 +401,7 @@ int fq_engine_process_device(fq_engine* e, const fq_batch* db, fq_read_result* d
         return fail(e, FQ_E_INVALID, "bad device batch");
     HIP_TRY(e, hipSetDevice(e->device));
     // NULL is the HIP default stream
-    return launch(e, *db, dres, (hipStream_t)stream, e->scratch, true, true, e->calls++);
+    return launch(e, *db, dres, (hipStream_t)stream, e->scratch, true, true, e->calls++, e->err);
 }
 
 size_t fq_engine_acc_words(const fq_engine* e) { return e ? e->acc_words : 0; }

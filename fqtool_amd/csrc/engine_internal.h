@@ -1,6 +1,9 @@
 // engine_internal.h -- launch entry points shared between the engine's translation units.
 #pragma once
 
+// largest fq_params.max_cycles an engine accepts (reads beyond it fail the pack with FQ_E_TOO_LONG)
+#define FQ_MAX_CYCLES_LIMIT 4096
+
 #include <hip/hip_runtime.h>
 
 #include "../../include/fqengine.h"

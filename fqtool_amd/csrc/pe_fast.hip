@@ -64,6 +64,9 @@ namespace {
 #ifndef FQ_MERGE_BLOCKS
 #define FQ_MERGE_BLOCKS 1
 #endif
+#ifndef FQ_LEAN_DIRECT
+#define FQ_LEAN_DIRECT 1  // LEAN passFilter: a window shorter than half the read is summed directly
+#endif
 #ifndef FQ_LEAN_WAVES
 #define FQ_LEAN_WAVES 8  // profiling: waves per workgroup of the LEAN variant
 #endif
@@ -238,18 +241,6 @@ __device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool
     return Fwd{cw, nw};
 }
 
-// fwd_chunk for a chunk known to lie inside the column (0 <= F < kChunks): no bounds handling
-__device__ __forceinline__ Fwd fwd_chunk_in(const uint32_t* col, int c, int F, bool rc) {
-    const int w = rc ? kChunks - 1 - F : F;
-    uint32_t cw = col[(kFC + w) * 64 + c], nw = col[(kFN + w) * 64 + c];
-    if (rc) {
-        cw = pairrev(cw);
-        nw = pairrev(nw);
-        cw ^= 0xAAAAAAAAu & ~(nw << 1);  // complement back, N stays code 3
-    }
-    return Fwd{cw, nw};
-}
-
 struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N)
     const uint32_t* col;
     int c;
@@ -273,28 +264,33 @@ struct OvOut {
 // positions compare r1 codes from p1 with rc2 codes from p2 over `ol` positions.  The four
 // streams (codes and N masks of both sides) slide one LDS word per 16 positions; a candidate whose
 // K-th mismatch lies in the first 50 positions is rejected after the first four words.
+// The words are read unclamped: p1, p2 >= 0 and p + ol <= the column length, so a look-ahead word
+// past the column (the next field, or the next wave's column: valid LDS) only feeds positions at
+// or beyond ol, which the last word's mask drops.
 __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int p2, int ol, int limit, int K,
                                 int& diff_out) {
     int d50 = 0, D = 0;
     const int nw = (ol + 15) >> 4;
-    const int w1 = p1 >> 4, s1 = 2 * (p1 & 15), w2 = p2 >> 4, s2 = 2 * (p2 & 15);
-    // word w of field f of column c, 0 outside the column
-    auto word = [&](int f, int c, int w) -> uint32_t {
-        const uint32_t v = col[(f + min(max(w, 0), kChunks - 1)) * 64 + c];
-        return (unsigned)w < (unsigned)kChunks ? v : 0u;
-    };
-    uint32_t a0 = word(kFC, c1, w1), an0 = word(kFN, c1, w1), b0 = word(kFC, c2, w2), bn0 = word(kFN, c2, w2);
+    const int s1 = 2 * (p1 & 15), s2 = 2 * (p2 & 15);
+    const uint32_t* A = col + (p1 >> 4) * 64 + c1;  // code word w of read 1's window: A[64 w]
+    const uint32_t* B = col + (p2 >> 4) * 64 + c2;
+    constexpr int kN = kFN * 64;                       // the N-mask field, kChunks words further
+    const uint32_t last = posmask(ol - 16 * (nw - 1));  // valid positions of the last word
+    uint32_t a0 = A[0], an0 = A[kN], b0 = B[0], bn0 = B[kN];
     for (int j = 0; j < nw; ++j) {
-        const uint32_t a1 = word(kFC, c1, w1 + j + 1), an1 = word(kFN, c1, w1 + j + 1);
-        const uint32_t b1 = word(kFC, c2, w2 + j + 1), bn1 = word(kFN, c2, w2 + j + 1);
+        const uint32_t a1 = A[64 * (j + 1)], an1 = A[64 * (j + 1) + kN];
+        const uint32_t b1 = B[64 * (j + 1)], bn1 = B[64 * (j + 1) + kN];
         const uint32_t a = __builtin_amdgcn_alignbit(a1, a0, s1), wa = __builtin_amdgcn_alignbit(an1, an0, s1);
         const uint32_t b = __builtin_amdgcn_alignbit(b1, b0, s2), wb = __builtin_amdgcn_alignbit(bn1, bn0, s2);
-        const uint32_t mism = (fold2(a ^ b) & ~(wa | wb)) | (wa ^ wb);
-        D += __popc(mism & posmask(ol - 16 * j));
-        d50 += __popc(mism & posmask(min(ol, 50) - 16 * j));
+        uint32_t mism = (fold2(a ^ b) & ~(wa | wb)) | (wa ^ wb);
+        if (j == nw - 1) mism &= last;
+        // mismatches within the first 50 positions: words 0-2 whole, word 3's positions 48, 49
+        if (j == 3) d50 = D + __popc(mism & 5u);
+        D += __popc(mism);
         if (j == 3 && d50 >= K) break;  // rejected whatever follows (the break happens within 50)
         a0 = a1; an0 = an1; b0 = b1; bn0 = bn1;
     }
+    if (nw <= 3) d50 = D;  // (ol <= 48: every position is within 50)
     diff_out = D;
     // break (rejection) happens iff the K-th mismatch lies within the first min(ol,50) positions
     if (d50 >= K) return false;
@@ -390,15 +386,24 @@ __device__ __forceinline__ void csa(uint32_t& hi, uint32_t& lo, uint32_t a, uint
 // spread over a word), and the 16 vectors are summed per offset with carry-save adders.
 __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint32_t fixed, int K, int cnt,
                                      uint32_t cand[kOvBlocks]) {
-    // planes of the 32 positions from mpos + 32 * i (i = block): low-bit plane, high-bit plane
-    auto planes = [&](int i, uint32_t& lp, uint32_t& hp) {
-        const uint32_t u0 = unzip2(field_window(col, kFC, cm, mpos + 32 * i));
-        const uint32_t u1 = unzip2(field_window(col, kFC, cm, mpos + 32 * i + 16));
+    // planes of the 32 positions from mpos + 32 * i (i = block): low-bit plane, high-bit plane,
+    // from a stream of the column's code words (two new LDS words per block).  Unclamped: mpos >= 0,
+    // and words past the column (the N field, or the next wave's column: valid LDS) only feed
+    // offsets >= cnt, which the block masks drop.
+    const int sh = 2 * (mpos & 15);
+    const uint32_t* W = col + (kFC + (mpos >> 4)) * 64 + cm;
+    uint32_t wlo = W[0];
+    auto planes = [&](uint32_t& lp, uint32_t& hp) {
+        const uint32_t wm = W[64], whi = W[128];
+        W += 128;
+        const uint32_t u0 = unzip2(__builtin_amdgcn_alignbit(wm, wlo, sh));
+        const uint32_t u1 = unzip2(__builtin_amdgcn_alignbit(whi, wm, sh));
+        wlo = whi;
         lp = __builtin_amdgcn_perm(u1, u0, 0x05040100u);  // u0 bits 0-15 | u1 bits 0-15 << 16
         hp = __builtin_amdgcn_perm(u1, u0, 0x07060302u);  // u0 bits 16-31 | u1 bits 16-31 << 16
     };
     uint32_t L0, H0, L1, H1;
-    planes(0, L0, H0);
+    planes(L0, H0);
     const uint32_t fu = unzip2(fixed);
     int nblk = 2;  // blocks holding some lane's offsets (wave-uniform)
 #pragma unroll
@@ -409,7 +414,7 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
         if (bk >= nblk) cand[bk] = 0u;
 #pragma unroll 1
     for (int bk = 0; bk < nblk; ++bk) {
-        if (bk < kOvBlocks - 1) planes(bk + 1, L1, H1);
+        if (bk < kOvBlocks - 1) planes(L1, H1);
         else L1 = H1 = 0u;
         // mismatch vector of compared position j over the block's 32 offsets
         auto m = [&](int j) -> uint32_t {
@@ -750,7 +755,9 @@ __device__ inline void correct_pair_fast(const fq_params& p, uint32_t* col, uint
 
 // XTRA: the -c / UMI / -e instantiation of the full variants (kept apart so the other variants'
 // register allocation does not carry that code)
-template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA = false>
+// FIX: rows of exactly kChunks chunks (the batch stride is the column length: 160, or 320 in the long
+// build), so every per-chunk offset and bound is a compile-time constant
+template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA = false, bool FIX = false>
 __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
@@ -778,11 +785,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
     // 1024 skip trimAndCut (FULL), 2048 skip polyX
     const int abl = p.reserved[0];
     const int ntiles = PAIRED ? (b.n + 31) >> 5 : (b.n + 63) >> 6;
-#if FQ_FIXED_STRIDE  // profiling only: assume rows of >= 160 bytes
-    constexpr int nchunks = kChunks;
-#else
-    const int nchunks = min(kChunks, b.stride >> 4);
-#endif
+    const int nchunks = FIX ? kChunks : min(kChunks, b.stride >> 4);
     const int limit = p.overlap_diff_limit;
     const int K = max(limit, 1);
     const int req = p.overlap_require;
@@ -888,7 +891,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         // be hoisted out of the tile loop and spilled
         int nch = nchunks;
 #if FQ_OPAQUE_NCH
-        asm volatile("" : "+s"(nch));
+        if constexpr (!FIX) asm volatile("" : "+s"(nch));
 #endif
         const int lastc = nch - 1;
         uint4 sb[kChunks], qb[kChunks];
@@ -1289,7 +1292,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             // tail [ws+wn, L): the trimmed parts are usually a few bases.  (FULL: a window
             // shorter than half the read, e.g. read 2's part of a merged read, is summed directly:
             // "subtracted" from 0 and negated.)
-            const bool direct = !LEAN && 2 * wn < L;
+            const bool direct = (!LEAN || FQ_LEAN_DIRECT) && 2 * wn < L;
             low = direct ? 0 : (int)lowf;
             tq = direct ? 0 : (int)tqf;
             nb = direct ? 0 : (int)nbf;
@@ -1322,7 +1325,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                         }
                     };
 #if FQ_FILTER_BATCH
-                    if (!LEAN && a0 < a1) {
+                    if ((!LEAN || FQ_LEAN_DIRECT) && a0 < a1) {
                         // (FULL) the range's row chunks from L2, four requested together per round
                         // trip (LEAN, whose ranges are the trimmed tails only, is faster as below)
                         for (int Fb = F0; Fb < F1; Fb += 4) {
@@ -1452,7 +1455,19 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             uint4 qb[kSA + 1];
 #pragma unroll
             for (int i = 0; i < kSA; ++i) qb[i] = qchunk(min(i, nchunks - 1));
-            Fwd fn = fwd_chunk_in(col, lane_x, 0, rc);
+            // this lane's column word of forward chunk F: cw0 + F * cstep (read 2's column is reversed)
+            const uint32_t* cwp = col + lane_x + (rc ? (kChunks - 1) * 64 : 0);
+            const int cstep = rc ? -64 : 64;
+            auto fwd_at = [&](const uint32_t* wp_) {
+                uint32_t cw = wp_[kFC * 64], nw = wp_[kFN * 64];
+                if (rc) {
+                    cw = pairrev(cw);
+                    nw = pairrev(nw);
+                    cw ^= 0xAAAAAAAAu & ~(nw << 1);  // complement back, N stays code 3
+                }
+                return Fwd{cw, nw};
+            };
+            Fwd fn = fwd_at(cwp);
             // nibble prefix masks from one 64-bit shift: ~(~0 << 4 * clamp(len, 0, 16)), the
             // 64th bit never needed (nibble 15's top bit is 0 in 0x4444... and 0xAAAA... masks)
             const int w4 = 4 * wlen, l4 = 4 * L;
@@ -1463,7 +1478,11 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                     const uint32_t q0 = qb[F % (kSA + 1)].x, q1 = qb[F % (kSA + 1)].y, q2 = qb[F % (kSA + 1)].z,
                                    q3 = qb[F % (kSA + 1)].w;
                     if (F + kSA < kChunks) qb[(F + kSA) % (kSA + 1)] = qchunk(min(F + kSA, nchunks - 1));
-                    if (F + 1 < kChunks) fn = fwd_chunk_in(col, lane_x, min(F + 1, nchunks - 1), rc);
+                    // (chunks from nch on are zero-filled by staging: no clamp)
+                    if (F + 1 < kChunks) {
+                        cwp += cstep;
+                        fn = fwd_at(cwp);
+                    }
                     const int vl = L - 16 * F;
                     // slot 4 * kept + code; an N (code 3) reads as a G here
                     const unsigned long long km = ~(~0ull << min(max(w4 - 64 * F, 0), 63));
@@ -1815,34 +1834,46 @@ extern "C" __attribute__((visibility("default"))) int fq_debug_phase_cycles(unsi
 #define FQ_LAUNCH fq_launch_pe_fast_long
 #endif
 
+// every instantiation (and its FIX twin) may use the LDS its layout declares
+template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA>
+static hipError_t set_lds() {
+    const int bytes = Layout<LEAN, MERGE>::kLdsW * 4 + (LEAN ? 4096 : 0);  // (LEAN: + profiling pad, reserved[2])
+    hipError_t e = hipFuncSetAttribute((const void*)pe_fast_kernel<LEAN, PAIRED, MERGE, XTRA, false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes > 160 * 1024 ? 160 * 1024 : bytes);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)pe_fast_kernel<LEAN, PAIRED, MERGE, XTRA, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes > 160 * 1024 ? 160 * 1024 : bytes);
+}
+
 hipError_t FQ_PREPARE() {
-    constexpr int nk = FQ_MAXLEN == 160 ? 5 : 4;
-    const void* k[5] = {(const void*)pe_fast_kernel<true, true, false>, (const void*)pe_fast_kernel<false, true, false>,
-                        (const void*)pe_fast_kernel<true, false, false>, (const void*)pe_fast_kernel<false, false, false>,
-#if FQ_MAXLEN == 160
-                        (const void*)pe_fast_kernel<false, true, true>
-#else
-                        nullptr
-#endif
-    };
-    for (int i = 0; i < nk; ++i) {
-        int words = (i & 1) ? Layout<false>::kLdsW : 160 * 1024 / 4;
-#if FQ_MAXLEN == 160
-        if (i == 4) words = Layout<false, true>::kLdsW;
-#endif
-        hipError_t e = hipFuncSetAttribute(k[i], hipFuncAttributeMaxDynamicSharedMemorySize, words * 4);
-        if (e != hipSuccess) return e;
-    }
+    hipError_t e;
+    if ((e = set_lds<true, true, false, false>()) != hipSuccess) return e;
+    if ((e = set_lds<false, true, false, false>()) != hipSuccess) return e;
+    if ((e = set_lds<true, false, false, false>()) != hipSuccess) return e;
+    if ((e = set_lds<false, false, false, false>()) != hipSuccess) return e;
     // the -c / UMI instantiations of the full variants
-    for (const void* kx : {(const void*)pe_fast_kernel<false, true, false, true>, (const void*)pe_fast_kernel<false, false, false, true>}) {
-        hipError_t e = hipFuncSetAttribute(kx, hipFuncAttributeMaxDynamicSharedMemorySize, Layout<false>::kLdsW * 4);
-        if (e != hipSuccess) return e;
-    }
+    if ((e = set_lds<false, true, false, true>()) != hipSuccess) return e;
+    if ((e = set_lds<false, false, false, true>()) != hipSuccess) return e;
 #if FQ_MAXLEN == 160
+    if ((e = set_lds<false, true, true, false>()) != hipSuccess) return e;
     return fq_pe_fast_long_prepare();
 #else
     return hipSuccess;
 #endif
+}
+
+template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA>
+static void launch_variant(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
+                           int* slow_tiles, int* slow_count, int grid, int extra_lds, hipStream_t stream) {
+    using LY = Layout<LEAN, MERGE>;
+    const dim3 g(grid * LY::kBlocksPerCU), t(LY::kThreads);
+    const size_t lds = LY::kLdsW * 4 + extra_lds;
+    if (b.stride == 16 * kChunks)
+        hipLaunchKernelGGL((pe_fast_kernel<LEAN, PAIRED, MERGE, XTRA, true>), g, t, lds, stream, p, b, res, acc, slow_tiles,
+                           slow_count);
+    else
+        hipLaunchKernelGGL((pe_fast_kernel<LEAN, PAIRED, MERGE, XTRA, false>), g, t, lds, stream, p, b, res, acc, slow_tiles,
+                           slow_count);
 }
 
 hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
@@ -1857,37 +1888,26 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
                       !p.cut_front && !p.cut_right && !p.cut_tail && !p.polyx_enabled && p.adapter1_len == 0 &&
                       p.adapter2_len == 0 && p.max_len1 <= 0 && p.max_len2 <= 0 && !p.complexity_enabled &&
                       !p.correction_enabled && p.umi_front1 <= 0 && p.umi_front2 <= 0;
-    using LL = Layout<true>;
-    using LF = Layout<false>;
     // -c, UMI and -e (the whole-read quality total) run on the XTRA instantiations (lean is false then)
     const bool xtra = p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0 || p.avg_qual_limit > 0;
-    const dim3 gl(grid * LL::kBlocksPerCU), gf(grid * LF::kBlocksPerCU);
+    const int pad = p.reserved[2] > 0 && p.reserved[2] <= 4096 ? p.reserved[2] : 0;  // profiling: extra LDS (LEAN)
 #if FQ_MAXLEN == 160
-    using LM = Layout<false, true>;
     if (p.merge_enabled)
-        hipLaunchKernelGGL((pe_fast_kernel<false, true, true>), dim3(grid * LM::kBlocksPerCU), dim3(LM::kThreads),
-                           LM::kLdsW * 4, stream, p, b, res, acc, slow_tiles, slow_count);
+        launch_variant<false, true, true, false>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
     else
 #endif
     if (p.paired && lean)
-        // (fq_params.reserved[2]: extra LDS bytes per workgroup, profiling only -- lowers occupancy)
-        hipLaunchKernelGGL((pe_fast_kernel<true, true, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4 + p.reserved[2], stream, p, b,
-                           res, acc, slow_tiles, slow_count);
+        launch_variant<true, true, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, pad, stream);
     else if (p.paired && xtra)
-        hipLaunchKernelGGL((pe_fast_kernel<false, true, false, true>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
-                           res, acc, slow_tiles, slow_count);
+        launch_variant<false, true, false, true>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
     else if (p.paired)
-        hipLaunchKernelGGL((pe_fast_kernel<false, true, false>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
-                           res, acc, slow_tiles, slow_count);
+        launch_variant<false, true, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
     else if (lean)
-        hipLaunchKernelGGL((pe_fast_kernel<true, false, false>), gl, dim3(LL::kThreads), LL::kLdsW * 4, stream, p, b,
-                           res, acc, slow_tiles, slow_count);
+        launch_variant<true, false, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, pad, stream);
     else if (xtra)
-        hipLaunchKernelGGL((pe_fast_kernel<false, false, false, true>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
-                           res, acc, slow_tiles, slow_count);
+        launch_variant<false, false, false, true>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
     else
-        hipLaunchKernelGGL((pe_fast_kernel<false, false, false>), gf, dim3(LF::kThreads), LF::kLdsW * 4, stream, p, b,
-                           res, acc, slow_tiles, slow_count);
+        launch_variant<false, false, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
     return hipGetLastError();
 }
 #undef FQ_PREPARE

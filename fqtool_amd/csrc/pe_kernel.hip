@@ -188,6 +188,9 @@ __device__ inline void correct_pair(const Smem& sm, Row s1, Row q1, Row s2, Row 
     lds_add64(&sm.tail[FQ_ACC_TAIL_CORRECTED_BASES], (unsigned long long)corrected);
     if (c1) r1.flags |= FQ_RF_CORRECTED;
     if (c2) r2.flags |= FQ_RF_CORRECTED;
+    // (a signed 16-bit offset is exact: fq_engine_create caps max_cycles at 4096, and longer reads are
+    // refused per pack with FQ_E_TOO_LONG before any kernel sees them as in range)
+    static_assert(FQ_MAX_CYCLES_LIMIT <= 32767, "-c carries the overlap offset in 16 signed bits");
     r2.m_len1 = (uint16_t)(int16_t)ov.offset;
     r2.m_len2 = (uint16_t)ol;
     r2.reserved = (uint16_t)n2;

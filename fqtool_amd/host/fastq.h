@@ -233,6 +233,7 @@ struct Pack {
     bool use_flags = false;
     PodBuf<fq_read_result> res;  // engine records: n (SE) or 2n (PE)
     uint64_t seq_no = 0;
+    int max_cycles = 0;  // the engine parameters' max_cycles this pack was submitted with
 
     // -c: pairs whose bases the engine corrected read their seq/qual from a corrected copy
     // (fix[i] -> seq1 qual1 seq2 qual2 back to back; nullptr = the original text)

@@ -818,6 +818,7 @@ Options prepare_options(int argc, char** argv, bool detect_adapters) {
         o.est_reads_num = evaluate_read_num(o.in1);
         if (o.split_number == 0) throw std::runtime_error("--split_file_number must be given (non-zero) with -s");
         o.split_size = (size_t)std::max(o.est_reads_num / o.split_number, 1);
+        log("total reds: " + std::to_string(o.est_reads_num) + " split size: " + std::to_string(o.split_size));
     }
     if (o.split() && o.paired() && o.out2.empty())  // the reference dereferences a null split writer
         throw std::runtime_error("split output of paired-end reads needs both -o and -O");
@@ -919,7 +920,7 @@ int run_tool(int argc, char** argv) {
                 std::unique_ptr<Pack> pk;
                 while (done.pop(pk)) {
                     const auto f0 = std::chrono::steady_clock::now();
-                    const fq_params p = o.to_params(eng.max_cycles);
+                    const fq_params p = o.to_params(pk->max_cycles);
                     apply_corrections(o, *pk, pk->res.data(), &pool);
                     if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p, &pool);
                     outs.consume(*pk, pk->res.data());
@@ -972,6 +973,7 @@ int run_tool(int argc, char** argv) {
                 if ((int)inflight.size() >= G * depth) complete_oldest();
                 const int g = (int)(pk->seq_no % (uint64_t)G);
                 const fq_batch b = pk->batch();
+                pk->max_cycles = eng.max_cycles;  // (read by the formatter; eng.max_cycles may grow meanwhile)
                 const auto e0 = std::chrono::steady_clock::now();
                 if (fq_engine_submit(eng.e[(size_t)g], &b, pk->results(), pk->seq_no) != FQ_OK)
                     throw std::runtime_error(std::string("fq_engine_submit: ") + fq_engine_last_error(eng.e[(size_t)g]));
@@ -980,6 +982,8 @@ int run_tool(int argc, char** argv) {
             }
             while (!inflight.empty()) complete_oldest();
         } catch (...) {
+            // the packs in flight own pinned buffers the engines may still be copying into
+            for (fq_engine* x : eng.e) (void)fq_engine_sync(x);
             packs.close();
             spare.close();
             done.close();
@@ -1007,7 +1011,11 @@ int run_tool(int argc, char** argv) {
         if (det.valid()) {
             Detection d = det.get();
             set_reader_stderr_gate(std::shared_future<void>());
-            if (d.err) std::rethrow_exception(d.err);
+            if (d.err) {  // the reference fails before creating any output (src/main.cpp:137-141)
+                for (const std::string* f : {&o.out1, &o.out2, &o.unpaired1, &o.unpaired2, &o.failed_out, &o.merge_out})
+                    if (!f->empty() && *f != "/dev/null" && *f != "-" && *f != "/dev/stdout") std::remove(f->c_str());
+                std::rethrow_exception(d.err);
+            }
             o.detected_adapter1 = d.a1;
             o.detected_adapter2 = d.a2;
             detect_s = d.seconds;
