@@ -14,11 +14,19 @@
 
 #include "../../include/fqengine.h"
 
+// All the set's work runs on its own non-blocking stream, with buffers allocated once and kept
+// (hipFree synchronises the device, and the legacy default stream serialises with the engines'
+// streams: either would tie the pre-pass to the pipeline's kernels running beside it).
 struct fq_kmer_set {
     int device = 0;
     int32_t n = 0;
     uint8_t* seq = nullptr;
     uint32_t* off = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t* counts = nullptr;  // 4^keylen bins (grown on demand)
+    size_t counts_bins = 0;
+    unsigned long long* occ = nullptr;  // [count, occurrences...] (grown on demand)
+    size_t occ_cap = 0;
 };
 
 namespace {
@@ -78,13 +86,18 @@ int fq_kmer_open(int device, const uint8_t* seq, const uint32_t* off, int32_t n,
     s->device = device;
     s->n = n;
     const size_t bytes = n ? off[n] : 0;
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        fq_kmer_close(s);
+        return FQ_E_HIP;
+    }
     if (hipMalloc(&s->seq, bytes ? bytes : 1) != hipSuccess ||
         hipMalloc(&s->off, ((size_t)n + 1) * sizeof(uint32_t)) != hipSuccess) {
         fq_kmer_close(s);
         return FQ_E_NOMEM;
     }
-    if ((bytes && hipMemcpy(s->seq, seq, bytes, hipMemcpyHostToDevice) != hipSuccess) ||
-        (n && hipMemcpy(s->off, off, ((size_t)n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)) {
+    if ((bytes && hipMemcpyAsync(s->seq, seq, bytes, hipMemcpyHostToDevice, s->stream) != hipSuccess) ||
+        (n && hipMemcpyAsync(s->off, off, ((size_t)n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s->stream) != hipSuccess) ||
+        hipStreamSynchronize(s->stream) != hipSuccess) {
         fq_kmer_close(s);
         return FQ_E_HIP;
     }
@@ -95,8 +108,12 @@ int fq_kmer_open(int device, const uint8_t* seq, const uint32_t* off, int32_t n,
 int fq_kmer_close(fq_kmer_set* s) {
     if (!s) return FQ_OK;
     (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->seq) (void)hipFree(s->seq);
     if (s->off) (void)hipFree(s->off);
+    if (s->counts) (void)hipFree(s->counts);
+    if (s->occ) (void)hipFree(s->occ);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return FQ_OK;
 }
@@ -105,16 +122,21 @@ int fq_kmer_count(fq_kmer_set* s, int32_t keylen, int32_t first, int32_t shift_t
     if (!s || keylen < 1 || keylen > 12 || first < 0 || !counts) return FQ_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return FQ_E_HIP;
     const size_t bins = (size_t)1 << (2 * keylen);
-    uint32_t* d = nullptr;
-    if (hipMalloc(&d, bins * 4) != hipSuccess) return FQ_E_NOMEM;
-    hipError_t e = hipMemset(d, 0, bins * 4);
+    if (bins > s->counts_bins) {
+        if (s->counts) (void)hipFree(s->counts);
+        s->counts = nullptr;
+        s->counts_bins = 0;
+        if (hipMalloc(&s->counts, bins * 4) != hipSuccess) return FQ_E_NOMEM;
+        s->counts_bins = bins;
+    }
+    hipError_t e = hipMemsetAsync(s->counts, 0, bins * 4, s->stream);
     if (e == hipSuccess && s->n > 0) {
-        hipLaunchKernelGGL(kmer_count_kernel, dim3((s->n + 255) / 256), dim3(256), 0, 0, s->seq, s->off, s->n, keylen,
-                           first, shift_tail, d);
+        hipLaunchKernelGGL(kmer_count_kernel, dim3((s->n + 255) / 256), dim3(256), 0, s->stream, s->seq, s->off, s->n,
+                           keylen, first, shift_tail, s->counts);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpy(counts, d, bins * 4, hipMemcpyDeviceToHost);
-    (void)hipFree(d);
+    if (e == hipSuccess) e = hipMemcpyAsync(counts, s->counts, bins * 4, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     return e == hipSuccess ? FQ_OK : FQ_E_HIP;
 }
 
@@ -122,18 +144,27 @@ int fq_kmer_find(fq_kmer_set* s, int32_t keylen, int32_t first, int32_t shift_ta
                  size_t cap, size_t* n_out) {
     if (!s || keylen < 1 || keylen > 12 || first < 0 || !n_out || (cap && !occ)) return FQ_E_INVALID;
     if (hipSetDevice(s->device) != hipSuccess) return FQ_E_HIP;
-    unsigned long long* d = nullptr;
-    if (hipMalloc(&d, (cap + 1) * 8) != hipSuccess) return FQ_E_NOMEM;
-    hipError_t e = hipMemset(d, 0, 8);
+    if (cap + 1 > s->occ_cap) {
+        if (s->occ) (void)hipFree(s->occ);
+        s->occ = nullptr;
+        s->occ_cap = 0;
+        if (hipMalloc(&s->occ, (cap + 1) * 8) != hipSuccess) return FQ_E_NOMEM;
+        s->occ_cap = cap + 1;
+    }
+    unsigned long long* d = s->occ;
+    hipError_t e = hipMemsetAsync(d, 0, 8, s->stream);
     if (e == hipSuccess && s->n > 0) {
-        hipLaunchKernelGGL(kmer_find_kernel, dim3((s->n + 255) / 256), dim3(256), 0, 0, s->seq, s->off, s->n, keylen,
-                           first, shift_tail, seed, d + 1, (unsigned long long)cap, d);
+        hipLaunchKernelGGL(kmer_find_kernel, dim3((s->n + 255) / 256), dim3(256), 0, s->stream, s->seq, s->off, s->n,
+                           keylen, first, shift_tail, seed, d + 1, (unsigned long long)cap, d);
         e = hipGetLastError();
     }
     unsigned long long n = 0;
-    if (e == hipSuccess) e = hipMemcpy(&n, d, 8, hipMemcpyDeviceToHost);
-    if (e == hipSuccess && n && cap) e = hipMemcpy(occ, d + 1, (size_t)std::min<unsigned long long>(n, cap) * 8, hipMemcpyDeviceToHost);
-    (void)hipFree(d);
+    if (e == hipSuccess) e = hipMemcpyAsync(&n, d, 8, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess && n && cap) {
+        e = hipMemcpyAsync(occ, d + 1, (size_t)std::min<unsigned long long>(n, cap) * 8, hipMemcpyDeviceToHost, s->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    }
     *n_out = (size_t)n;
     return e == hipSuccess ? FQ_OK : FQ_E_HIP;
 }

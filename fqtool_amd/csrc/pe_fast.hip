@@ -224,6 +224,16 @@ struct Fwd {
     uint32_t c, n;
 };
 
+// field_window for callers whose positions below 0 (or past the column) are masked off anyway: the
+// words are read without the range checks (a word index below 0 reads word 0; past the column the
+// next field or the next wave's column, valid LDS), so only in-column positions are exact
+__device__ __forceinline__ uint32_t field_window_masked(const uint32_t* col, int f, int c, int pos) {
+    const int w = pos >> 4, sh = 2 * (pos & 15);
+    const uint32_t* p = col + (f + max(w, 0)) * 64 + c;
+    const uint32_t lo = p[0], hi = p[w >= 0 ? 64 : 0];
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+}
+
 // forward codes / N mask of positions [16F, 16F+16) of lane c's read.  Read 2 columns hold the
 // reverse complement of the whole 160-position row, so forward chunk F is stored word 9-F with
 // its fields reversed and complemented; positions >= L are garbage for the caller to mask.
@@ -490,7 +500,8 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, in
         int cum = 0;  // non-G bases before the current group
         for (int g = 0; 16 * g < n && iend == n; ++g) {
             const int pos0 = rc ? kMaxLen - 1 - e + 16 * g : e - 16 * g - 15;
-            const uint32_t cw = field_window(col, kFC, c, pos0), nw = field_window(col, kFN, c, pos0);
+            // (positions outside [st, e] are scan indices >= n, dropped by `valid`)
+            const uint32_t cw = field_window_masked(col, kFC, c, pos0), nw = field_window_masked(col, kFN, c, pos0);
             uint32_t x = fold2(cw ^ (rc ? 0x55555555u : 0xFFFFFFFFu)) | nw;  // non-G (N included), spaced
             if (!rc) x = __builtin_bitreverse32(x) >> 1;                        // forward window -> scan order
             const uint32_t valid = posmask(n - 16 * g);
@@ -535,7 +546,8 @@ __device__ inline bool polyx_no_trim(const uint32_t* col, int c, bool rc, int st
     if (maxMM < 1 || per < 1 || n <= 0) return false;
     const int e = st + n - 1;
     const int pos0 = rc ? kMaxLen - 1 - e : e - 15;
-    const uint32_t cw = field_window(col, kFC, c, pos0), nw = field_window(col, kFN, c, pos0);
+    // (positions outside the window are scan indices >= lim, dropped by `valid`)
+    const uint32_t cw = field_window_masked(col, kFC, c, pos0), nw = field_window_masked(col, kFN, c, pos0);
     const int lim = min(min(2 * per - 1, 16), n);  // scan indices [0, lim) are decided here
     const uint32_t valid = posmask(lim);
     int brk = 0;
@@ -883,6 +895,10 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         // ten addresses are not kept live across tiles)
         uint32_t* wp = col + lane_x + (rc ? (kChunks - 1) * 64 : 0);
         const int wstep = rc ? -64 : 64;
+        // read 2: v_perm selector reversing a dword pair's bytes (0x04050607: src0 reversed), and the
+        // complement mask of its codes
+        const uint32_t rsel = rc ? 0x04050607u : 0x03020100u;
+        const uint32_t rcx = rc ? 0xAAAAAAAAu : 0u;
         // Row chunks are requested kAhead ahead of their use (software pipelining: one HBM round
         // trip per tile instead of one per chunk); every row is readable up to its stride, so
         // the look-ahead loads are clamped, never guarded.  Only the chunks that some lane's read
@@ -936,17 +952,21 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                     constexpr bool FULL = decltype(full_c)::value;
                     if (LY::kQLds) qrow[4 * k + j] = qw[j];
                     const uint32_t bm = FULL ? 0xFFFFFFFFu : bytemask(Lk - 4 * j);
-                    const uint32_t kk = (sw[j] >> 1) & 0x07070707u;
+                    // read 2 (the column holds its reverse complement): the chunk's bytes reversed
+                    // (dword 3 - j byte-swapped, one v_perm), so its codes come out in column order
+                    const uint32_t sr = PAIRED ? __builtin_amdgcn_perm(sw[3 - j], sw[j], rsel) : sw[j];
+                    const uint32_t bms = FULL ? 0xFFFFFFFFu : rc ? ~bytemask(16 - Lk - 4 * j) : bm;
+                    const uint32_t kk = (sr >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
                     const uint32_t canon = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, kk);
                     // sum of |canon - byte| (one v_sad_u8): zero iff every byte is canonical, and
                     // at most 40 dwords x 4 x 255 per tile, so it never wraps
-                    exo = FULL ? __builtin_amdgcn_sad_u8(canon, sw[j], exo)
-                               : __builtin_amdgcn_sad_u8(canon & bm, sw[j] & bm, exo);
+                    exo = FULL ? __builtin_amdgcn_sad_u8(canon, sr, exo)
+                               : __builtin_amdgcn_sad_u8(canon & bms, sr & bms, exo);
                     const uint32_t qm = FULL ? qw[j] : (qw[j] & bm);
                     qhi |= qm;
                     q20 += __popc((qm + 0x4A4A4A4Au) & (0x80808080u & bm));  // q > '5'
-                    q30 += __popc((qm + 0x40404040u) & (0x80808080u & bm));  // q > '?'
+                    q30 += __popc(qm & 0x40404040u);  // q > '?' (= bit 6: q < 128 here; qm already masked)
                     lowf += __popc(~(qm + limq) & (0x80808080u & bm));        // q < limit
                     // whole-read quality total: only -e reads it (passFilter's mean quality),
                     // which runs on the XTRA instantiation (and the merge variant)
@@ -963,17 +983,21 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                     for (int j = 0; j < 4; ++j) dword(j, std::false_type{});
                 }
                 if (!LEAN) lowr |= (lr != 0 ? 1u : 0u) << k;
-                // N flags are kept only for positions inside the read (later passes rely on it)
-                const uint32_t fck = tr4x4(cc), fwk = tr4x4(nn4) & (full ? 0x55555555u : posmask(Lk));
+                // N flags are kept only for positions inside the read (later passes rely on it);
+                // read 2's chunk is reversed: its positions inside the read are the high ones
+                const uint32_t vmask = full ? 0x55555555u : rc ? 0x55555555u & ~posmask(16 - Lk) : posmask(Lk);
+                uint32_t fck = tr4x4(cc);
+                const uint32_t fwk = tr4x4(nn4) & vmask;
                 nbf += __popc(fwk);
                 // read 2: the column is the reverse complement of the 160-position row, so the
-                // read's rc position j sits at index j + (160 - L); garbage beyond L lands below
-                const uint32_t rn = pairrev(fwk);
+                // read's rc position j sits at index j + (160 - L); garbage beyond L lands below.
+                // Complement: code ^ 2 for A C G T, N stays code 3.
+                fck ^= rcx & ~(fwk << 1);
 #if FQ_ABLATE_STAGE == 2  // profiling only: no LDS column writes (results invalid)
-                tqf ^= (rc ? (pairrev(fck) ^ (0xAAAAAAAAu & ~(rn << 1))) : fck) ^ (rc ? rn : fwk);
+                tqf ^= fck ^ fwk;
 #else
-                wp[kFC * 64] = rc ? (pairrev(fck) ^ (0xAAAAAAAAu & ~(rn << 1))) : fck;
-                wp[kFN * 64] = rc ? rn : fwk;
+                wp[kFC * 64] = fck;
+                wp[kFN * 64] = fwk;
 #endif
                 wp += wstep;
             }
@@ -1317,7 +1341,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const uint32_t rf = (b1 + 0x04040404u * j) & ~(b2 + 0x04040404u * j) & 0x80808080u;
-                            const uint32_t w7 = wq[j] & 0x7F7F7F7Fu;
+                            // (no carry reaches an in-range byte: the bytes below a1 <= L are qualities < 128,
+                            // the only bytes >= 128 are row padding past L, whose carries run upward)
+                            const uint32_t w7 = wq[j];
                             low -= __popc(~(w7 + limq) & rf);
                             w20 -= __popc((w7 + 0x4A4A4A4Au) & rf);
                             w30 -= __popc((w7 + 0x40404040u) & rf);
@@ -1580,8 +1606,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
 #pragma unroll
             for (int i = 0; i < 5; ++i) qw5[i] = qword(wl0 - 4 * mate + i);
             for (int J = mate; 16 * J < m2; J += 2) {
-                const uint32_t cw = field_window(col, kFC, c2, ci0 + 16 * J);
-                const uint32_t nw = field_window(col, kFN, c2, ci0 + 16 * J);
+                // (ci0 >= 0; positions past the part are the dummy slot / masked by rem)
+                const uint32_t cw = field_window_masked(col, kFC, c2, ci0 + 16 * J);
+                const uint32_t nw = field_window_masked(col, kFN, c2, ci0 + 16 * J);
                 uint32_t qn[5];
 #pragma unroll
                 for (int i = 0; i < 5; ++i) qn[i] = qword(wl0 - 4 * (J + 2) + i);

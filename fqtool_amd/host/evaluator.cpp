@@ -6,6 +6,8 @@
 
 #include <fstream>
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <memory>
@@ -32,49 +34,54 @@ std::string int2seq(size_t val, int len) {
     return s;
 }
 
-// NucleotideTree, src/nucleotidetree.cpp:41-90
-struct Node {
-    int count = 0;
-    char base = 'N';
-    std::unique_ptr<Node> child[8];
+// NucleotideTree::getDominantPath over the trie of a set of sequences (src/nucleotidetree.cpp:41-90),
+// walked without building the trie: the path's node at depth d is reached by the sequences whose
+// first d characters fall in the path's buckets (c & 7, NucleotideTree::addSeq stops at 'N').  At
+// each node the children's counts are the next-character buckets of those sequences; the walk
+// goes on while they total >= 50 and one bucket holds >= 95 % of them, and the node's base is the
+// character of the first such sequence (in insertion order) that created it.  Each step keeps only
+// the sequences that follow the dominant bucket, so the work is the path length times the
+// surviving sequences, with no per-node allocation.
+struct Seqs {  // sequence i = base[i][0 .. len[i]) read forward (dir 1) or backward (dir -1)
+    std::vector<const char*> base;
+    std::vector<int> len;
+    int dir = 1;
+    char at(size_t i, int d) const { return dir > 0 ? base[i][d] : base[i][-d]; }
 };
 
-void add_seq(Node* root, const std::string& s) {
-    Node* cur = root;
-    for (char c : s) {
-        if (c == 'N') break;
-        const int b = c & 7;
-        if (!cur->child[b]) {
-            cur->child[b].reset(new Node());
-            cur->child[b]->base = c;
-        }
-        cur->child[b]->count++;
-        cur = cur->child[b].get();
-    }
-}
-
-std::string dominant_path(Node* root, bool& reached_leaf) {
+std::string dominant_path(const Seqs& S, bool& reached_leaf) {
     std::string out;
-    Node* cur = root;
-    for (;;) {
+    std::vector<uint32_t> live(S.base.size()), next;
+    for (size_t i = 0; i < live.size(); ++i) live[i] = (uint32_t)i;
+    for (int d = 0;; ++d) {
+        int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        char first[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int total = 0;
-        for (int i = 0; i < 8; ++i)
-            if (cur->child[i]) total += cur->child[i]->count;
+        for (uint32_t i : live) {
+            if (d >= S.len[i]) continue;
+            const char c = S.at(i, d);
+            if (c == 'N') continue;  // (addSeq stops at an uppercase N)
+            const int b = c & 7;
+            if (!cnt[b]) first[b] = c;
+            ++cnt[b];
+            ++total;
+        }
         if (total < 50) break;
-        bool dom = false;
-        for (int i = 0; i < 8; ++i) {
-            if (!cur->child[i]) continue;
-            if (cur->child[i]->count / (double)total >= 0.95) {
-                dom = true;
-                out += cur->child[i]->base;
-                cur = cur->child[i].get();
+        int dom = -1;
+        for (int b = 0; b < 8; ++b)
+            if (cnt[b] && cnt[b] / (double)total >= 0.95) {
+                dom = b;
                 break;
             }
-        }
-        if (!dom) {
+        if (dom < 0) {
             reached_leaf = false;
             break;
         }
+        out += first[dom];
+        next.clear();
+        for (uint32_t i : live)
+            if (d < S.len[i] && S.at(i, d) != 'N' && (S.at(i, d) & 7) == dom) next.push_back(i);
+        live.swap(next);
     }
     return out;
 }
@@ -117,24 +124,32 @@ fqh_kmer_backend g_kmer = kGpuKmer;
 // the k-mer backend; the prefix trees do not depend on their order
 std::string adapter_with_seed(int seed, const ReadSet& reads, void* kset, uint32_t seed_count, int keylen, int trim) {
     const int shift_tail = std::max(1, trim);
-    Node fwd, bwd;
     std::vector<uint64_t> occ(seed_count);
     size_t n = 0;
     if (g_kmer.find(kset, keylen, 20, shift_tail, (uint32_t)seed, occ.data(), occ.size(), &n) != FQ_OK)
         throw std::runtime_error("adapter detection: k-mer search failed");
-    for (size_t k = 0; k < std::min(n, occ.size()); ++k) {
+    n = std::min(n, occ.size());
+    // the forward tree gets the read after the seed (minus the tail), the backward tree the read
+    // before it, reversed (src/evaluator.cpp:405-414)
+    Seqs fwd, bwd;
+    fwd.base.reserve(n);
+    fwd.len.reserve(n);
+    bwd.base.reserve(n);
+    bwd.len.reserve(n);
+    bwd.dir = -1;
+    for (size_t k = 0; k < n; ++k) {
         const size_t r = (size_t)(occ[k] >> 32);
         const int pos = (int)(uint32_t)occ[k];
         const char* s = reads.seq.data() + reads.off[r];
         const int len = (int)(reads.off[r + 1] - reads.off[r]);
-        add_seq(&fwd, std::string(s + pos + keylen, (size_t)(len - keylen - shift_tail - pos)));
-        std::string head(s, (size_t)pos);
-        std::reverse(head.begin(), head.end());
-        add_seq(&bwd, head);
+        fwd.base.push_back(s + pos + keylen);
+        fwd.len.push_back(len - keylen - shift_tail - pos);
+        bwd.base.push_back(s + pos - 1);
+        bwd.len.push_back(pos);
     }
     bool reached_leaf = true;
-    const std::string f = dominant_path(&fwd, reached_leaf);
-    std::string b = dominant_path(&bwd, reached_leaf);
+    const std::string f = dominant_path(fwd, reached_leaf);
+    std::string b = dominant_path(bwd, reached_leaf);
     std::reverse(b.begin(), b.end());
     std::string adapter = b + int2seq((size_t)seed, keylen) + f;
     if (adapter.size() > 60) adapter.resize(60);
@@ -185,6 +200,23 @@ int evaluate_read_num(const std::string& path) {  // Evaluator::evaluateReadNum,
 // Evaluator::evaluateAdapterSeq, src/evaluator.cpp:229-390
 std::string detect_adapter(const std::string& path, int trim_tail1, std::string* msgs, int device) {
     const size_t kReadLimit = 256 * 1024, kBaseLimit = 151 * kReadLimit;
+    // FQH_DETECT_TIMING=1: stage times on stderr (profiling aid, tools/detect_timing.py)
+    static const bool timing = std::getenv("FQH_DETECT_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    std::string stages;
+    auto stage = [&](const char* name) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        stages += std::string(" ") + name + " " + std::to_string(std::chrono::duration<double>(now - t_last).count());
+        t_last = now;
+    };
+    struct Report {
+        const std::string& s;
+        const std::string& path;
+        ~Report() {
+            if (timing) std::cerr << "adapter detection " << path << ":" << s << std::endl;
+        }
+    } report{stages, path};
     FqReader r(path, false);
     ReadSet reads;
     size_t bases = 0;
@@ -203,6 +235,7 @@ std::string detect_adapter(const std::string& path, int trim_tail1, std::string*
         reads.seq.append(text.data() + rec.seq_off(), rec.len);
         reads.off.push_back((uint32_t)reads.seq.size());
     }
+    stage("read");
     if (reads.size() < 10000) return "";
     const int shift_tail = std::max(1, trim_tail1);
     const int keylen = 10;
@@ -216,9 +249,11 @@ std::string detect_adapter(const std::string& path, int trim_tail1, std::string*
         void* h;
         ~Closer() { g_kmer.close(h); }
     } closer{kset};
+    stage("open");
     std::vector<uint32_t> counts(size, 0);
     if (g_kmer.count(kset, keylen, 20, shift_tail, counts.data()) != FQ_OK)
         throw std::runtime_error("adapter detection: k-mer count failed");
+    stage("count");
     counts[0] = 0;
     const int topnum = 10;
     int top[topnum] = {0};
@@ -247,6 +282,7 @@ std::string detect_adapter(const std::string& path, int trim_tail1, std::string*
             }
         }
     }
+    stage("top10");
     for (int t = 0; t < topnum; ++t) {
         const int key = top[t];
         if (key == 0) continue;
@@ -257,6 +293,7 @@ std::string detect_adapter(const std::string& path, int trim_tail1, std::string*
         for (size_t i = 0; i + 1 < sq.size(); ++i) diff += sq[i] != sq[i + 1];
         if (diff < 3) continue;
         const std::string est = adapter_with_seed(key, reads, kset, counts[(size_t)key], keylen, trim_tail1);
+        stage("seed");
         if (!est.empty()) return est;
     }
     return "";
