@@ -1,6 +1,7 @@
 # Top-level build (no cmake needed).  `make -j8` builds:
 #   fqtool_amd/lib/libfqengine.so  -- C-ABI engine: HIP kernels for gfx950 (include/fqengine.h)
 #   oracle/build/liboracle.so      -- CPU restatement (test infrastructure only)
+.DEFAULT_GOAL := all
 HIPCC      ?= /opt/rocm/bin/hipcc
 ARCH       ?= gfx950
 HIPFLAGS   ?= -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
@@ -28,7 +29,7 @@ CSRC       := fqtool_amd/csrc
 LIBDIR     := fqtool_amd/lib
 OBJDIR     := build/obj
 
-ENGINE_SRCS := $(CSRC)/engine.hip $(CSRC)/pe_kernel.hip $(CSRC)/pe_fast.hip $(CSRC)/pe_fast_long.hip $(CSRC)/synth.hip $(CSRC)/dup.hip $(CSRC)/kmer.hip
+ENGINE_SRCS := $(CSRC)/engine.hip $(CSRC)/pe_kernel.hip $(CSRC)/pe_fast.hip $(CSRC)/pe_fast_long.hip $(CSRC)/synth.hip $(CSRC)/dup.hip $(CSRC)/kmer.hip $(CSRC)/text.hip
 ENGINE_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(ENGINE_SRCS))
 ENGINE_HDRS := include/fqengine.h $(CSRC)/engine_internal.h $(CSRC)/device_ops.h
 $(OBJDIR)/pe_fast_long.o: $(CSRC)/pe_fast.hip

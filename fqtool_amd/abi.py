@@ -9,6 +9,7 @@ import os
 
 FQ_MAX_ADAPTER = 128
 FQ_OK = 0
+FQ_E_INVALID = -1
 
 FQ_ACC_FILTER = 0
 FQ_ACC_ADAPTER_READS = 32
@@ -87,6 +88,25 @@ class FqBatch(ctypes.Structure):
         ("seq2", ctypes.c_void_p), ("qual2", ctypes.c_void_p), ("len2", ctypes.c_void_p),
         ("flags", ctypes.c_void_p),
     ]
+
+
+class FqTextRec(ctypes.Structure):  # fq_text_rec (include/fqengine.h), 24 bytes
+    _fields_ = [("name_off", ctypes.c_uint32), ("seq_off", ctypes.c_uint32), ("strand_off", ctypes.c_uint32),
+                ("qual_off", ctypes.c_uint32), ("name_len", ctypes.c_uint16), ("strand_len", ctypes.c_uint16),
+                ("len", ctypes.c_uint16), ("pad", ctypes.c_uint16)]
+
+
+TEXT_REC_DTYPE = [("name_off", "<u4"), ("seq_off", "<u4"), ("strand_off", "<u4"), ("qual_off", "<u4"),
+                  ("name_len", "<u2"), ("strand_len", "<u2"), ("len", "<u2"), ("pad", "<u2")]
+
+
+class FqTextBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("stride", ctypes.c_int32), ("text", ctypes.c_void_p * 2),
+                ("text_bytes", ctypes.c_uint64 * 2), ("rec", ctypes.c_void_p * 2)]
+
+
+class FqTextOut(ctypes.Structure):
+    _fields_ = [("text", ctypes.c_void_p * 2), ("bytes", ctypes.c_uint64 * 2)]
 
 
 # Batch planes hold rows in chunk-interleaved tiles (include/fqengine.h): byte j of read i at
@@ -217,6 +237,7 @@ def load_engine(path=ENGINE_LIB):
     lib.fq_engine_last_kernel_ms.argtypes = [vp]
     lib.fq_engine_last_kernel_ms.restype = ctypes.c_double
     lib.fq_engine_submit.argtypes = [vp, ctypes.POINTER(FqBatch), vp, u64]
+    lib.fq_engine_submit_text.argtypes = [vp, ctypes.POINTER(FqTextBatch), vp, ctypes.POINTER(FqTextOut), u64]
     lib.fq_engine_poll.argtypes = [vp, ctypes.c_int, ctypes.POINTER(u64)]
     lib.fq_engine_pending.argtypes = [vp]
     lib.fq_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
@@ -238,7 +259,7 @@ ENGINE_SYMBOLS = [
     "fq_engine_create", "fq_engine_destroy", "fq_engine_process", "fq_engine_process_device",
     "fq_engine_acc_words", "fq_engine_acc_device_ptr", "fq_engine_read_acc", "fq_engine_reset_acc",
     "fq_engine_sync", "fq_engine_set_acc_buffer", "fq_engine_last_error", "fq_engine_device_info", "fq_synth_fill_device",
-    "fq_engine_last_kernel_ms", "fq_engine_submit", "fq_engine_poll", "fq_engine_pending", "fq_host_alloc",
+    "fq_engine_last_kernel_ms", "fq_engine_submit", "fq_engine_submit_text", "fq_engine_poll", "fq_engine_pending", "fq_host_alloc",
     "fq_host_free", "fq_dup_create", "fq_dup_destroy", "fq_dup_reset", "fq_engine_set_dup", "fq_dup_merge",
     "fq_dup_stat", "fq_kmer_open", "fq_kmer_close", "fq_kmer_count", "fq_kmer_find",
 ]

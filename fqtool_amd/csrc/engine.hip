@@ -28,6 +28,19 @@ struct Slot {
     fq_read_result* d_res = nullptr;
     Scratch scratch;
     hipEvent_t ev_in = nullptr, ev_kern = nullptr, ev_done = nullptr;
+    // FASTQ-text packs (fq_engine_submit_text): per mate text, records, output text, sizes, offsets
+    char* d_text[2] = {nullptr, nullptr};
+    char* d_out[2] = {nullptr, nullptr};
+    size_t text_cap[2] = {0, 0};
+    fq_text_rec* d_trec[2] = {nullptr, nullptr};
+    uint32_t* d_tsize[2] = {nullptr, nullptr};
+    uint32_t* d_toff[2] = {nullptr, nullptr};
+    size_t trec_cap = 0;
+    void* d_scan = nullptr;
+    size_t scan_bytes = 0;
+    unsigned long long* d_total = nullptr;  // [2]
+    unsigned long long* h_total = nullptr;  // pinned [2]
+    fq_text_out* text_out = nullptr;        // the pending text pack's output descriptor
     int* d_err = nullptr;  // this pack's device error word (cleared at submit, set by its kernels)
     int* h_err = nullptr;  // pinned: d_err as of this pack's kernels
     bool busy = false;      // events recorded and not yet waited for
@@ -123,6 +136,16 @@ static void free_slot(Slot& s) {
     if (s.d_lens) (void)hipFree(s.d_lens);
     if (s.d_flags) (void)hipFree(s.d_flags);
     if (s.d_res) (void)hipFree(s.d_res);
+    for (int m = 0; m < 2; ++m) {
+        if (s.d_text[m]) (void)hipFree(s.d_text[m]);
+        if (s.d_out[m]) (void)hipFree(s.d_out[m]);
+        if (s.d_trec[m]) (void)hipFree(s.d_trec[m]);
+        if (s.d_tsize[m]) (void)hipFree(s.d_tsize[m]);
+        if (s.d_toff[m]) (void)hipFree(s.d_toff[m]);
+    }
+    if (s.d_scan) (void)hipFree(s.d_scan);
+    if (s.d_total) (void)hipFree(s.d_total);
+    if (s.h_total) (void)hipHostFree(s.h_total);
     if (s.d_err) (void)hipFree(s.d_err);
     if (s.h_err) (void)hipHostFree(s.h_err);
     if (s.ev_in) (void)hipEventDestroy(s.ev_in);
@@ -285,6 +308,57 @@ static int retire_slot(fq_engine* e, int k) {
             q.done = true;
             q.err = *s.h_err;
         }
+    if (s.text_out) {  // a text pack: its output sizes are in now
+        s.text_out->bytes[0] = s.h_total[0];
+        s.text_out->bytes[1] = s.h_total[1];
+        s.text_out = nullptr;
+    }
+    return FQ_OK;
+}
+
+// a text pack's output is at most its input plus the final line terminator an input may lack
+static const size_t kTextSlack = 16;
+
+// device buffers of a text pack (grown on demand; growing frees the old ones, which waits for the
+// device, so steady-state packs of similar size reuse them)
+static int ensure_text(fq_engine* e, Slot& s, const fq_text_batch* tb) {
+    const bool pe = e->p.paired;
+    for (int m = 0; m < (pe ? 2 : 1); ++m) {
+        const size_t need = tb->text_bytes[m] + kTextSlack;
+        if (need > s.text_cap[m]) {
+            if (s.d_text[m]) (void)hipFree(s.d_text[m]);
+            if (s.d_out[m]) (void)hipFree(s.d_out[m]);
+            s.d_text[m] = s.d_out[m] = nullptr;
+            s.text_cap[m] = 0;
+            const size_t cap = need + need / 8;
+            HIP_TRY(e, hipMalloc(&s.d_text[m], cap));
+            HIP_TRY(e, hipMalloc(&s.d_out[m], cap));
+            s.text_cap[m] = cap;
+        }
+    }
+    if ((size_t)tb->n > s.trec_cap || !s.d_total) {
+        const size_t cap = (size_t)tb->n + (size_t)tb->n / 8 + 1;
+        for (int m = 0; m < 2; ++m) {
+            if (s.d_trec[m]) (void)hipFree(s.d_trec[m]);
+            if (s.d_tsize[m]) (void)hipFree(s.d_tsize[m]);
+            if (s.d_toff[m]) (void)hipFree(s.d_toff[m]);
+            s.d_trec[m] = nullptr;
+            s.d_tsize[m] = s.d_toff[m] = nullptr;
+        }
+        if (s.d_scan) (void)hipFree(s.d_scan);
+        s.d_scan = nullptr;
+        s.trec_cap = 0;
+        for (int m = 0; m < 2; ++m) {
+            HIP_TRY(e, hipMalloc(&s.d_trec[m], cap * sizeof(fq_text_rec)));
+            HIP_TRY(e, hipMalloc(&s.d_tsize[m], cap * sizeof(uint32_t)));
+            HIP_TRY(e, hipMalloc(&s.d_toff[m], cap * sizeof(uint32_t)));
+        }
+        s.scan_bytes = fq_text_scan_temp_bytes((int)cap);
+        HIP_TRY(e, hipMalloc(&s.d_scan, s.scan_bytes ? s.scan_bytes : 1));
+        if (!s.d_total) HIP_TRY(e, hipMalloc(&s.d_total, 2 * sizeof(unsigned long long)));
+        if (!s.h_total) HIP_TRY(e, hipHostMalloc((void**)&s.h_total, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+        s.trec_cap = cap;
+    }
     return FQ_OK;
 }
 
@@ -357,6 +431,80 @@ int fq_engine_submit(fq_engine* e, const fq_batch* hb, fq_read_result* results, 
     HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
     HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
     s.busy = true;
+    e->pending.push_back(Pending{seq_no, k, false, 0});
+    return FQ_OK;
+}
+
+int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result* results, fq_text_out* out,
+                          uint64_t seq_no) {
+    if (!e || !tb || !results || !out) return FQ_E_INVALID;
+    const bool pe = e->p.paired;
+    if (tb->n < 0 || tb->n > e->max_batch || tb->stride <= 0 || tb->stride > e->max_stride || (tb->stride & 15))
+        return fail(e, FQ_E_INVALID, "text pack exceeds the engine's max_batch/max_stride (or stride % 16 != 0)");
+    if (e->p.merge_enabled || e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0)
+        return fail(e, FQ_E_INVALID, "text packs take no -m, -c or UMI options");
+    for (int m = 0; m < (pe ? 2 : 1); ++m)
+        if (tb->n > 0 && (!tb->text[m] || !tb->rec[m] || !out->text[m]))
+            return fail(e, FQ_E_INVALID, "missing text pack arrays");
+    out->bytes[0] = out->bytes[1] = 0;
+    if (tb->n == 0) {
+        e->pending.push_back(Pending{seq_no, -1, true, 0});
+        return FQ_OK;
+    }
+    HIP_TRY(e, hipSetDevice(e->device));
+    int k = 0;
+    for (auto it = e->pending.rbegin(); it != e->pending.rend(); ++it)
+        if (it->slot >= 0) {
+            k = (it->slot + 1) % kSlots;
+            break;
+        }
+    int rc = retire_slot(e, k);
+    if (rc != FQ_OK) return rc;
+    Slot& s = e->slots[k];
+    if ((rc = alloc_slot(e, s)) != FQ_OK) return rc;
+    if ((rc = ensure_text(e, s, tb)) != FQ_OK) return rc;
+    const size_t plane = fq_batch_bytes(e->max_batch, e->max_stride);
+    fq_batch db{};
+    db.n = tb->n;
+    db.stride = tb->stride;
+    db.seq1 = s.d_rows;
+    db.qual1 = s.d_rows + plane;
+    db.len1 = s.d_lens;
+    db.seq2 = pe ? s.d_rows + 2 * plane : nullptr;
+    db.qual2 = pe ? s.d_rows + 3 * plane : nullptr;
+    db.len2 = pe ? s.d_lens + e->max_batch : nullptr;
+    // H2D of the text spans and records on the copy-in stream
+    for (int m = 0; m < (pe ? 2 : 1); ++m) {
+        HIP_TRY(e, hipMemcpyAsync(s.d_text[m], tb->text[m], tb->text_bytes[m], hipMemcpyHostToDevice, e->s_in));
+        HIP_TRY(e, hipMemcpyAsync(s.d_trec[m], tb->rec[m], (size_t)tb->n * sizeof(fq_text_rec), hipMemcpyHostToDevice,
+                                  e->s_in));
+    }
+    HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
+    HIP_TRY(e, hipStreamWaitEvent(e->stream, s.ev_in, 0));
+    // planes from the text, the pack's kernels, then the output text
+    for (int m = 0; m < (pe ? 2 : 1); ++m)
+        HIP_TRY(e, fq_launch_text_tiles(s.d_text[m], s.d_trec[m], tb->n, tb->stride, const_cast<uint8_t*>(m ? db.seq2 : db.seq1),
+                                        const_cast<uint8_t*>(m ? db.qual2 : db.qual1), const_cast<uint16_t*>(m ? db.len2 : db.len1),
+                                        e->stream));
+    HIP_TRY(e, hipMemsetAsync(s.d_err, 0, sizeof(int), e->stream));
+    if ((rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false, seq_no, s.d_err)) != FQ_OK) return rc;
+    for (int m = 0; m < (pe ? 2 : 1); ++m)
+        HIP_TRY(e, fq_launch_text_out(s.d_text[m], s.d_trec[m], s.d_res, tb->n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
+                                      s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, e->stream));
+    if (!pe) HIP_TRY(e, hipMemsetAsync(s.d_total + 1, 0, sizeof(unsigned long long), e->stream));
+    HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
+    // D2H: records, output sizes and text (the text up to its input span: an upper bound of the
+    // output, no device-to-host round trip for the exact size), the error word
+    HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
+    const size_t nres = (size_t)tb->n * (pe ? 2 : 1);
+    HIP_TRY(e, hipMemcpyAsync(results, s.d_res, nres * sizeof(fq_read_result), hipMemcpyDeviceToHost, e->s_out));
+    HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
+    for (int m = 0; m < (pe ? 2 : 1); ++m)
+        HIP_TRY(e, hipMemcpyAsync(out->text[m], s.d_out[m], tb->text_bytes[m] + kTextSlack, hipMemcpyDeviceToHost, e->s_out));
+    HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
+    HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
+    s.busy = true;
+    s.text_out = out;
     e->pending.push_back(Pending{seq_no, k, false, 0});
     return FQ_OK;
 }

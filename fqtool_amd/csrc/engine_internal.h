@@ -35,3 +35,10 @@ hipError_t fq_launch_synth(const fq_batch& b, uint64_t seed, uint64_t first_inde
 int fq_dup_pack(fq_dup* d, const fq_batch& b, int paired, unsigned long long order_base, hipStream_t s);
 const char* fq_dup_error(const fq_dup* d);
 int fq_dup_device(const fq_dup* d, int* device);
+// FASTQ-text packs (text.hip): tile planes built from the text; output text of the passing records
+hipError_t fq_launch_text_tiles(const char* d_text, const fq_text_rec* d_rec, int n, int stride, uint8_t* seq,
+                                uint8_t* qual, uint16_t* lens, hipStream_t s);
+size_t fq_text_scan_temp_bytes(int n);
+hipError_t fq_launch_text_out(const char* d_text, const fq_text_rec* d_rec, const fq_read_result* d_res, int n, int paired,
+                              int m, uint32_t* d_size, uint32_t* d_off, void* d_temp, size_t temp_bytes, char* d_out,
+                              unsigned long long* d_total, hipStream_t s);

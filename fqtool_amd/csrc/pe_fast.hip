@@ -114,7 +114,7 @@ static_assert(kMaxLen % 32 == 0 && kMaxLen <= 320, "reads per column: a multiple
 constexpr int kOvBlocks = kMaxLen / 32;           // 32-offset blocks of the overlap candidate scan
 constexpr int kChunks = kMaxLen / 16;             // 16-position chunks per read
 constexpr int kFC = 0;                            // column fields (words): 2-bit codes,
-constexpr int kFN = kChunks;                      //   spaced N mask,
+constexpr int kFN = kChunks;                      //   spaced N mask (+ lowercase flags at the odd bits),
 constexpr int kCodeW = 2 * kChunks * 64;          // code + N columns of a wave
 constexpr int kQS = kMaxLen / 4 + 1;              // quality row stride (odd: conflict-free per lane)
 // Stats histograms: u64 cells [cycle / 16][slot][cycle % 16], slots A C T G N + one dummy slot
@@ -251,7 +251,7 @@ __device__ __forceinline__ Fwd fwd_chunk(const uint32_t* col, int c, int F, bool
     return Fwd{cw, nw};
 }
 
-struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N)
+struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G T N a c g t)
     const uint32_t* col;
     int c;
     bool rc;
@@ -259,9 +259,10 @@ struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G 
         const int q = rc ? kMaxLen - 1 - i : i;
         const int w = q >> 4, sh = 2 * (q & 15);
         uint32_t code = (col[(kFC + w) * 64 + c] >> sh) & 3u;
-        const uint32_t nb = (col[(kFN + w) * 64 + c] >> sh) & 1u;
+        const uint32_t nx = col[(kFN + w) * 64 + c] >> sh;  // bit 0: N, bit 1: lowercase
         code ^= rc ? 2u : 0u;
-        return nb ? (uint8_t)'N' : (uint8_t)(0x47544341u >> (8 * code));  // "ACTG"
+        // "ACTG", lowercase with the flag (its code is its uppercase letter's, never N)
+        return (nx & 1u) ? (uint8_t)'N' : (uint8_t)(((0x47544341u >> (8 * code)) & 0xFFu) | ((nx & 2u) << 4));
     }
 };
 
@@ -292,7 +293,9 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
         const uint32_t b1 = B[64 * (j + 1)], bn1 = B[64 * (j + 1) + kN];
         const uint32_t a = __builtin_amdgcn_alignbit(a1, a0, s1), wa = __builtin_amdgcn_alignbit(an1, an0, s1);
         const uint32_t b = __builtin_amdgcn_alignbit(b1, b0, s2), wb = __builtin_amdgcn_alignbit(bn1, bn0, s2);
-        uint32_t mism = (fold2(a ^ b) & ~(wa | wb)) | (wa ^ wb);
+        // (a lowercase base of read 1 -- odd flag bit of wa -- differs from every base of the
+        // reverse complement, which is upper case; read 2's lowercase flags do not count)
+        uint32_t mism = ((fold2(a ^ b) & ~(wa | wb)) | (wa ^ wb) | (wa >> 1)) & 0x55555555u;
         if (j == nw - 1) mism &= last;
         // mismatches within the first 50 positions: words 0-2 whole, word 3's positions 48, 49
         if (j == 3) d50 = D + __popc(mism & 5u);
@@ -502,7 +505,8 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, in
             const int pos0 = rc ? kMaxLen - 1 - e + 16 * g : e - 16 * g - 15;
             // (positions outside [st, e] are scan indices >= n, dropped by `valid`)
             const uint32_t cw = field_window_masked(col, kFC, c, pos0), nw = field_window_masked(col, kFN, c, pos0);
-            uint32_t x = fold2(cw ^ (rc ? 0x55555555u : 0xFFFFFFFFu)) | nw;  // non-G (N included), spaced
+            // non-G (N and lowercase included; odd bits dropped by `valid`), spaced
+            uint32_t x = fold2(cw ^ (rc ? 0x55555555u : 0xFFFFFFFFu)) | nw | (nw >> 1);
             if (!rc) x = __builtin_bitreverse32(x) >> 1;                        // forward window -> scan order
             const uint32_t valid = posmask(n - 16 * g);
             x &= valid;
@@ -558,9 +562,9 @@ __device__ inline bool polyx_no_trim(const uint32_t* col, int c, bool rc, int st
         uint32_t nonb;  // forward-order spaced mask of the positions that are not b
         if (b < 4) {
             const uint32_t code = (uint32_t)((0x3120 >> (4 * b)) & 3) ^ (rc ? 2u : 0u);
-            nonb = (fold2(cw ^ (code * 0x55555555u)) | nw) & 0x55555555u;
-        } else {
-            nonb = ~nw & 0x55555555u;
+            nonb = (fold2(cw ^ (code * 0x55555555u)) | nw | (nw >> 1)) & 0x55555555u;
+        } else {  // class 4: N and every other byte (lowercase included), src/polyx.cpp:56-70
+            nonb = ~(nw | (nw >> 1)) & 0x55555555u;
         }
         if (!rc) nonb = __builtin_bitreverse32(nonb) >> 1;  // forward window -> scan order
         nonb &= valid;
@@ -631,6 +635,40 @@ __device__ inline bool cut_right_w4(const fq_params& p, const uint8_t* Q, int nc
     out_start = front;
     out_len = min(rlen, l - front);
     return true;
+}
+
+// (rare) the lowercase flags of one lane's read: re-reads its row chunks, ORs a flag at the odd bit
+// of the N word for each lowercase a c g t (the uppercase letter | 0x20, whose 3-bit key and code
+// are the uppercase letter's) and returns true when the read holds any other byte outside ACGTN.
+// xp: the lane's column word of row chunk 0 (read 2: its reverse complement, stepped by wstep).
+template <bool PAIRED>
+__device__ __attribute__((noinline)) bool lower_flags(const uint8_t* S, uint32_t* xp, int wstep, int nch, int L, bool rc,
+                                                     uint32_t rsel) {
+    constexpr int cst = FQ_TILE_READS * FQ_CHUNK;
+    bool hard = false;
+    for (int k = 0; k < nch; ++k, xp += wstep) {
+        const uint4 s4 = *reinterpret_cast<const uint4*>(S + cst * k);
+        const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
+        const int Lk = L - 16 * k;
+        uint32_t x4 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t sr = PAIRED ? __builtin_amdgcn_perm(sw[3 - j], sw[j], rsel) : sw[j];
+            const uint32_t bms = rc ? ~bytemask(16 - Lk - 4 * j) : bytemask(Lk - 4 * j);
+            const uint32_t kk = (sr >> 1) & 0x07070707u;
+            const uint32_t canon = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, kk);
+            const uint32_t d = (sr ^ canon) & bms;  // per byte: 0 canonical, 0x20 lowercase
+            const uint32_t t = d ^ 0x20202020u;
+            const uint32_t low = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & ~((kk & 0x04040404u) << 5) &
+                                 0x80808080u;  // d == 0x20 and not 'n' (whose key is N's)
+            const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
+            hard |= (nz & ~low) != 0u;
+            x4 |= (low >> 7) << (2 * j);
+        }
+        const uint32_t vm = rc ? 0x55555555u & ~posmask(16 - Lk) : posmask(Lk);
+        xp[kFN * 64] |= (tr4x4(x4) & vm) << 1;
+    }
+    return hard;
 }
 
 __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
@@ -1002,9 +1040,29 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 wp += wstep;
             }
         }
+        // Lowercase a c g t (the uppercase letter | 0x20: the same 3-bit key, so the same code) stay
+        // on this kernel with a flag at the odd bit of the N word, for the steps that compare bytes:
+        // read 1 against the reverse complement (which upper-cases them, src/seq.h:24-48), polyG,
+        // polyX, adapter sequences, the complexity filter.  The Stats bucket byte & 7 is the
+        // uppercase letter's (src/stats.cpp:249) and passFilter counts only 'N' (src/filter.cpp:18),
+        // so those passes need nothing.  Any other byte outside ACGTN hands the pair over.  Rare: only
+        // lanes holding such a byte re-read their row (from L2) here.
+        bool hard = false, xl = false;
+        if (__any(exo != 0)) {
+            if (exo != 0) {
+                hard = lower_flags<PAIRED>(S, col + lane_x + (rc ? (kChunks - 1) * 64 : 0), wstep, nch, L, rc, rsel);
+                // (-c rewrites bases across the pair: its pairs with lowercase go over)
+                if (XTRA && p.correction_enabled) hard = true;
+                xl = !hard;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const bool tile_x = __any(xl);  // some kept lane carries lowercase flags
         // (index filter: a pair the host dropped counts only in the pre-filter Stats,
         // src/peprocessor.cpp:283-286 -- rare, so it goes over too)
-        const bool bad = odd || exo != 0 || (qhi & 0x80808080u) != 0 ||
+        const bool bad = odd || hard || (qhi & 0x80808080u) != 0 ||
                          (b.flags && valid && (b.flags[idx] & FQ_BF_INDEX_FILTERED));
         for (int k = nch; k < kChunks; ++k) {  // unused tail of the row
             wp[kFC * 64] = 0u;
@@ -1012,7 +1070,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             wp += wstep;
         }
         // Pairs (single-end: reads) this kernel cannot take -- a read longer than the columns or
-        // max_cycles, a byte outside ACGTN, a quality >= 128, an index-filtered pair -- are
+        // max_cycles, a byte outside ACGTN and acgt, a quality >= 128, an index-filtered pair -- are
         // handed to the general kernel one by one (item list: pair / read indices); the rest of
         // the tile stays here, the handed-over lanes continuing as empty lanes (valid false,
         // length 0).
@@ -1457,6 +1515,13 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         }
 
         FQ_STAMP(5)
+        if (tile_x) {  // (rare) the lowercase flags have served: the Stats passes read spaced N masks
+            if (xl)
+                for (int c = 0; c < kChunks; ++c) col[(kFN + c) * 64 + lane_x] &= 0x55555555u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         // ---------------- Stats::statRead, pre and post (src/peprocessor.cpp:276-277,400-401) ----
         if (valid && !(abl & 4) && removed_mode) {
             // Every kept window is a prefix [0, wlen): each base goes to exactly one cell, kept or

@@ -245,8 +245,10 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     if (!fp_) throw std::runtime_error("Failed to open file: " + path);
     struct stat st;
     if (fp_ != stdin && fstat(fileno(fp_), &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
-        // a regular file is mapped (private, so phred64 conversion writes stay in this process)
-        void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ | PROT_WRITE, MAP_PRIVATE, fileno(fp_), 0);
+        // a regular file is mapped (private, so phred64 conversion writes stay in this process).
+        // Read-only unless phred64 rewrites it: the engine's text packs are copied to the GPU
+        // straight from the mapping, and pinning writable private pages would copy them first.
+        void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ | (phred64 ? PROT_WRITE : 0), MAP_PRIVATE, fileno(fp_), 0);
         if (m != MAP_FAILED) {
             madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
             map_ = static_cast<char*>(m);
@@ -695,7 +697,69 @@ fq_batch Pack::batch() const {
     return b;
 }
 
+bool pack_text(Pack& pk, Pool* pool) {
+    const int mates = pk.paired ? 2 : 1;
+    const size_t n = (size_t)pk.n;
+    std::atomic<bool> ok{true};
+    for (int m = 0; m < mates; ++m) {
+        const std::vector<Rec>& R = pk.rec[m];
+        pk.span[m] = pk.arena(m);
+        pk.span_bytes[m] = 0;
+        pk.max_len[m] = 0;
+        if (!n) continue;
+        const uint64_t a = R[0].off, b = R[n - 1].qual_off() + R[n - 1].len;
+        if (b - a > 0xFFFFFFFFull) return false;
+        pk.span[m] = pk.arena(m) + a;
+        pk.span_bytes[m] = b - a;
+        pk.trec[m].resize(n);
+        pk.out_text[m].resize_uninit(b - a + 16);  // (fq_text_out: + the final terminator an input may lack)
+    }
+    for (int m = mates; m < 2; ++m) {
+        pk.span[m] = nullptr;
+        pk.span_bytes[m] = 0;
+        pk.max_len[m] = 0;
+    }
+    const int parts = pool ? std::max(1, std::min(pool->size() * 2, (int)((n + 16383) / 16384))) : 1;
+    std::vector<int> mx((size_t)parts * 2, 0);
+    auto work = [&](int k) {
+        const size_t i0 = n * (size_t)k / (size_t)parts, i1 = n * (size_t)(k + 1) / (size_t)parts;
+        for (int m = 0; m < mates; ++m) {
+            const std::vector<Rec>& R = pk.rec[m];
+            const uint64_t a = R[0].off;
+            fq_text_rec* T = pk.trec[m].data();
+            int mxl = 0;
+            for (size_t i = i0; i < i1; ++i) {
+                const Rec& r = R[i];
+                if (r.len > 65535 || r.name_len > 65535 || r.strand_len > 65535) {
+                    ok = false;
+                    return;
+                }
+                T[i] = fq_text_rec{(uint32_t)(r.off - a), (uint32_t)(r.seq_off() - a), (uint32_t)(r.strand_off() - a),
+                                   (uint32_t)(r.qual_off() - a), (uint16_t)r.name_len, (uint16_t)r.strand_len,
+                                   (uint16_t)r.len, 0};
+                mxl = std::max(mxl, (int)r.len);
+            }
+            mx[(size_t)(2 * k + m)] = mxl;
+        }
+    };
+    if (pool && parts > 1) pool->run(parts, work);
+    else if (n) work(0);
+    if (!ok) return false;
+    int maxlen = 0;
+    for (int k = 0; k < parts; ++k)
+        for (int m = 0; m < mates; ++m) {
+            pk.max_len[m] = std::max(pk.max_len[m], mx[(size_t)(2 * k + m)]);
+            maxlen = std::max(maxlen, mx[(size_t)(2 * k + m)]);
+        }
+    pk.stride = std::max(16, (maxlen + 15) & ~15);
+    for (int m = 0; m < 2; ++m) pk.tout.text[m] = m < mates && n ? pk.out_text[m].data() : nullptr;
+    pk.tout.bytes[0] = pk.tout.bytes[1] = 0;
+    pk.text_mode = true;
+    return true;
+}
+
 void pack_tiles(Pack& pk, Pool* pool) {
+    pk.text_mode = false;
     const int mates = pk.paired ? 2 : 1;
     size_t maxlen = 0;
     for (int m = 0; m < mates; ++m) {
@@ -881,6 +945,19 @@ void Writer::close() {
         throw;
     }
     if (std::fclose(fp) != 0) throw std::runtime_error(std::string("closing output failed: ") + std::strerror(errno));
+}
+
+void Writer::write_raw(const char* p, size_t n, Pool* pool) {
+    if (!fp_) throw std::runtime_error("write to a closed output");
+    if (!n) return;
+    if (!gzip_) {
+        if (std::fwrite(p, 1, n, fp_) != n) throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
+        return;
+    }
+    const size_t blk = (size_t)4 << 20;  // (one gzip member per block; the decompressed bytes are the text)
+    std::vector<std::string> blocks;
+    for (size_t o = 0; o < n; o += blk) blocks.emplace_back(p + o, std::min(blk, n - o));
+    write(blocks, pool);
 }
 
 void Writer::write(const std::vector<std::string>& blocks, Pool* pool) {

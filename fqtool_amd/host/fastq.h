@@ -220,7 +220,9 @@ struct Pack {
           qual{ByteBuf(pinned), ByteBuf(pinned)},
           len{PodBuf<uint16_t>(pinned), PodBuf<uint16_t>(pinned)},
           flags(pinned),
-          res(pinned) {}
+          res(pinned),
+          trec{PodBuf<fq_text_rec>(pinned), PodBuf<fq_text_rec>(pinned)},
+          out_text{ByteBuf(pinned), ByteBuf(pinned)} {}
     int n = 0;
     int stride = 0;
     bool paired = false;
@@ -234,6 +236,16 @@ struct Pack {
     PodBuf<fq_read_result> res;  // engine records: n (SE) or 2n (PE)
     uint64_t seq_no = 0;
     int max_cycles = 0;  // the engine parameters' max_cycles this pack was submitted with
+
+    // FASTQ-text pack (fq_engine_submit_text, pack_text): each mate's text span (inside its arena or
+    // the file mapping), the per-record index into it, and the output text the engine writes back
+    bool text_mode = false;
+    const char* span[2] = {nullptr, nullptr};
+    uint64_t span_bytes[2] = {0, 0};
+    PodBuf<fq_text_rec> trec[2];
+    ByteBuf out_text[2];
+    fq_text_out tout{};
+    int max_len[2] = {0, 0};
 
     // -c: pairs whose bases the engine corrected read their seq/qual from a corrected copy
     // (fix[i] -> seq1 qual1 seq2 qual2 back to back; nullptr = the original text)
@@ -262,6 +274,12 @@ struct Pack {
 // Fills the pack's lengths, stride and tile planes from its record text (pool-parallel over
 // whole tiles when a pool is given).  Throws on reads longer than 65535 bases.
 void pack_tiles(Pack& pk, Pool* pool);
+
+// The FASTQ-text form of a pack (fq_engine_submit_text): each mate's span of text, one
+// fq_text_rec per record, the planes' stride and the output buffers; no planes are built on the
+// host.  False (the pack then goes through pack_tiles) when a span exceeds 4 GiB or a line 65535
+// bytes.
+bool pack_text(Pack& pk, Pool* pool);
 
 // Reads up to max_n records (pairs) into a pack and builds its planes.  Two-file PE input is
 // parsed by two threads, one per mate, with the reference's stop rule and messages (the pair
@@ -297,6 +315,8 @@ class Writer {
     Writer& operator=(const Writer&) = delete;
     void write(const std::vector<std::string>& blocks, Pool* pool = nullptr);
     void write(const std::string& s) { write(std::vector<std::string>{s}); }
+    // n bytes from p as they are (gzip: in blocks compressed in parallel on the pool)
+    void write_raw(const char* p, size_t n, Pool* pool = nullptr);
     void close();  // flushes; throws on a short write or a failed close (full disk)
 
    private:

@@ -5,6 +5,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <fstream>
@@ -369,12 +370,13 @@ template <class T>
 class Queue {  // bounded FIFO between pipeline threads; push/pop return at once after close()
    public:
     explicit Queue(size_t cap) : cap_(cap) {}
-    void push(T v) {
+    bool push(T v) {  // false: the queue was closed and v dropped
         std::unique_lock<std::mutex> l(m_);
         not_full_.wait(l, [&] { return q_.size() < cap_ || closed_; });
-        if (closed_) return;
+        if (closed_) return false;
         q_.push_back(std::move(v));
         not_empty_.notify_one();
+        return true;
     }
     bool pop(T& v) {
         std::unique_lock<std::mutex> l(m_);
@@ -418,7 +420,16 @@ class AsyncWriter {
         if (err_) std::rethrow_exception(err_);
         bool any = false;
         for (const auto& s : blocks) any = any || !s.empty();
-        if (any) q_.push(std::move(blocks));
+        if (any) q_.push(Job{std::move(blocks), nullptr, 0, nullptr});
+    }
+    // queue n bytes at p (which stay valid until `done` runs); the writer thread runs it once the
+    // bytes are written (or dropped after a write error)
+    void write_raw(const char* p, size_t n, std::function<void()> done) {
+        if (err_ || !q_.push(Job{{}, p, n, done})) {
+            done();  // (the writer has stopped: nothing will take the text)
+            if (err_) std::rethrow_exception(err_);
+            throw std::runtime_error("write to a closed output");
+        }
     }
     void close() {
         if (closed_) return;
@@ -436,18 +447,38 @@ class AsyncWriter {
     }
 
    private:
+    struct Job {
+        std::vector<std::string> blocks;
+        const char* raw;
+        size_t raw_n;
+        std::function<void()> done;
+    };
     void loop() {
-        std::vector<std::string> b;
+        Job j;
         try {
-            while (q_.pop(b)) w_.write(b, pool_);
+            while (q_.pop(j)) {
+                if (j.done) {
+                    try {
+                        w_.write_raw(j.raw, j.raw_n, pool_);
+                    } catch (...) {
+                        j.done();
+                        throw;
+                    }
+                    j.done();
+                } else {
+                    w_.write(j.blocks, pool_);
+                }
+            }
         } catch (...) {
             err_ = std::current_exception();
             q_.close();  // the producer's next push returns at once; write() rethrows
+            while (q_.pop(j))  // (raw jobs queued behind the failure are released)
+                if (j.done) j.done();
         }
     }
     Writer w_;
     Pool* pool_;
-    Queue<std::vector<std::string>> q_;
+    Queue<Job> q_;
     std::exception_ptr err_;
     bool closed_ = false;
     std::thread t_;
@@ -483,6 +514,32 @@ void OutputSet::write(PackOutput&& out) {
     }
     if (wu1_) wu1_->write(std::move(out.unpaired1));
     if (wu2_) wu2_->write(std::move(out.unpaired2));
+}
+
+void OutputSet::write_text(const char* t1, size_t n1, const char* t2, size_t n2, std::function<void()> done) {
+    if (!(w1_ && (!paired_ || w2_))) {  // PE writes the pair outputs only with both writers (:469)
+        done();
+        return;
+    }
+    // `done` runs once, when the last writer is through with its text
+    auto left = std::make_shared<std::atomic<int>>(w2_ ? 2 : 1);
+    auto fin = [left, done] {
+        if (left->fetch_sub(1) == 1) done();
+    };
+    std::exception_ptr err;
+    try {
+        w1_->write_raw(t1, n1, fin);
+    } catch (...) {
+        err = std::current_exception();
+    }
+    if (w2_) {
+        try {
+            w2_->write_raw(t2, n2, fin);
+        } catch (...) {
+            if (!err) err = std::current_exception();
+        }
+    }
+    if (err) std::rethrow_exception(err);
 }
 
 void OutputSet::close() {
@@ -686,6 +743,11 @@ void Sink::consume(const Pack& pk, const fq_read_result* res) {
     pairs_ += (uint64_t)pk.n;
 }
 
+void Sink::consume_text(const Pack& pk, std::function<void()> done) {
+    pairs_ += (uint64_t)pk.n;
+    outs_->write_text(pk.out_text[0].data(), pk.tout.bytes[0], pk.out_text[1].data(), pk.tout.bytes[1], std::move(done));
+}
+
 void Sink::close() {
     if (split_) split_->close();
     if (outs_) outs_->close();
@@ -695,71 +757,143 @@ void Sink::close() {
 
 namespace {
 
-// One engine per entry of --devices (several may share a GPU).  All have the same geometry;
-// a pack with longer reads (or more of them) re-creates them larger after draining them.
-struct Engines {
-    std::vector<int> devices;
-    std::vector<fq_engine*> e;
-    std::vector<fq_dup*> dup;  // -d: one table per engine slot, kept across re-creation
-    int max_cycles = 0, max_batch = 0, max_stride = 0;
-    ~Engines() {
-        destroy();
-        for (fq_dup* d : dup) fq_dup_destroy(d);
-    }
-    void destroy() {
-        for (fq_engine* x : e) fq_engine_destroy(x);
-        e.clear();
-    }
-};
-
 int round16(int x) { return (x + 15) & ~15; }
 
-void make_engines(Engines& en, const Options& o, int max_cycles, int max_batch, int max_stride) {
-    en.destroy();
-    fq_params p = o.to_params(max_cycles);
-    for (int dev : en.devices) {
-        fq_engine* x = nullptr;
-        const int rc = fq_engine_create(&p, dev, max_batch, max_stride, &x);
-        if (rc != FQ_OK)
-            throw std::runtime_error("fq_engine_create (device " + std::to_string(dev) + "): " + fq_engine_last_error(nullptr));
-        en.e.push_back(x);
-        if (o.dup) {
-            const size_t g = en.e.size() - 1;
-            if (en.dup.size() <= g) {
-                fq_dup* d = nullptr;
-                if (fq_dup_create(dev, o.dup_keylen, &d) != FQ_OK)
-                    throw std::runtime_error("fq_dup_create (device " + std::to_string(dev) + ") failed");
-                en.dup.push_back(d);
-            }
-            if (fq_engine_set_dup(x, en.dup[g]) != FQ_OK)
-                throw std::runtime_error(std::string("fq_engine_set_dup: ") + fq_engine_last_error(x));
-        }
-    }
-    en.max_cycles = max_cycles;
-    en.max_batch = max_batch;
-    en.max_stride = max_stride;
+double since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
 }
 
-// the engines' accumulators summed into the host's (RCCL-free: they are in this process)
-void drain(Engines& en, HostAcc& acc) {
-    for (fq_engine* x : en.e) {
-        std::vector<uint64_t> buf(fq_engine_acc_words(x));
-        if (fq_engine_read_acc(x, buf.data(), buf.size()) != FQ_OK)
-            throw std::runtime_error(std::string("fq_engine_read_acc: ") + fq_engine_last_error(x));
-        acc.add(buf.data(), en.max_cycles);
-        fq_engine_reset_acc(x);
+struct Stopped {};  // another pipeline stage failed and closed the queues
+
+// One engine per entry of --devices (several may share a GPU), each fed by its own dispatcher
+// thread: pack k goes to engine k mod G.  A pack with longer reads (or more of them) re-creates
+// that engine larger after draining it.
+struct Lane {
+    Lane(int device, int depth_) : dev(device), depth(depth_), in(2), out((size_t)depth_ + 2) {}
+    ~Lane() {
+        if (t.joinable()) t.join();
+        if (e) fq_engine_destroy(e);
+        if (dup) fq_dup_destroy(dup);
     }
-}
+    int dev, depth;
+    fq_engine* e = nullptr;
+    fq_dup* dup = nullptr;  // -d: this engine's table, kept across re-creation
+    int max_cycles = 0, max_batch = 0, max_stride = 0;
+    Queue<std::unique_ptr<Pack>> in, out;
+    std::deque<std::unique_ptr<Pack>> inflight;  // submission order == input order
+    std::thread t;
+    std::exception_ptr err;
+    double tiles_s = 0, submit_s = 0, wait_s = 0;
+
+    void make(const Options& o, int cycles, int batch, int stride) {
+        if (e) fq_engine_destroy(e);
+        e = nullptr;
+        fq_params p = o.to_params(cycles);
+        if (fq_engine_create(&p, dev, batch, stride, &e) != FQ_OK)
+            throw std::runtime_error("fq_engine_create (device " + std::to_string(dev) + "): " + fq_engine_last_error(nullptr));
+        if (o.dup) {
+            if (!dup && fq_dup_create(dev, o.dup_keylen, &dup) != FQ_OK)
+                throw std::runtime_error("fq_dup_create (device " + std::to_string(dev) + ") failed");
+            if (fq_engine_set_dup(e, dup) != FQ_OK)
+                throw std::runtime_error(std::string("fq_engine_set_dup: ") + fq_engine_last_error(e));
+        }
+        max_cycles = cycles;
+        max_batch = batch;
+        max_stride = stride;
+    }
+
+    // the engine's accumulators summed into the host's (RCCL-free: they are in this process)
+    void drain(HostAcc& acc) {
+        std::vector<uint64_t> buf(fq_engine_acc_words(e));
+        if (fq_engine_read_acc(e, buf.data(), buf.size()) != FQ_OK)
+            throw std::runtime_error(std::string("fq_engine_read_acc: ") + fq_engine_last_error(e));
+        acc.add(buf.data(), max_cycles);
+        fq_engine_reset_acc(e);
+    }
+
+    void complete_oldest() {
+        std::unique_ptr<Pack> pk = std::move(inflight.front());
+        inflight.pop_front();
+        uint64_t seq = 0;
+        const auto e0 = std::chrono::steady_clock::now();
+        const int rc = fq_engine_poll(e, 1, &seq);
+        wait_s += since(e0);
+        if (rc != 1) throw std::runtime_error(std::string("fq_engine_poll: ") + fq_engine_last_error(e));
+        if (seq != pk->seq_no) throw std::runtime_error("engine completed packs out of order");
+        if (!out.push(std::move(pk))) throw Stopped();
+    }
+
+    void submit(Pack& pk, bool as_text) {
+        const auto e0 = std::chrono::steady_clock::now();
+        if (as_text) {
+            fq_text_batch tb{};
+            tb.n = pk.n;
+            tb.stride = pk.stride;
+            for (int m = 0; m < (pk.paired ? 2 : 1); ++m) {
+                tb.text[m] = pk.span[m];
+                tb.text_bytes[m] = pk.span_bytes[m];
+                tb.rec[m] = pk.trec[m].data();
+            }
+            if (fq_engine_submit_text(e, &tb, pk.results(), &pk.tout, pk.seq_no) != FQ_OK)
+                throw std::runtime_error(std::string("fq_engine_submit_text: ") + fq_engine_last_error(e));
+        } else {
+            const fq_batch b = pk.batch();
+            if (fq_engine_submit(e, &b, pk.results(), pk.seq_no) != FQ_OK)
+                throw std::runtime_error(std::string("fq_engine_submit: ") + fq_engine_last_error(e));
+        }
+        submit_s += since(e0);
+    }
+
+    // the dispatcher: planes (or the text index) of each pack, submit, completions in order
+    void run(const Options& o, bool text_mode, Pool& pool, HostAcc& acc, std::mutex& acc_m) {
+        try {
+            std::unique_ptr<Pack> pk;
+            while (in.pop(pk)) {
+                const auto p0 = std::chrono::steady_clock::now();
+                const bool as_text = text_mode && pack_text(*pk, &pool);
+                if (!as_text) {
+                    pack_tiles(*pk, &pool);
+                    prepare_pack(o, *pk, &pool);
+                }
+                tiles_s += since(p0);
+                int max1 = 0, max2 = 0;
+                if (as_text) {
+                    max1 = pk->max_len[0];
+                    max2 = pk->max_len[1];
+                } else {
+                    for (uint16_t l : pk->len[0]) max1 = std::max(max1, (int)l);
+                    if (pk->paired)
+                        for (uint16_t l : pk->len[1]) max2 = std::max(max2, (int)l);
+                }
+                const int need = o.merge ? max1 + max2 : std::max(max1, max2);
+                if (need > max_cycles || pk->stride > max_stride || pk->n > max_batch) {
+                    while (!inflight.empty()) complete_oldest();
+                    {  // keep what the old engine accumulated, then grow it
+                        std::lock_guard<std::mutex> g(acc_m);
+                        drain(acc);
+                    }
+                    make(o, std::max(max_cycles, round16(need)), std::max(max_batch, pk->n), std::max(max_stride, pk->stride));
+                }
+                if ((int)inflight.size() >= depth) complete_oldest();
+                pk->max_cycles = max_cycles;  // (read by the formatter)
+                submit(*pk, as_text);
+                inflight.push_back(std::move(pk));
+            }
+            while (!inflight.empty()) complete_oldest();
+        } catch (...) {
+            // the packs in flight own pinned buffers the engine may still be copying into
+            (void)fq_engine_sync(e);
+            inflight.clear();
+            throw;
+        }
+    }
+};
 
 void log(const std::string& s) {
     std::time_t t = std::time(nullptr);
     char d[64];
     std::strftime(d, sizeof d, "[%Y-%m-%d %H:%M:%S] ", std::localtime(&t));
     std::cerr << d << s << std::endl;
-}
-
-double since(std::chrono::steady_clock::time_point t) {
-    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
 }
 
 }  // namespace
@@ -876,25 +1010,48 @@ int run_tool(int argc, char** argv) {
         const bool paired = o.paired();
         const size_t pack_n = o.pack_pairs ? o.pack_pairs : std::max<size_t>(o.max_reads_in_pack, 262144);
         int est = std::max(o.est_seq_len1, paired ? o.est_seq_len2 : 0);
-        Engines eng;
-        eng.devices = o.device_list();
-        const int G = (int)eng.devices.size();
+        const std::vector<int> devices = o.device_list();
+        const int G = (int)devices.size();
         const int depth = G > 2 ? 2 : 3;  // packs in flight per engine (each holds a device slot)
-        make_engines(eng, o, std::max(16, round16(o.merge ? 2 * est : est)), (int)pack_n, round16(std::max(est, 16)));
         // -w host threads (the reference's worker count) pack tiles, format and compress
         Pool pool(std::max(0, o.threads - 1));
-        Sink outs(o, &pool);
-        // reader thread -> dispatcher (this thread: submit to engine seq_no mod G, poll in
-        // submission order) -> formatter thread (records -> output text, in input order) ->
-        // writer threads.  Packs (pinned planes and records) are recycled.
-        const int n_packs = G * depth + 4;
-        Queue<std::unique_ptr<Pack>> packs(2), done(2), spare((size_t)n_packs);
+        // (before the outputs: their writer threads hand text packs back to it until they close)
+        const int n_packs = G * (depth + 1) + 4;
+        Queue<std::unique_ptr<Pack>> spare((size_t)n_packs);
         for (int i = 0; i < n_packs; ++i) spare.push(std::unique_ptr<Pack>(new Pack(true)));
+        Sink outs(o, &pool);
+        // reader thread -> one dispatcher thread per engine (pack g of every G: planes or text
+        // index, submit, poll in submission order) -> formatter thread (takes pack k from engine
+        // k mod G: records -> output text, in input order) -> writer threads.  Packs (pinned
+        // planes and records) are recycled.  (src/peprocessor.cpp:99-247: producer, -w workers,
+        // writer threads.)
+        // GPU-side ingest and egress (fq_engine_submit_text): the engine builds the planes from
+        // the FASTQ text and writes the output text, for the plain out1 (+ out2) case
+        const char* tm_env = std::getenv("FQ_TEXT_MODE");
+        const bool text_mode = !(tm_env && std::string(tm_env) == "0") && !o.merge && !o.correction && !o.umi &&
+                               !o.index_filter && !o.split() && !o.phred64 && o.failed_out.empty() &&
+                               o.unpaired1.empty() && o.unpaired2.empty() && !o.out1.empty() &&
+                               (!paired || !o.out2.empty());
+        std::vector<std::unique_ptr<Lane>> lanes;
+        const int cyc0 = std::max(16, round16(o.merge ? 2 * est : est)), stride0 = round16(std::max(est, 16));
+        for (int g = 0; g < G; ++g) {
+            lanes.emplace_back(new Lane(devices[(size_t)g], depth));
+            lanes.back()->make(o, cyc0, (int)pack_n, stride0);
+        }
         std::exception_ptr reader_err, format_err;
-        double parse_s = 0, tiles_s = 0, spare_wait_s = 0;
+        double parse_s = 0, spare_wait_s = 0;
+        HostAcc acc(o.insert_size_max);
+        std::mutex acc_m;  // engines re-created larger mid-run add their accumulators here
+        auto stop_all = [&] {
+            spare.close();
+            for (auto& l : lanes) {
+                l->in.close();
+                l->out.close();
+            }
+        };
         // (owned here, not by the reader thread: packs in flight point into its file mappings)
         PackReader pr(o.in1, o.in2, o.interleaved, o.phred64);
-        pr.defer_tiles = true;  // the dispatcher fills the planes while the reader parses on
+        pr.defer_tiles = true;  // the dispatchers fill the planes while the reader parses on
         std::thread reader([&] {
             try {
                 std::unique_ptr<Pack> pk;
@@ -903,106 +1060,81 @@ int run_tool(int argc, char** argv) {
                     if (!spare.pop(pk)) break;
                     spare_wait_s += since(w0);
                     if (!pr.next(*pk, pack_n, &pool)) break;
-                    packs.push(std::move(pk));
+                    Lane& l = *lanes[(size_t)(pk->seq_no % (uint64_t)G)];
+                    if (!l.in.push(std::move(pk))) break;
                 }
                 parse_s = pr.parse_s;
             } catch (...) {
                 reader_err = std::current_exception();
             }
-            packs.close();
+            for (auto& l : lanes) l->in.close();
         });
-        HostAcc acc(o.insert_size_max);
+        for (auto& lp : lanes) {
+            Lane* l = lp.get();
+            l->t = std::thread([&, l] {
+                try {
+                    l->run(o, text_mode, pool, acc, acc_m);
+                } catch (const Stopped&) {  // (the stage that failed reports)
+                } catch (...) {
+                    l->err = std::current_exception();
+                    stop_all();
+                }
+                l->out.close();
+            });
+        }
         AdapterCounts ac;
         uint64_t reads = 0;
-        double engine_s = 0, format_s = 0;
+        double format_s = 0;
         std::thread formatter([&] {
             try {
                 std::unique_ptr<Pack> pk;
-                while (done.pop(pk)) {
+                for (uint64_t k = 0; lanes[(size_t)(k % (uint64_t)G)]->out.pop(pk); ++k) {
                     const auto f0 = std::chrono::steady_clock::now();
+                    if (pk->seq_no != k) throw std::runtime_error("packs reached the formatter out of order");
                     const fq_params p = o.to_params(pk->max_cycles);
-                    apply_corrections(o, *pk, pk->res.data(), &pool);
-                    if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p, &pool);
-                    outs.consume(*pk, pk->res.data());
+                    if (pk->text_mode) {  // the engine wrote the output text
+                        if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p, &pool);
+                        format_s += since(f0);
+                        reads += (uint64_t)pk->n * (paired ? 2 : 1);
+                        // the writers recycle the pack once its output text is written
+                        Pack* raw = pk.release();
+                        outs.consume_text(*raw, [raw, &spare] { spare.push(std::unique_ptr<Pack>(raw)); });
+                        continue;
+                    } else {
+                        apply_corrections(o, *pk, pk->res.data(), &pool);
+                        if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p, &pool);
+                        outs.consume(*pk, pk->res.data());
+                    }
                     format_s += since(f0);
                     reads += (uint64_t)pk->n * (paired ? 2 : 1);
                     spare.push(std::move(pk));
                 }
             } catch (...) {
                 format_err = std::current_exception();
-                done.close();
-                spare.close();
-                packs.close();
+                stop_all();
             }
         });
-        struct InFlight {
-            std::unique_ptr<Pack> pk;
-            int g;
-        };
-        std::deque<InFlight> inflight;  // submission order == input order
-        auto complete_oldest = [&] {
-            InFlight f = std::move(inflight.front());
-            inflight.pop_front();
-            uint64_t seq = 0;
-            const auto e0 = std::chrono::steady_clock::now();
-            const int rc = fq_engine_poll(eng.e[(size_t)f.g], 1, &seq);
-            engine_s += since(e0);
-            if (rc != 1)
-                throw std::runtime_error(std::string("fq_engine_poll: ") + fq_engine_last_error(eng.e[(size_t)f.g]));
-            if (seq != f.pk->seq_no) throw std::runtime_error("engine completed packs out of order");
-            done.push(std::move(f.pk));
-        };
-        try {
-            std::unique_ptr<Pack> pk;
-            while (packs.pop(pk)) {
-                const auto p0 = std::chrono::steady_clock::now();
-                pack_tiles(*pk, &pool);
-                prepare_pack(o, *pk, &pool);
-                tiles_s += since(p0);
-                int max1 = 0, max2 = 0;
-                for (uint16_t l : pk->len[0]) max1 = std::max(max1, (int)l);
-                if (paired)
-                    for (uint16_t l : pk->len[1]) max2 = std::max(max2, (int)l);
-                const int need = o.merge ? max1 + max2 : std::max(max1, max2);
-                if (need > eng.max_cycles || pk->stride > eng.max_stride || pk->n > eng.max_batch) {
-                    while (!inflight.empty()) complete_oldest();
-                    drain(eng, acc);  // keep what the old engines accumulated, then grow them
-                    make_engines(eng, o, std::max(eng.max_cycles, round16(need)), std::max(eng.max_batch, pk->n),
-                                 std::max(eng.max_stride, pk->stride));
-                }
-                if ((int)inflight.size() >= G * depth) complete_oldest();
-                const int g = (int)(pk->seq_no % (uint64_t)G);
-                const fq_batch b = pk->batch();
-                pk->max_cycles = eng.max_cycles;  // (read by the formatter; eng.max_cycles may grow meanwhile)
-                const auto e0 = std::chrono::steady_clock::now();
-                if (fq_engine_submit(eng.e[(size_t)g], &b, pk->results(), pk->seq_no) != FQ_OK)
-                    throw std::runtime_error(std::string("fq_engine_submit: ") + fq_engine_last_error(eng.e[(size_t)g]));
-                engine_s += since(e0);
-                inflight.push_back(InFlight{std::move(pk), g});
-            }
-            while (!inflight.empty()) complete_oldest();
-        } catch (...) {
-            // the packs in flight own pinned buffers the engines may still be copying into
-            for (fq_engine* x : eng.e) (void)fq_engine_sync(x);
-            packs.close();
-            spare.close();
-            done.close();
-            reader.join();
-            formatter.join();
-            throw;
-        }
-        done.close();
+        for (auto& l : lanes) l->t.join();
         formatter.join();
         reader.join();
+        double tiles_s = 0, submit_s = 0, wait_s = 0;
+        std::exception_ptr lane_err;
+        for (auto& l : lanes) {
+            tiles_s += l->tiles_s;
+            submit_s += l->submit_s;
+            wait_s += l->wait_s;
+            if (l->err && !lane_err) lane_err = l->err;
+        }
         if (format_err) std::rethrow_exception(format_err);
+        if (lane_err) std::rethrow_exception(lane_err);
         if (reader_err) std::rethrow_exception(reader_err);
-        drain(eng, acc);
+        for (auto& l : lanes) l->drain(acc);
         if (o.dup) {  // Duplicate::statAll over the merged tables, src/peprocessor.cpp:200-207
-            for (size_t g = 1; g < eng.dup.size(); ++g)
-                if (fq_dup_merge(eng.dup[0], eng.dup[g]) != FQ_OK) throw std::runtime_error("fq_dup_merge failed");
+            for (size_t g = 1; g < lanes.size(); ++g)
+                if (fq_dup_merge(lanes[0]->dup, lanes[g]->dup) != FQ_OK) throw std::runtime_error("fq_dup_merge failed");
             std::vector<uint64_t> hist((size_t)o.dup_hist_size), gcs((size_t)o.dup_hist_size);
             uint64_t tot[2] = {0, 0};
-            if (fq_dup_stat(eng.dup[0], o.dup_hist_size, hist.data(), gcs.data(), tot) != FQ_OK)
+            if (fq_dup_stat(lanes[0]->dup, o.dup_hist_size, hist.data(), gcs.data(), tot) != FQ_OK)
                 throw std::runtime_error("fq_dup_stat failed");
             acc.set_dup(hist, gcs, tot[0], tot[1]);
         }
@@ -1029,8 +1161,9 @@ int run_tool(int argc, char** argv) {
             std::ofstream hs(o.html_file, std::ios::binary);
             hs << build_html(o, acc, ac, html_time_now());
         }
-        log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s), wall " +
-            std::to_string(since(t0)) + " s, engine submit/wait " + std::to_string(engine_s) + " s; pre-pass " +
+        log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s)" +
+            (text_mode ? " (text packs: GPU ingest/egress)" : "") + ", wall " +
+            std::to_string(since(t0)) + " s, engine submit " + std::to_string(submit_s) + " s, wait " + std::to_string(wait_s) + " s; pre-pass " +
             std::to_string(prepass_s) + " s, adapter detection (concurrent) " + std::to_string(detect_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +
             " s, tiles " + std::to_string(tiles_s) + " s, reader waiting " + std::to_string(spare_wait_s) +
             " s; JSON report " + o.json_file + ", HTML report " + o.html_file);

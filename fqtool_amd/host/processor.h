@@ -9,6 +9,7 @@
 #pragma once
 
 #include <memory>
+#include <functional>
 #include <string>
 
 #include "fastq.h"
@@ -33,6 +34,9 @@ class OutputSet {
     explicit OutputSet(const Options& o, Pool* pool = nullptr);  // pool: gzip compression
     ~OutputSet();
     void write(PackOutput&& out);
+    // out1 / out2 text as is (waits until both writers have taken it)
+    // queue engine-assembled output text of both mates; `done` runs once both are written
+    void write_text(const char* t1, size_t n1, const char* t2, size_t n2, std::function<void()> done);
     void close();  // flushes and closes every file
 
    private:
@@ -56,6 +60,9 @@ class Sink {
     Sink(const Options& o, Pool* pool);
     ~Sink();
     void consume(const Pack& pk, const fq_read_result* res);  // format + write one processed pack
+    // write a text pack's engine-assembled output (no split); `done` runs (on a writer thread) once
+    // the pack's text is written
+    void consume_text(const Pack& pk, std::function<void()> done);
     void close();
 
    private:

@@ -347,6 +347,41 @@ int fq_engine_submit(fq_engine* e, const fq_batch* host_batch, fq_read_result* r
 int fq_engine_poll(fq_engine* e, int wait, uint64_t* seq_no);
 int fq_engine_pending(const fq_engine* e); /* packs submitted and not yet reported */
 
+/* ---- FASTQ-text packs: GPU-side ingest and egress ------------------------------------------
+ * Replaces the host's tile packing and output formatting (Read::toString + the writers' input,
+ * src/read.h:166-168, src/peprocessor.cpp:457-491, src/seprocessor.cpp:337-350) for the plain
+ * output case: the pack's records go over as the bytes of the input FASTQ (a span of the mapped
+ * file or of the read arena, pageable or pinned) plus one fq_text_rec per record; the device builds
+ * the tiled batch planes from the text, runs the pack's kernels, and writes the output FASTQ text
+ * of the records that pass (both mates of a pair for PE, to out1 / out2, in input order, each
+ * record "name\nseq[start, start+len)\nstrand\nqual[start, start+len)\n" as the reference writes
+ * it) into `out`.  Only for options whose outputs are out1 (+ out2): no -m, -c, UMI, index filter,
+ * phred64, split, failed or unpaired outputs; the host routes everything else through
+ * fq_engine_submit.  Records and text must stay valid until fq_engine_poll reports the pack; then
+ * `results` holds the records as from fq_engine_submit and out->bytes[m] the bytes of out->text[m].
+ * out->text[m] must hold at least the mate's text_bytes + 16 (a record's output is never longer
+ * than its input text, except by the final line terminator that the input may lack). */
+typedef struct fq_text_rec {
+    uint32_t name_off;   /* offsets from the mate's text pointer: the name line (without its terminator), */
+    uint32_t seq_off;    /* the sequence, */
+    uint32_t strand_off; /* the strand line, */
+    uint32_t qual_off;   /* the quality line */
+    uint16_t name_len, strand_len, len, pad;
+} fq_text_rec;
+typedef struct fq_text_batch {
+    int32_t n;      /* records (PE: pairs) */
+    int32_t stride; /* row stride of the planes the device builds (multiple of 16, >= every len) */
+    const char* text[2];
+    uint64_t text_bytes[2];
+    const fq_text_rec* rec[2]; /* rec[1]: PE only */
+} fq_text_batch;
+typedef struct fq_text_out {
+    char* text[2];      /* host buffers (pinned for full speed) of at least text_bytes[m] */
+    uint64_t bytes[2];  /* set when the pack is reported by fq_engine_poll */
+} fq_text_out;
+int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result* results, fq_text_out* out,
+                          uint64_t seq_no);
+
 /* Page-locked host memory for packs and records (hipHostMalloc, portable across devices).
  * FQ_E_NO_DEVICE without a HIP device: callers then use ordinary memory. */
 int fq_host_alloc(size_t bytes, void** out);

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from fqtool_amd import abi
-from batch_util import ALL_CONFIGS, Pack, config, edge_pack, polyx_pack, polyx_params, run_oracle, synth_pack
+from batch_util import AD1, AD2, ALL_CONFIGS, Pack, config, edge_pack, polyx_pack, polyx_params, run_oracle, synth_pack
 
 pytestmark = pytest.mark.gpu
 
@@ -149,6 +149,55 @@ def test_dense_per_pair_handoff(eng_lib, oracle, name, stride):
                 s[i, 150:330] = ord("G")
                 q[i, 150:330] = ord("F")
                 ln[i] = 330
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+@pytest.mark.parametrize("stride", [160, 336])
+@pytest.mark.parametrize("name", ["C3", "C3b", "C4", "C5", "PE_all", "PE_correct", "PE_umi_x", "C2", "SE_all"])
+def test_lowercase_bases(eng_lib, oracle, name, stride):
+    """Soft-masked reads: lowercase a c g t stay on the fast kernels (a per-base flag beside the
+    codes) -- stretches anywhere in either mate, lowercase polyG / polyX tails, lowercase adapter
+    copies, lowercase in the overlap of truly overlapping pairs -- next to a few hard bytes ('n',
+    IUPAC) that still go to the general kernel.  Byte semantics as the reference: the reverse
+    complement upper-cases them (src/seq.h:24-48), Stats buckets byte & 7 (src/stats.cpp:249),
+    passFilter counts 'N' only, polyG/polyX/adapter/complexity compare bytes."""
+    p = config(name, max_cycles=512)
+    paired = bool(p.paired)
+    n = 7001
+    pk = synth_pack(oracle, n, paired, first=4242, stride=stride)
+    rng = np.random.default_rng(41)
+    mates = [(pk.seq1, pk.len1)] + ([(pk.seq2, pk.len2)] if paired else [])
+    acgt = np.zeros(256, bool)
+    acgt[[ord(c) for c in "ACGT"]] = True
+    for m, (s, ln) in enumerate(mates):
+        ad = (AD1 if m == 0 else AD2).lower().encode()
+        for i in range(n):
+            L = int(ln[i])
+            u = rng.random()
+            if u < 0.25:  # a stretch
+                a = int(rng.integers(0, L))
+                b = min(L, a + int(rng.integers(1, 61)))
+            elif u < 0.32:  # the tail (polyG / polyX / adapter region)
+                a, b = L - int(rng.integers(1, 31)), L
+            elif u < 0.36 and L > 60:  # a lowercase adapter copy
+                k = int(rng.integers(20, L - 10))
+                t = ad[: L - k]
+                s[i, k:k + len(t)] = np.frombuffer(t, np.uint8)
+                continue
+            elif u < 0.39:  # a lowercase polyG tail
+                g = int(rng.integers(5, 40))
+                s[i, max(0, L - g):L] = ord("g")
+                continue
+            elif u < 0.41:  # a hard byte: the pair goes over
+                s[i, int(rng.integers(0, L))] = ord("n") if rng.random() < 0.5 else ord("R")
+                continue
+            else:
+                continue
+            a = max(a, 0)
+            row = s[i, a:b]
+            row[acgt[row]] |= 0x20
     res_o, acc_o = run_oracle(oracle, p, pk)
     res_e, acc_e = run_engine(eng_lib, p, pk)
     assert_same(p, res_o, acc_o, res_e, acc_e)

@@ -77,10 +77,10 @@ def masked_json(path):
     return j
 
 
-def run(tool, r1, r2, d, tag, cfg, workers):
+def run(tool, r1, r2, d, tag, cfg, workers, extra=()):
     o = {k: os.path.join(d, f"{tag}_{k}") for k in ("o1.fq", "o2.fq", "m.fq", "r.json", "r.html")}
     cmd = [tool, "-i", r1, "-I", r2, "-o", o["o1.fq"], "-O", o["o2.fq"], *OPTS[cfg], "-w", str(workers),
-           "-J", o["r.json"], "-H", o["r.html"]]
+           "-J", o["r.json"], "-H", o["r.html"], *extra]
     if cfg == "C4":
         cmd += ["--merge_output", o["m.fq"]]
     t0 = time.perf_counter()
@@ -88,8 +88,8 @@ def run(tool, r1, r2, d, tag, cfg, workers):
     wall = time.perf_counter() - t0
     if p.returncode != 0:
         raise SystemExit(f"{tag} failed rc={p.returncode}: {p.stderr[-2000:]}")
-    m = re.search(r"wall ([0-9.]+) s, engine submit/wait ([0-9.]+) s(.*)", p.stderr)
-    return wall, (m.groups() if m else None), o
+    m = re.search(r"fqtool-amd: (.*)", p.stderr)
+    return wall, (m.group(1) if m else None), o
 
 
 def main():
@@ -98,6 +98,8 @@ def main():
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--config", default="C3", choices=sorted(OPTS))
     ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--devices", default=None, help="--devices of the fqtool-amd run (e.g. 0,0,0,0)")
+    ap.add_argument("--repeat", type=int, default=1, help="runs of the fqtool-amd binary (all printed)")
     args = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="fqe2e_")
     try:
@@ -107,11 +109,14 @@ def main():
         print(f"[e2e] wrote {args.pairs} pairs ({gb:.2f} GB FASTQ) in {time.perf_counter() - t0:.1f}s", flush=True)
         reads = 2 * args.pairs
         ours = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
-        wall, inner, o_ours = run(ours, r1, r2, tmp, "amd", args.config, args.workers)
-        line = {"tool": "fqtool-amd", "config": args.config, "pairs": args.pairs, "fastq_GB": round(gb, 3),
-                "wall_s": round(wall, 3), "Mreads_s": round(reads / wall / 1e6, 3),
-                "fastq_GB_s": round(gb / wall, 3), "workers": args.workers, "tool_log": inner}
-        print(json.dumps(line), flush=True)
+        extra = ["--devices", args.devices] if args.devices else []
+        for _ in range(args.repeat):
+            wall, inner, o_ours = run(ours, r1, r2, tmp, "amd", args.config, args.workers, extra)
+            line = {"tool": "fqtool-amd", "config": args.config, "pairs": args.pairs, "fastq_GB": round(gb, 3),
+                    "wall_s": round(wall, 3), "Mreads_s": round(reads / wall / 1e6, 3),
+                    "fastq_GB_s": round(gb / wall, 3), "workers": args.workers, "devices": args.devices,
+                    "text_mode": os.environ.get("FQ_TEXT_MODE", "1") != "0", "tool_log": inner}
+            print(json.dumps(line), flush=True)
         ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
         if not args.no_ref and os.path.exists(ref):
             w = min(16, args.workers)
