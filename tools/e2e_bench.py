@@ -77,8 +77,11 @@ def masked_json(path):
     return j
 
 
-def run(tool, r1, r2, d, tag, cfg, workers, extra=()):
+def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
     o = {k: os.path.join(d, f"{tag}_{k}") for k in ("o1.fq", "o2.fq", "m.fq", "r.json", "r.html")}
+    if null_out:
+        for k in ("o1.fq", "o2.fq", "m.fq"):
+            o[k] = "/dev/null"
     cmd = [tool, "-i", r1, "-I", r2, "-o", o["o1.fq"], "-O", o["o2.fq"], *OPTS[cfg], "-w", str(workers),
            "-J", o["r.json"], "-H", o["r.html"], *extra]
     if cfg == "C4":
@@ -100,6 +103,8 @@ def main():
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--devices", default=None, help="--devices of the fqtool-amd run (e.g. 0,0,0,0)")
     ap.add_argument("--repeat", type=int, default=1, help="runs of the fqtool-amd binary (all printed)")
+    ap.add_argument("--null-out", action="store_true", help="FASTQ outputs to /dev/null (as bench.py's e2e leg)")
+    ap.add_argument("--workers-list", default=None, help="comma list of -w values to run (overrides --workers)")
     args = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="fqe2e_")
     try:
@@ -110,15 +115,16 @@ def main():
         reads = 2 * args.pairs
         ours = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
         extra = ["--devices", args.devices] if args.devices else []
-        for _ in range(args.repeat):
-            wall, inner, o_ours = run(ours, r1, r2, tmp, "amd", args.config, args.workers, extra)
+        wl = [int(x) for x in args.workers_list.split(",")] if args.workers_list else [args.workers]
+        for _, w in [(r, w) for w in wl for r in range(args.repeat)]:
+            wall, inner, o_ours = run(ours, r1, r2, tmp, "amd", args.config, w, extra, args.null_out)
             line = {"tool": "fqtool-amd", "config": args.config, "pairs": args.pairs, "fastq_GB": round(gb, 3),
                     "wall_s": round(wall, 3), "Mreads_s": round(reads / wall / 1e6, 3),
-                    "fastq_GB_s": round(gb / wall, 3), "workers": args.workers, "devices": args.devices,
+                    "fastq_GB_s": round(gb / wall, 3), "workers": w, "devices": args.devices,
                     "text_mode": os.environ.get("FQ_TEXT_MODE", "1") != "0", "tool_log": inner}
             print(json.dumps(line), flush=True)
         ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
-        if not args.no_ref and os.path.exists(ref):
+        if not args.no_ref and not args.null_out and os.path.exists(ref):
             w = min(16, args.workers)
             wall_r, _, o_ref = run(ref, r1, r2, tmp, "ref", args.config, w)
             print(json.dumps({"tool": "reference", "config": args.config, "pairs": args.pairs, "wall_s": round(wall_r, 3),
