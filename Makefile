@@ -29,7 +29,7 @@ CSRC       := fqtool_amd/csrc
 LIBDIR     := fqtool_amd/lib
 OBJDIR     := build/obj
 
-ENGINE_SRCS := $(CSRC)/engine.hip $(CSRC)/pe_kernel.hip $(CSRC)/pe_fast.hip $(CSRC)/pe_fast_long.hip $(CSRC)/synth.hip $(CSRC)/dup.hip $(CSRC)/kmer.hip $(CSRC)/text.hip
+ENGINE_SRCS := $(CSRC)/engine.hip $(CSRC)/pe_kernel.hip $(CSRC)/pe_fast.hip $(CSRC)/pe_fast_long.hip $(CSRC)/synth.hip $(CSRC)/dup.hip $(CSRC)/kmer.hip $(CSRC)/text.hip $(CSRC)/raw.hip
 ENGINE_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(ENGINE_SRCS))
 ENGINE_HDRS := include/fqengine.h $(CSRC)/engine_internal.h $(CSRC)/device_ops.h
 $(OBJDIR)/pe_fast_long.o: $(CSRC)/pe_fast.hip

@@ -729,7 +729,7 @@ def main():
                          "(config 4's 1 B pairs over 8 GPUs)")
     ap.add_argument("--cpu-pairs", type=int, default=1_000_000, help="CPU-baseline sample size (pairs)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip both host legs (e2e and CPU baseline)")
-    ap.add_argument("--e2e-pairs", type=int, default=10_000_000, help="pairs of the end-to-end tool leg (0: off)")
+    ap.add_argument("--e2e-pairs", type=int, default=50_000_000, help="pairs of the end-to-end tool leg (0: off)")
     ap.add_argument("--paths-pairs", type=int, default=20_000_000,
                     help="pairs of the off-baseline path leg (C3 + UMI / -c / 1 %% lowercase; 0: off)")
     ap.add_argument("--sample-pairs", type=int, default=1_000_000,

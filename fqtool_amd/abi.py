@@ -109,6 +109,20 @@ class FqTextOut(ctypes.Structure):
     _fields_ = [("text", ctypes.c_void_p * 2), ("bytes", ctypes.c_uint64 * 2)]
 
 
+class FqRawWindow(ctypes.Structure):  # fq_raw_window
+    _fields_ = [("bytes", ctypes.c_void_p * 2), ("n", ctypes.c_uint64 * 2)]
+
+
+class FqRawResult(ctypes.Structure):  # fq_raw_result
+    _fields_ = [("pairs", ctypes.c_int32), ("stop", ctypes.c_int32), ("max_len", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("carry", ctypes.c_uint64 * 2), ("text_bytes", ctypes.c_uint64 * 2)]
+
+
+class FqRawOut(ctypes.Structure):  # fq_raw_out
+    _fields_ = [("text", FqTextOut), ("adapters", ctypes.c_void_p * 2), ("adapter_cap", ctypes.c_uint64 * 2),
+                ("adapter_bytes", ctypes.c_uint64 * 2)]
+
+
 # Batch planes hold rows in chunk-interleaved tiles (include/fqengine.h): byte j of read i at
 # (i // 32) * 32 * stride + (j // 16) * 512 + (i % 32) * 16 + j % 16.
 TILE_READS = 32
@@ -240,6 +254,11 @@ def load_engine(path=ENGINE_LIB):
     lib.fq_engine_submit_text.argtypes = [vp, ctypes.POINTER(FqTextBatch), vp, ctypes.POINTER(FqTextOut), u64]
     lib.fq_engine_poll.argtypes = [vp, ctypes.c_int, ctypes.POINTER(u64)]
     lib.fq_engine_pending.argtypes = [vp]
+    lib.fq_engine_raw_begin.argtypes = [vp, u64, u64]
+    lib.fq_engine_raw_enqueue.argtypes = [vp, ctypes.POINTER(FqRawWindow)]
+    lib.fq_engine_raw_launch.argtypes = [vp, ctypes.POINTER(FqRawResult), ctypes.POINTER(FqRawOut), u64]
+    lib.fq_host_register.argtypes = [vp, ctypes.c_size_t]
+    lib.fq_host_unregister.argtypes = [vp]
     lib.fq_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
     lib.fq_host_free.argtypes = [vp]
     lib.fq_dup_create.argtypes = [ctypes.c_int, i32, ctypes.POINTER(vp)]
@@ -262,6 +281,7 @@ ENGINE_SYMBOLS = [
     "fq_engine_last_kernel_ms", "fq_engine_submit", "fq_engine_submit_text", "fq_engine_poll", "fq_engine_pending", "fq_host_alloc",
     "fq_host_free", "fq_dup_create", "fq_dup_destroy", "fq_dup_reset", "fq_engine_set_dup", "fq_dup_merge",
     "fq_dup_stat", "fq_kmer_open", "fq_kmer_close", "fq_kmer_count", "fq_kmer_find",
+    "fq_engine_raw_begin", "fq_engine_raw_enqueue", "fq_engine_raw_launch", "fq_host_register", "fq_host_unregister",
 ]
 
 

@@ -6,7 +6,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <deque>
+#include <mutex>
+#include <unordered_map>
+#include <sys/mman.h>
 #include <string>
 
 #include "engine_internal.h"
@@ -41,6 +45,17 @@ struct Slot {
     unsigned long long* d_total = nullptr;  // [2]
     unsigned long long* h_total = nullptr;  // pinned [2]
     fq_text_out* text_out = nullptr;        // the pending text pack's output descriptor
+    // raw windows (fq_engine_raw_*): line index, block counts / bases, indexing state, adapter entries
+    uint32_t* d_lines[2] = {nullptr, nullptr};
+    uint32_t* d_bcnt[2] = {nullptr, nullptr};
+    uint32_t* d_bbase[2] = {nullptr, nullptr};
+    fq_raw_state* d_rstate = nullptr;  // [2]
+    fq_raw_state* h_rstate = nullptr;  // pinned [2]
+    char* d_ad[2] = {nullptr, nullptr};
+    size_t ad_cap = 0;
+    bool raw_ready = false;
+    hipEvent_t ev_idx = nullptr;
+    fq_raw_out* raw_out = nullptr;  // the pending raw pack's output descriptor
     int* d_err = nullptr;  // this pack's device error word (cleared at submit, set by its kernels)
     int* h_err = nullptr;  // pinned: d_err as of this pack's kernels
     bool busy = false;      // events recorded and not yet waited for
@@ -75,6 +90,13 @@ struct fq_engine {
     bool fast = false;  // pe_fast kernel usable for these params
     Scratch scratch;    // hand-off list of fq_engine_process_device
     bool timed = false;
+    // raw stream (fq_engine_raw_*): window / carry capacity, index stream, windows not yet launched
+    bool raw = false;
+    uint64_t raw_wcap = 0, raw_ccap = 0;
+    uint32_t raw_nblocks = 0;
+    hipStream_t s_idx = nullptr;
+    std::deque<int> raw_queued;
+    int raw_prev_slot = -1;
     fq_dup* dup = nullptr;    // duplication table fed by every pack (-d)
     uint64_t calls = 0;       // order of process / process_device packs for the table
     std::string last_error;
@@ -146,6 +168,15 @@ static void free_slot(Slot& s) {
     if (s.d_scan) (void)hipFree(s.d_scan);
     if (s.d_total) (void)hipFree(s.d_total);
     if (s.h_total) (void)hipHostFree(s.h_total);
+    for (int m = 0; m < 2; ++m) {
+        if (s.d_lines[m]) (void)hipFree(s.d_lines[m]);
+        if (s.d_bcnt[m]) (void)hipFree(s.d_bcnt[m]);
+        if (s.d_bbase[m]) (void)hipFree(s.d_bbase[m]);
+        if (s.d_ad[m]) (void)hipFree(s.d_ad[m]);
+    }
+    if (s.d_rstate) (void)hipFree(s.d_rstate);
+    if (s.h_rstate) (void)hipHostFree(s.h_rstate);
+    if (s.ev_idx) (void)hipEventDestroy(s.ev_idx);
     if (s.d_err) (void)hipFree(s.d_err);
     if (s.h_err) (void)hipHostFree(s.h_err);
     if (s.ev_in) (void)hipEventDestroy(s.ev_in);
@@ -237,7 +268,7 @@ int fq_engine_destroy(fq_engine* e) {
     free_scratch(e->scratch);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
-    for (hipStream_t s : {e->stream, e->s_in, e->s_out})
+    for (hipStream_t s : {e->stream, e->s_in, e->s_out, e->s_idx})
         if (s) (void)hipStreamDestroy(s);
     delete e;
     return FQ_OK;
@@ -313,6 +344,18 @@ static int retire_slot(fq_engine* e, int k) {
         s.text_out->bytes[1] = s.h_total[1];
         s.text_out = nullptr;
     }
+    if (s.raw_out) {  // a raw pack: its trimmed-adapter entries, exactly sized, before the slot is reused
+        fq_raw_out* o = s.raw_out;
+        s.raw_out = nullptr;
+        for (int m = 0; m < 2; ++m) {
+            const uint64_t b = s.h_total[2 + m];
+            o->adapter_bytes[m] = 0;
+            if (!b) continue;
+            if (b > o->adapter_cap[m] || !o->adapters[m]) return fail(e, FQ_E_INVALID, "raw pack: adapter buffer too small");
+            HIP_TRY(e, hipMemcpy(o->adapters[m], s.d_ad[m], b, hipMemcpyDeviceToHost));
+            o->adapter_bytes[m] = b;
+        }
+    }
     return FQ_OK;
 }
 
@@ -326,6 +369,7 @@ static int ensure_text(fq_engine* e, Slot& s, const fq_text_batch* tb) {
     for (int m = 0; m < (pe ? 2 : 1); ++m) {
         const size_t need = tb->text_bytes[m] + kTextSlack;
         if (need > s.text_cap[m]) {
+            s.raw_ready = false;  // (the raw-window buffers are re-made by ensure_raw)
             if (s.d_text[m]) (void)hipFree(s.d_text[m]);
             if (s.d_out[m]) (void)hipFree(s.d_out[m]);
             s.d_text[m] = s.d_out[m] = nullptr;
@@ -337,6 +381,7 @@ static int ensure_text(fq_engine* e, Slot& s, const fq_text_batch* tb) {
         }
     }
     if ((size_t)tb->n > s.trec_cap || !s.d_total) {
+        s.raw_ready = false;
         const size_t cap = (size_t)tb->n + (size_t)tb->n / 8 + 1;
         for (int m = 0; m < 2; ++m) {
             if (s.d_trec[m]) (void)hipFree(s.d_trec[m]);
@@ -355,8 +400,8 @@ static int ensure_text(fq_engine* e, Slot& s, const fq_text_batch* tb) {
         }
         s.scan_bytes = fq_text_scan_temp_bytes((int)cap);
         HIP_TRY(e, hipMalloc(&s.d_scan, s.scan_bytes ? s.scan_bytes : 1));
-        if (!s.d_total) HIP_TRY(e, hipMalloc(&s.d_total, 2 * sizeof(unsigned long long)));
-        if (!s.h_total) HIP_TRY(e, hipHostMalloc((void**)&s.h_total, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+        if (!s.d_total) HIP_TRY(e, hipMalloc(&s.d_total, 4 * sizeof(unsigned long long)));
+        if (!s.h_total) HIP_TRY(e, hipHostMalloc((void**)&s.h_total, 4 * sizeof(unsigned long long), hipHostMallocDefault));
         s.trec_cap = cap;
     }
     return FQ_OK;
@@ -509,6 +554,203 @@ int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*
     return FQ_OK;
 }
 
+// ---- raw FASTQ streams -----------------------------------------------------------------------
+
+// the raw-window buffers of slot s (the text-pack buffers at raw capacity plus the line index)
+static int ensure_raw(fq_engine* e, Slot& s) {
+    if (s.raw_ready) return FQ_OK;
+    const bool pe = e->p.paired;
+    const size_t text = (size_t)e->raw_nblocks * 4096;
+    const size_t recs = (size_t)e->max_batch + 1;
+    const size_t cap_lines = 4 * recs + 8;
+    for (int m = 0; m < 2; ++m) {
+        if (s.d_text[m]) (void)hipFree(s.d_text[m]);
+        if (s.d_out[m]) (void)hipFree(s.d_out[m]);
+        if (s.d_trec[m]) (void)hipFree(s.d_trec[m]);
+        if (s.d_tsize[m]) (void)hipFree(s.d_tsize[m]);
+        if (s.d_toff[m]) (void)hipFree(s.d_toff[m]);
+        s.d_text[m] = s.d_out[m] = nullptr;
+        s.d_trec[m] = nullptr;
+        s.d_tsize[m] = s.d_toff[m] = nullptr;
+        for (uint32_t** q : {&s.d_lines[m], &s.d_bcnt[m], &s.d_bbase[m]})
+            if (*q) {
+                (void)hipFree(*q);
+                *q = nullptr;
+            }
+        if (s.d_ad[m]) (void)hipFree(s.d_ad[m]);
+        s.d_ad[m] = nullptr;
+        if (m == 1 && !pe) continue;
+        HIP_TRY(e, hipMalloc(&s.d_text[m], text));
+        HIP_TRY(e, hipMalloc(&s.d_out[m], text));
+        HIP_TRY(e, hipMalloc(&s.d_trec[m], recs * sizeof(fq_text_rec)));
+        HIP_TRY(e, hipMalloc(&s.d_tsize[m], recs * sizeof(uint32_t)));
+        HIP_TRY(e, hipMalloc(&s.d_toff[m], recs * sizeof(uint32_t)));
+        HIP_TRY(e, hipMalloc(&s.d_lines[m], cap_lines * sizeof(uint32_t)));
+        HIP_TRY(e, hipMalloc(&s.d_bcnt[m], (size_t)e->raw_nblocks * sizeof(uint32_t)));
+        HIP_TRY(e, hipMalloc(&s.d_bbase[m], (size_t)e->raw_nblocks * sizeof(uint32_t)));
+        s.ad_cap = recs * (size_t)(3 + e->max_stride);
+        HIP_TRY(e, hipMalloc(&s.d_ad[m], s.ad_cap));
+    }
+    s.text_cap[0] = s.text_cap[1] = 0;  // (not the text-pack sizes: ensure_text re-allocates)
+    s.trec_cap = 0;
+    if (s.d_scan) (void)hipFree(s.d_scan);
+    s.scan_bytes = std::max(fq_raw_scan_temp_bytes((int)e->raw_nblocks, (int)recs), fq_text_scan_temp_bytes((int)recs));
+    HIP_TRY(e, hipMalloc(&s.d_scan, s.scan_bytes));
+    if (!s.d_total) HIP_TRY(e, hipMalloc(&s.d_total, 4 * sizeof(unsigned long long)));
+    if (!s.h_total) HIP_TRY(e, hipHostMalloc((void**)&s.h_total, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+    if (!s.d_rstate) HIP_TRY(e, hipMalloc(&s.d_rstate, 2 * sizeof(fq_raw_state)));
+    if (!s.h_rstate) HIP_TRY(e, hipHostMalloc((void**)&s.h_rstate, 2 * sizeof(fq_raw_state), hipHostMallocDefault));
+    if (!s.ev_idx) HIP_TRY(e, hipEventCreateWithFlags(&s.ev_idx, hipEventDisableTiming));
+    s.raw_ready = true;
+    return FQ_OK;
+}
+
+int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap) {
+    if (!e) return FQ_E_INVALID;
+    if (!e->pending.empty() || !e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_begin with packs in flight");
+    if (e->p.merge_enabled || e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0)
+        return fail(e, FQ_E_INVALID, "raw streams take no -m, -c or UMI options");
+    carry_cap = (carry_cap + 4095) / 4096 * 4096;
+    if (!window_cap || carry_cap + window_cap + 4096 >= (1ull << 31) || e->max_batch <= 0)
+        return fail(e, FQ_E_INVALID, "raw window / carry capacity out of range");
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipDeviceSynchronize());
+    if (!e->s_idx) HIP_TRY(e, hipStreamCreateWithFlags(&e->s_idx, hipStreamNonBlocking));
+    const uint32_t nb = (uint32_t)((carry_cap + window_cap + 64 + 4095) / 4096);
+    if (!e->raw || nb != e->raw_nblocks || carry_cap != e->raw_ccap)
+        for (Slot& s : e->slots) s.raw_ready = false;
+    e->raw = true;
+    e->raw_wcap = window_cap;
+    e->raw_ccap = carry_cap;
+    e->raw_nblocks = nb;
+    e->raw_prev_slot = -1;
+    e->raw_queued.clear();
+    return FQ_OK;
+}
+
+int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w) {
+    if (!e || !w) return FQ_E_INVALID;
+    if (!e->raw) return fail(e, FQ_E_INVALID, "fq_engine_raw_enqueue before fq_engine_raw_begin");
+    if (e->raw_queued.size() >= 2) return fail(e, FQ_E_INVALID, "two raw windows are already waiting for fq_engine_raw_launch");
+    const bool pe = e->p.paired;
+    for (int m = 0; m < (pe ? 2 : 1); ++m)
+        if (w->n[m] > e->raw_wcap || (w->n[m] && !w->bytes[m])) return fail(e, FQ_E_INVALID, "raw window exceeds its capacity");
+    HIP_TRY(e, hipSetDevice(e->device));
+    const int k = (e->raw_prev_slot + 1) % kSlots;
+    int rc = retire_slot(e, k);
+    if (rc != FQ_OK) return rc;
+    Slot& s = e->slots[k];
+    if ((rc = alloc_slot(e, s)) != FQ_OK) return rc;
+    if ((rc = ensure_raw(e, s)) != FQ_OK) return rc;
+    for (int m = 0; m < (pe ? 2 : 1); ++m)
+        if (w->n[m])
+            HIP_TRY(e, hipMemcpyAsync(s.d_text[m] + e->raw_ccap, w->bytes[m], w->n[m], hipMemcpyHostToDevice, e->s_in));
+    HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
+    HIP_TRY(e, hipStreamWaitEvent(e->s_idx, s.ev_in, 0));
+    fq_raw_text_args a{};
+    const Slot* ps = e->raw_prev_slot >= 0 ? &e->slots[e->raw_prev_slot] : nullptr;
+    for (int m = 0; m < 2; ++m) {
+        a.text[m] = s.d_text[m];
+        a.prev_text[m] = ps ? ps->d_text[m] : nullptr;
+        a.raw_bytes[m] = (uint32_t)w->n[m];
+        a.bcnt[m] = s.d_bcnt[m];
+        a.bbase[m] = s.d_bbase[m];
+        a.lines[m] = s.d_lines[m];
+        a.rec[m] = s.d_trec[m];
+    }
+    a.prev_state = ps ? ps->d_rstate : nullptr;
+    a.state = s.d_rstate;
+    a.carry_cap = (uint32_t)e->raw_ccap;
+    a.nblocks = e->raw_nblocks;
+    a.cap_lines = (uint32_t)(4 * ((size_t)e->max_batch + 1) + 8);
+    a.cap_records = e->max_batch + 1;
+    a.max_len = std::min(e->max_stride, e->p.max_cycles);
+    HIP_TRY(e, fq_launch_raw_index(a, pe ? 2 : 1, e->max_batch, s.d_scan, s.scan_bytes, e->s_idx));
+    HIP_TRY(e, hipMemcpyAsync(s.h_rstate, s.d_rstate, 2 * sizeof(fq_raw_state), hipMemcpyDeviceToHost, e->s_idx));
+    HIP_TRY(e, hipEventRecord(s.ev_idx, e->s_idx));
+    e->raw_queued.push_back(k);
+    e->raw_prev_slot = k;
+    return FQ_OK;
+}
+
+int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64_t seq_no) {
+    if (!e || !r || !out) return FQ_E_INVALID;
+    if (e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_launch without an enqueued window");
+    HIP_TRY(e, hipSetDevice(e->device));
+    const int k = e->raw_queued.front();
+    e->raw_queued.pop_front();
+    Slot& s = e->slots[k];
+    HIP_TRY(e, hipEventSynchronize(s.ev_idx));
+    const bool pe = e->p.paired;
+    const int mates = pe ? 2 : 1;
+    std::memset(r, 0, sizeof *r);
+    const int n = s.h_rstate[0].n;
+    r->pairs = n;
+    for (int m = 0; m < mates; ++m) {
+        const fq_raw_state& st = s.h_rstate[m];
+        r->carry[m] = st.avail - st.consumed;
+        r->text_bytes[m] = st.consumed;
+        r->max_len = std::max(r->max_len, st.max_len);
+        if (st.overflow || st.first_bad == n) r->stop = 1;
+    }
+    out->text.bytes[0] = out->text.bytes[1] = 0;
+    out->adapter_bytes[0] = out->adapter_bytes[1] = 0;
+    if (n <= 0) {
+        e->pending.push_back(Pending{seq_no, -1, true, 0});
+        return FQ_OK;
+    }
+    for (int m = 0; m < mates; ++m)
+        if (!out->text.text[m]) return fail(e, FQ_E_INVALID, "raw pack: missing output buffer");
+    const size_t plane = fq_batch_bytes(e->max_batch, e->max_stride);
+    fq_batch db{};
+    db.n = n;
+    db.stride = std::max(16, (r->max_len + 15) & ~15);
+    db.seq1 = s.d_rows;
+    db.qual1 = s.d_rows + plane;
+    db.len1 = s.d_lens;
+    db.seq2 = pe ? s.d_rows + 2 * plane : nullptr;
+    db.qual2 = pe ? s.d_rows + 3 * plane : nullptr;
+    db.len2 = pe ? s.d_lens + e->max_batch : nullptr;
+    HIP_TRY(e, hipStreamWaitEvent(e->stream, s.ev_idx, 0));
+    for (int m = 0; m < mates; ++m)
+        HIP_TRY(e, fq_launch_text_tiles(s.d_text[m], s.d_trec[m], n, db.stride, const_cast<uint8_t*>(m ? db.seq2 : db.seq1),
+                                        const_cast<uint8_t*>(m ? db.qual2 : db.qual1), const_cast<uint16_t*>(m ? db.len2 : db.len1),
+                                        e->stream));
+    HIP_TRY(e, hipMemsetAsync(s.d_err, 0, sizeof(int), e->stream));
+    int rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false, seq_no, s.d_err);
+    if (rc != FQ_OK) return rc;
+    HIP_TRY(e, hipMemsetAsync(s.d_total, 0, 4 * sizeof(unsigned long long), e->stream));
+    for (int m = 0; m < mates; ++m) {
+        HIP_TRY(e, fq_launch_text_out(s.d_text[m], s.d_trec[m], s.d_res, n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
+                                      s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, e->stream));
+        if (e->p.adapter_trimming)
+            HIP_TRY(e, fq_launch_raw_adapters(s.d_text[m], s.d_trec[m], s.d_res, n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
+                                              s.d_scan, s.scan_bytes, s.d_ad[m], s.d_total + 2 + m, e->stream));
+    }
+    HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
+    HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
+    HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
+    for (int m = 0; m < mates; ++m)
+        HIP_TRY(e, hipMemcpyAsync(out->text.text[m], s.d_out[m], r->text_bytes[m] + kTextSlack, hipMemcpyDeviceToHost, e->s_out));
+    HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
+    HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
+    s.busy = true;
+    s.text_out = &out->text;
+    s.raw_out = out;
+    e->pending.push_back(Pending{seq_no, k, false, 0});
+    return FQ_OK;
+}
+
+int fq_host_register(const void* p, size_t bytes) {
+    if (!p || !bytes) return FQ_E_INVALID;
+    return hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterReadOnly) == hipSuccess ? FQ_OK : FQ_E_HIP;
+}
+
+int fq_host_unregister(const void* p) {
+    if (!p) return FQ_E_INVALID;
+    return hipHostUnregister(const_cast<void*>(p)) == hipSuccess ? FQ_OK : FQ_E_HIP;
+}
+
 int fq_engine_poll(fq_engine* e, int wait, uint64_t* seq_no) {
     if (!e) return FQ_E_INVALID;
     if (e->pending.empty()) return 0;
@@ -611,12 +853,34 @@ int fq_engine_device_info(const fq_engine* e, int* device, char* arch, size_t ar
     return FQ_OK;
 }
 
+// Page-locked host memory as anonymous transparent-huge-page memory, populated, then registered
+// with every device (portable): 0.06 s per GiB to set up and 0.04 s to release, against 0.23 s
+// and 0.13 s for hipHostMalloc (tools/micro/h2d.hip on MI355X), and DMA at the same 57 GB/s.
+// The mapping length of each block is kept for fq_host_free; hipHostMalloc is the fallback.
+namespace {
+std::mutex g_host_mu;
+std::unordered_map<void*, size_t> g_host_maps;  // registered anonymous mappings -> length
+}  // namespace
+
 int fq_host_alloc(size_t bytes, void** out) {
     if (!out) return FQ_E_INVALID;
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return FQ_E_NO_DEVICE;
-    // portable: any device's DMA engines may read it (packs are dealt over several GPUs)
+    const size_t huge = (size_t)2 << 20;
+    const size_t len = ((bytes ? bytes : 1) + huge - 1) / huge * huge;
+    void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m != MAP_FAILED) {
+        (void)madvise(m, len, MADV_HUGEPAGE);
+        std::memset(m, 0, len);  // populate (registration pins what is there)
+        if (hipHostRegister(m, len, hipHostRegisterPortable) == hipSuccess) {
+            std::lock_guard<std::mutex> g(g_host_mu);
+            g_host_maps[m] = len;
+            *out = m;
+            return FQ_OK;
+        }
+        munmap(m, len);
+    }
     if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) {
         *out = nullptr;
         return FQ_E_NOMEM;
@@ -626,6 +890,20 @@ int fq_host_alloc(size_t bytes, void** out) {
 
 int fq_host_free(void* p) {
     if (!p) return FQ_OK;
+    size_t len = 0;
+    {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        auto it = g_host_maps.find(p);
+        if (it != g_host_maps.end()) {
+            len = it->second;
+            g_host_maps.erase(it);
+        }
+    }
+    if (len) {
+        const bool ok = hipHostUnregister(p) == hipSuccess;
+        munmap(p, len);
+        return ok ? FQ_OK : FQ_E_HIP;
+    }
     return hipHostFree(p) == hipSuccess ? FQ_OK : FQ_E_HIP;
 }
 

@@ -42,3 +42,39 @@ size_t fq_text_scan_temp_bytes(int n);
 hipError_t fq_launch_text_out(const char* d_text, const fq_text_rec* d_rec, const fq_read_result* d_res, int n, int paired,
                               int m, uint32_t* d_size, uint32_t* d_off, void* d_temp, size_t temp_bytes, char* d_out,
                               unsigned long long* d_total, hipStream_t s);
+// Raw FASTQ streams (raw.hip): per (window, mate) device state of the record indexing
+struct fq_raw_state {
+    uint32_t text_start;  // buffer offset of the window's text (the carried bytes first)
+    uint32_t carry_in;    // bytes carried over from the previous window
+    uint32_t avail;       // carry_in + the window's raw bytes
+    uint32_t overflow;    // the carry did not fit (nothing is indexed)
+    int32_t first_bad;    // lowest index of a complete record that is not plain (INT_MAX: none)
+    int32_t complete;     // records whose four lines are in the text (capped by the record capacity)
+    int32_t max_len;      // longest sequence of the plain records
+    uint32_t total_lines;
+    uint32_t consumed;    // text bytes taken by the pack's records
+    int32_t n;            // records (pairs) of the pack
+    uint32_t pad[2];
+};
+struct fq_raw_text_args {
+    char* text[2];
+    const char* prev_text[2];
+    const fq_raw_state* prev_state;  // previous window's states, nullptr at the start of the stream
+    fq_raw_state* state;             // [2]
+    uint32_t raw_bytes[2];
+    uint32_t carry_cap;              // the raw bytes land at this buffer offset
+    uint32_t nblocks;                // 4 KiB blocks of the buffer
+    uint32_t* bcnt[2];
+    uint32_t* bbase[2];
+    uint32_t* lines[2];
+    uint32_t cap_lines;
+    int cap_records;
+    fq_text_rec* rec[2];
+    int max_len;                     // longest sequence the engine takes (longer: not plain)
+};
+size_t fq_raw_scan_temp_bytes(int nblocks, int n);
+hipError_t fq_launch_raw_index(const fq_raw_text_args& a, int mates, int cap_batch, void* d_temp, size_t temp_bytes,
+                               hipStream_t s);
+hipError_t fq_launch_raw_adapters(const char* d_text, const fq_text_rec* d_rec, const fq_read_result* d_res, int n,
+                                  int paired, int m, uint32_t* d_size, uint32_t* d_off, void* d_temp, size_t temp_bytes,
+                                  char* d_out, unsigned long long* d_total, hipStream_t s);

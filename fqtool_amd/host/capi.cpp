@@ -80,7 +80,7 @@ char* fqh_report_json(int argc, const char* argv_blob, const uint64_t* acc, int 
             else if (tag == "D2") o.detected_adapter2 = seq;
             else if (tag == "1" || tag == "2") {
                 ls >> cnt;
-                (tag == "1" ? ac.r1 : ac.r2)[seq] += cnt;
+                ac.add(tag == "1" ? 0 : 1, seq, cnt);
             }
         }
         HostAcc h(o.insert_size_max);

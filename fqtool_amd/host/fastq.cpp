@@ -668,6 +668,7 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
 // ---- Pack ----
 void Pack::clear() {
     n = 0;
+    raw = false;
     stride = 0;
     base[0] = base[1] = nullptr;
     for (int m = 0; m < 2; ++m) {
@@ -812,6 +813,13 @@ void pack_tiles(Pack& pk, Pool* pool) {
     else if (tiles) work(0);
 }
 
+void FqBulkReader::seek(uint64_t off) {
+    if (!map_) throw std::runtime_error("FqBulkReader::seek on an unmapped input");
+    pos_ = (size_t)std::min<uint64_t>(off, map_size_);
+    tbase_ = pos_ >> 6;
+    indexed_ = tbase_ << 6;
+}
+
 // ---- PackReader ----
 PackReader::PackReader(const std::string& in1, const std::string& in2, bool interleaved, bool phred64, int buf_size)
     : r1_(in1, phred64, buf_size), paired_(!in2.empty() || interleaved), interleaved_(interleaved) {
@@ -832,6 +840,13 @@ size_t read_mate(FqBulkReader& r, Pack& pk, int m, size_t max_n, Pool* pool) {
     return k;
 }
 }  // namespace
+
+void PackReader::seek(uint64_t off1, uint64_t off2, uint64_t first_seq) {
+    r1_.seek(off1);
+    if (r2_) r2_->seek(off2);
+    packs_ = first_seq;
+    done_ = false;
+}
 
 bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     if (done_) return false;

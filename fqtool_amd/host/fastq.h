@@ -166,6 +166,8 @@ class FqBulkReader {
     // the records' offsets refer to (the arena, or the file mapping)
     const char* end();
     const std::string& error() const { return err_; }
+    bool mapped() const { return map_ != nullptr; }
+    void seek(uint64_t off);  // mapped files: the next record is read from stream offset off
 
    private:
     bool line(size_t x, size_t& e, size_t& next);
@@ -222,7 +224,8 @@ struct Pack {
           flags(pinned),
           res(pinned),
           trec{PodBuf<fq_text_rec>(pinned), PodBuf<fq_text_rec>(pinned)},
-          out_text{ByteBuf(pinned), ByteBuf(pinned)} {}
+          out_text{ByteBuf(pinned), ByteBuf(pinned)},
+          ad{ByteBuf(pinned), ByteBuf(pinned)} {}
     int n = 0;
     int stride = 0;
     bool paired = false;
@@ -246,6 +249,13 @@ struct Pack {
     ByteBuf out_text[2];
     fq_text_out tout{};
     int max_len[2] = {0, 0};
+
+    // raw-stream pack (fq_engine_raw_*): the engine cut the records from the input bytes; its
+    // trimmed-adapter entries land in ad[m]; its staging window is recycled once the pack is reported
+    bool raw = false;
+    fq_raw_out rout{};
+    ByteBuf ad[2];
+    int stage = -1;  // the raw driver's staging window of the pack's input bytes
 
     // -c: pairs whose bases the engine corrected read their seq/qual from a corrected copy
     // (fix[i] -> seq1 qual1 seq2 qual2 back to back; nullptr = the original text)
@@ -292,6 +302,10 @@ class PackReader {
     bool next(Pack& pk, size_t max_n, Pool* pool = nullptr);
     bool paired() const { return paired_; }
     uint64_t reads_seen() const { return reads_; }
+    // continue at stream offsets off1 / off2 (mapped regular files only: where the GPU's raw
+    // stream stopped), numbering packs from first_seq
+    void seek(uint64_t off1, uint64_t off2, uint64_t first_seq);
+    bool mapped() const { return r1_.mapped() && (!r2_ || r2_->mapped()); }
     double parse_s = 0, tiles_s = 0;  // time spent parsing records / filling batch planes
     bool defer_tiles = false;         // next() leaves pack_tiles to the caller (another thread)
 

@@ -264,7 +264,7 @@ HNode stats_contents(const Summary& st, const std::string& filtering, const std:
 }
 
 // FilterResult::reportAdaptersHtmlDetails, src/filterresult.cpp:267-306
-HNode adapter_details(const std::map<std::string, size_t>& counts) {
+HNode adapter_details(const AdapterCounts::Report& rep) {
     HNode table("table.summary_table");
     HNode head("tr");
     HNode c1("td.adapter_col", "Sequence");
@@ -273,12 +273,11 @@ HNode adapter_details(const std::map<std::string, size_t>& counts) {
     c2.attr("style", "font-size:14px;color:#ffffff;background:#556699");
     head.add(c1).add(c2);
     table.add(head);
-    size_t total = 0;
-    for (auto& e : counts) total += e.second;
+    const size_t total = rep.total;
     if (total == 0) return table;
     const double dt = (double)total;
     size_t reported = 0;
-    for (auto& e : counts) {
+    for (auto& e : rep.top) {
         if (e.second / dt < 0.01) continue;
         HNode r("tr");
         r.add(HNode("td.adapter_col", e.first));
@@ -494,13 +493,11 @@ std::string build_html(const Options& o, const HostAcc& a, const AdapterCounts& 
     pre_t.add(row2("Read1 Mean Length", pre1.mean_length()));
     if (pe) pre_t.add(row2("Read2 Mean Length", pe ? pre2.mean_length() : 0));
     if (o.adapter_trimming) {
-        size_t with = 0;
-        for (auto& e : ac.r1) with += e.second;
+        size_t with = ac.report(0).total;
         double r = pe ? with * 1.0 / pre_reads * 2 : with * 1.0 / pre_reads;
         pre_t.add(row2("Read1 Adapters Left", std::to_string(with) + "(" + fstr(r * 100) + "%)"));
         if (pe) {
-            with = 0;
-            for (auto& e : ac.r2) with += e.second;
+            with = ac.report(1).total;
             r = with * 1.0 / pre_reads * 2;
             pre_t.add(row2("Read2 Adapters Left", std::to_string(with) + "(" + fstr(r * 100) + "%)"));
         }
@@ -550,12 +547,12 @@ std::string build_html(const Options& o, const HostAcc& a, const AdapterCounts& 
         sec.add(section_title("Adapters", "adapters"));
         HNode ids("div#adapters");
         HNode a1("div#read1_adapters");
-        a1.add(adapter_details(ac.r1));
+        a1.add(adapter_details(ac.report(0)));
         ids.add(subsection("Adapter or bad ligation of read1", "read1_adapters"));
         ids.add(a1);
         if (pe) {
             HNode a2("div#read2_adapters");
-            a2.add(adapter_details(ac.r2));
+            a2.add(adapter_details(ac.report(1)));
             ids.add(subsection("Adapter or bad ligation of read2", "read2_adapters"));
             ids.add(a2);
         }

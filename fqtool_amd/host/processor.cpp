@@ -15,6 +15,11 @@
 #include <future>
 #include <thread>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include "evaluator.h"
 
 namespace fqhost {
@@ -393,6 +398,10 @@ class Queue {  // bounded FIFO between pipeline threads; push/pop return at once
         not_empty_.notify_all();
         not_full_.notify_all();
     }
+    void reopen() {
+        std::lock_guard<std::mutex> l(m_);
+        closed_ = false;
+    }
 
    private:
     size_t cap_;
@@ -759,6 +768,8 @@ namespace {
 
 int round16(int x) { return (x + 15) & ~15; }
 
+bool ends_with_gz(const std::string& f) { return f.size() >= 3 && f.compare(f.size() - 3, 3, ".gz") == 0; }
+
 double since(std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
 }
@@ -784,6 +795,8 @@ struct Lane {
     std::thread t;
     std::exception_ptr err;
     double tiles_s = 0, submit_s = 0, wait_s = 0;
+    double first_submit = -1;  // seconds from t_start to this engine's first submission
+    std::chrono::steady_clock::time_point t_start = std::chrono::steady_clock::now();
 
     void make(const Options& o, int cycles, int batch, int stride) {
         if (e) fq_engine_destroy(e);
@@ -820,6 +833,11 @@ struct Lane {
         wait_s += since(e0);
         if (rc != 1) throw std::runtime_error(std::string("fq_engine_poll: ") + fq_engine_last_error(e));
         if (seq != pk->seq_no) throw std::runtime_error("engine completed packs out of order");
+        if (pk->raw) {  // its input window was copied: recycle the staging; the output sizes are in
+            if (pk->stage >= 0) free_stages.push(pk->stage);
+            pk->stage = -1;
+            pk->tout = pk->rout.text;
+        }
         if (!out.push(std::move(pk))) throw Stopped();
     }
 
@@ -842,6 +860,256 @@ struct Lane {
                 throw std::runtime_error(std::string("fq_engine_submit: ") + fq_engine_last_error(e));
         }
         submit_s += since(e0);
+    }
+
+    // Raw-stream ingest (fq_engine_raw_*, include/fqengine.h): the inputs (regular files) go to
+    // the GPU in consecutive windows; the engine cuts the records, pairs the mates and runs the
+    // pack.  A reader thread fills page-locked staging windows with parallel preads on the pool
+    // (no mapping, no registration: the copies are plain DMA) while this thread enqueues them and
+    // launches the packs.  Windows are sized to bring about `target` pairs per pack from what the
+    // packs so far took per pair and left over (published after every launch).  Ends at the end
+    // of the input (done) or where the GPU path stops (an irregular record, no progress, bytes
+    // left at the end): the host reader then resumes at the returned stream offsets, pack numbers
+    // continuing.
+    struct RawResume {
+        bool done = false;
+        uint64_t off[2] = {0, 0};
+        uint64_t next_seq = 0;
+    };
+    struct Stage {  // one window's staging buffers (one per mate)
+        Stage() : buf{ByteBuf(true), ByteBuf(true)} {}
+        ByteBuf buf[2];
+    };
+    std::vector<std::unique_ptr<Stage>> stages;
+    Queue<int> free_stages{64};
+    uint64_t raw_pairs = 0, raw_packs = 0;  // what the raw stream took
+    std::string raw_end;                    // why it ended
+
+    RawResume run_raw(const std::string* files, int mates, int target, Queue<std::unique_ptr<Pack>>& spare, Pool& pool) {
+        RawResume rr;
+        int fd[2] = {-1, -1};
+        uint64_t size[2] = {0, 0};
+        auto close_all = [&] {
+            for (int& f : fd)
+                if (f >= 0) {
+                    ::close(f);
+                    f = -1;
+                }
+        };
+        for (int m = 0; m < mates; ++m) {
+            fd[m] = ::open(files[m].c_str(), O_RDONLY);
+            struct stat st;
+            if (fd[m] < 0 || fstat(fd[m], &st) != 0 || !S_ISREG(st.st_mode) || st.st_size <= 0) {
+                close_all();
+                return rr;  // (the host reader takes the whole input)
+            }
+            size[m] = (uint64_t)st.st_size;
+            (void)posix_fadvise(fd[m], 0, 0, POSIX_FADV_SEQUENTIAL);
+        }
+        const uint64_t wcap = (uint64_t)128 << 20, ccap = (uint64_t)32 << 20;
+        if (fq_engine_raw_begin(e, wcap, ccap) != FQ_OK)
+            throw std::runtime_error(std::string("fq_engine_raw_begin: ") + fq_engine_last_error(e));
+        const int kStages = depth + 4;  // enqueued (2) + in flight (depth) + being filled
+        while ((int)stages.size() < kStages) {
+            stages.emplace_back(new Stage);
+            free_stages.push((int)stages.size() - 1);
+        }
+        struct Win {
+            uint64_t start[2] = {0, 0}, n[2] = {0, 0};
+            int stage = -1;
+            uint64_t id = 0;
+        };
+        // published by this thread after each launch, read by the window reader
+        std::mutex fb_m;
+        double bpr[2] = {0, 0};      // text bytes per record of the packs so far
+        uint64_t carry[2] = {0, 0};  // after the last launched window
+        uint64_t launched = 0;       // windows launched
+        Queue<Win> ready(2);
+        std::exception_ptr rd_err;
+        const char* w0_env = std::getenv("FQ_RAW_WINDOW0");  // first window's bytes (tests: tiny windows)
+        const uint64_t w0 = w0_env ? std::max<uint64_t>(4096, std::strtoull(w0_env, nullptr, 10)) : (uint64_t)4 << 20;
+        std::thread rd([&] {  // the window reader
+            try {
+                uint64_t pos[2] = {0, 0};
+                std::deque<Win> made;  // windows produced and (maybe) not yet launched
+                for (uint64_t id = 0;; ++id) {
+                    bool more = false;
+                    for (int m = 0; m < mates; ++m) more = more || pos[m] < size[m];
+                    if (!more) break;
+                    double b[2], pairs_held = 1e18;
+                    uint64_t held[2];
+                    {
+                        std::lock_guard<std::mutex> g(fb_m);
+                        while (!made.empty() && made.front().id < launched) made.pop_front();
+                        for (int m = 0; m < 2; ++m) {
+                            b[m] = bpr[m];
+                            held[m] = carry[m];
+                        }
+                    }
+                    for (const Win& q : made)
+                        for (int m = 0; m < mates; ++m) held[m] += q.n[m];
+                    for (int m = 0; m < mates; ++m) pairs_held = std::min(pairs_held, b[m] > 0 ? held[m] / b[m] : 0.0);
+                    Win w;
+                    w.id = id;
+                    for (int m = 0; m < mates; ++m) {
+                        uint64_t want;
+                        if (b[m] <= 0) {
+                            want = w0;
+                        } else {
+                            const double after = held[m] - std::min(pairs_held, (double)target) * b[m];
+                            const double need = target * b[m] * 1.02 - std::max(0.0, after);
+                            want = need <= 0 ? 0 : (uint64_t)need;
+                        }
+                        w.start[m] = pos[m];
+                        w.n[m] = std::min(std::min<uint64_t>((want + 4095) / 4096 * 4096, wcap), size[m] - pos[m]);
+                        pos[m] += w.n[m];
+                    }
+                    if (!free_stages.pop(w.stage)) break;
+                    Stage& st = *stages[(size_t)w.stage];
+                    const uint64_t piece = (uint64_t)4 << 20;
+                    int pieces[2] = {0, 0};
+                    for (int m = 0; m < mates; ++m) {
+                        st.buf[m].resize_uninit((size_t)std::max<uint64_t>(w.n[m], 1));
+                        pieces[m] = (int)((w.n[m] + piece - 1) / piece);
+                    }
+                    std::atomic<bool> short_read{false};
+                    pool.run(pieces[0] + pieces[1], [&](int k) {
+                        const int m = k < pieces[0] ? 0 : 1;
+                        const uint64_t o = (uint64_t)(m ? k - pieces[0] : k) * piece;
+                        const uint64_t len = std::min(piece, w.n[m] - o);
+                        uint64_t got = 0;
+                        while (got < len) {
+                            const ssize_t r = pread(fd[m], st.buf[m].data() + o + got, (size_t)(len - got), (off_t)(w.start[m] + o + got));
+                            if (r <= 0) {
+                                short_read = true;
+                                return;
+                            }
+                            got += (uint64_t)r;
+                        }
+                    });
+                    if (short_read) throw std::runtime_error("input file changed while reading");
+                    made.push_back(w);
+                    if (!ready.push(w)) break;
+                }
+            } catch (...) {
+                rd_err = std::current_exception();
+            }
+            ready.close();
+        });
+        std::deque<Win> wins;  // enqueued, not launched
+        bool input_done = false;
+        auto enqueue_next = [&]() -> bool {
+            Win w;
+            if (input_done || !ready.pop(w)) {
+                input_done = true;
+                return false;
+            }
+            Stage& st = *stages[(size_t)w.stage];
+            fq_raw_window rw{};
+            for (int m = 0; m < mates; ++m) {
+                rw.bytes[m] = st.buf[m].data();
+                rw.n[m] = w.n[m];
+            }
+            if (fq_engine_raw_enqueue(e, &rw) != FQ_OK) {
+                free_stages.push(w.stage);
+                throw std::runtime_error(std::string("fq_engine_raw_enqueue: ") + fq_engine_last_error(e));
+            }
+            wins.push_back(w);
+            return true;
+        };
+        uint64_t seq = 0;
+        auto finish = [&] {
+            ready.close();
+            free_stages.close();  // (a reader waiting for a stage stops)
+            rd.join();
+            free_stages.reopen();
+        };
+        try {
+            if (enqueue_next()) {
+                for (;;) {
+                    if (wins.size() < 2) enqueue_next();
+                    const Win w = wins.front();
+                    wins.pop_front();
+                    std::unique_ptr<Pack> pk;
+                    if (!spare.pop(pk)) throw Stopped();
+                    pk->clear();
+                    pk->raw = true;
+                    pk->text_mode = true;
+                    pk->paired = mates == 2;
+                    pk->seq_no = seq;
+                    pk->stage = w.stage;
+                    uint64_t cin[2];
+                    {
+                        std::lock_guard<std::mutex> g(fb_m);
+                        cin[0] = carry[0];
+                        cin[1] = carry[1];
+                    }
+                    for (int m = 0; m < 2; ++m) {
+                        const size_t cap = m < mates ? (size_t)(cin[m] + w.n[m] + 64) : 0;
+                        pk->out_text[m].resize_uninit(cap);
+                        pk->ad[m].resize_uninit(cap);
+                        pk->rout.text.text[m] = m < mates ? pk->out_text[m].data() : nullptr;
+                        pk->rout.adapters[m] = m < mates ? pk->ad[m].data() : nullptr;
+                        pk->rout.adapter_cap[m] = cap;
+                    }
+                    fq_raw_result r{};
+                    const auto e0 = std::chrono::steady_clock::now();
+                    if (fq_engine_raw_launch(e, &r, &pk->rout, seq) != FQ_OK)
+                        throw std::runtime_error(std::string("fq_engine_raw_launch: ") + fq_engine_last_error(e));
+                    submit_s += since(e0);
+                    if (first_submit < 0) first_submit = since(t_start);
+                    pk->n = r.pairs;
+                    pk->max_cycles = max_cycles;
+                    {
+                        std::lock_guard<std::mutex> g(fb_m);
+                        for (int m = 0; m < mates; ++m) {
+                            carry[m] = r.carry[m];
+                            if (r.pairs > 0)
+                                bpr[m] = bpr[m] > 0 ? 0.5 * bpr[m] + 0.5 * (double)r.text_bytes[m] / r.pairs
+                                                    : (double)r.text_bytes[m] / r.pairs;
+                        }
+                        launched = w.id + 1;
+                    }
+                    if ((int)inflight.size() >= depth) complete_oldest();
+                    inflight.push_back(std::move(pk));
+                    ++seq;
+                    if (wins.empty()) enqueue_next();
+                    const bool last = wins.empty() && input_done;
+                    bool left = false;
+                    for (int m = 0; m < mates; ++m) left = left || r.carry[m] > 0;
+                    raw_pairs += (uint64_t)r.pairs;
+                    ++raw_packs;
+                    if (r.stop || r.pairs == 0 || last) {
+                        rr.done = last && !left && !r.stop;
+                        raw_end = rr.done ? "end of input"
+                                          : std::string(r.stop ? "irregular record" : r.pairs == 0 ? "no pairs" : "bytes left at the end") +
+                                                " after pack " + std::to_string(seq - 1) + " (window bytes " + std::to_string(w.n[0]) + "/" +
+                                                std::to_string(w.n[1]) + ", carry " + std::to_string(r.carry[0]) + "/" +
+                                                std::to_string(r.carry[1]) + ", max_len " + std::to_string(r.max_len) + ")";
+                        for (int m = 0; m < mates; ++m) rr.off[m] = w.start[m] + w.n[m] - r.carry[m];
+                        break;
+                    }
+                }
+            } else {
+                rr.done = false;  // (nothing to read: the host reader reports the empty input)
+            }
+            while (!inflight.empty()) complete_oldest();
+            // windows enqueued after the stop are dropped once their copies are done
+            (void)fq_engine_sync(e);
+            for (const Win& w : wins) free_stages.push(w.stage);
+            wins.clear();
+            finish();
+            if (rd_err) std::rethrow_exception(rd_err);
+        } catch (...) {
+            (void)fq_engine_sync(e);
+            inflight.clear();
+            finish();
+            close_all();
+            throw;
+        }
+        close_all();
+        rr.next_seq = seq;
+        return rr;
     }
 
     // the dispatcher: planes (or the text index) of each pack, submit, completions in order
@@ -877,6 +1145,7 @@ struct Lane {
                 if ((int)inflight.size() >= depth) complete_oldest();
                 pk->max_cycles = max_cycles;  // (read by the formatter)
                 submit(*pk, as_text);
+                if (first_submit < 0) first_submit = since(t_start);
                 inflight.push_back(std::move(pk));
             }
             while (!inflight.empty()) complete_oldest();
@@ -1006,6 +1275,15 @@ int run_tool(int argc, char** argv) {
             return d;
         });
     }
+    // FQ_TIMING=1: the time the pipeline's teardown (pinned packs, engines, pool, mappings) takes
+    // after the summary line, on stderr once everything is destroyed
+    struct TeardownClock {
+        std::chrono::steady_clock::time_point t0, logged;
+        bool on = false;
+        ~TeardownClock() {
+            if (on) std::cerr << "fqtool-amd timing: teardown " << since(logged) << " s, total " << since(t0) << " s" << std::endl;
+        }
+    } teardown{t0, t0, std::getenv("FQ_TIMING") != nullptr};
     try {
         const bool paired = o.paired();
         const size_t pack_n = o.pack_pairs ? o.pack_pairs : std::max<size_t>(o.max_reads_in_pack, 262144);
@@ -1036,6 +1314,7 @@ int run_tool(int argc, char** argv) {
         const int cyc0 = std::max(16, round16(o.merge ? 2 * est : est)), stride0 = round16(std::max(est, 16));
         for (int g = 0; g < G; ++g) {
             lanes.emplace_back(new Lane(devices[(size_t)g], depth));
+            lanes.back()->t_start = t0;
             lanes.back()->make(o, cyc0, (int)pack_n, stride0);
         }
         std::exception_ptr reader_err, format_err;
@@ -1052,8 +1331,23 @@ int run_tool(int argc, char** argv) {
         // (owned here, not by the reader thread: packs in flight point into its file mappings)
         PackReader pr(o.in1, o.in2, o.interleaved, o.phred64);
         pr.defer_tiles = true;  // the dispatchers fill the planes while the reader parses on
+        // GPU-side record indexing (fq_engine_raw_*) for plain files on one engine: the engine's
+        // dispatcher drives the raw stream first; the host reader takes over only where it stops
+        const char* raw_env = std::getenv("FQ_RAW_MODE");
+        const bool raw_mode = text_mode && G == 1 && !o.interleaved && !(raw_env && std::string(raw_env) == "0") &&
+                              pr.mapped() && !ends_with_gz(o.in1) && (!paired || !ends_with_gz(o.in2));
+        std::promise<Lane::RawResume> raw_p;
+        std::shared_future<Lane::RawResume> raw_f = raw_p.get_future().share();
         std::thread reader([&] {
             try {
+                if (raw_mode) {  // wait for the raw stream's end; resume where it stopped
+                    const Lane::RawResume rr = raw_f.get();
+                    if (rr.done) {
+                        for (auto& l : lanes) l->in.close();
+                        return;
+                    }
+                    pr.seek(rr.off[0], rr.off[1], rr.next_seq);
+                }
                 std::unique_ptr<Pack> pk;
                 for (;;) {
                     const auto w0 = std::chrono::steady_clock::now();
@@ -1073,6 +1367,18 @@ int run_tool(int argc, char** argv) {
             Lane* l = lp.get();
             l->t = std::thread([&, l] {
                 try {
+                    if (raw_mode) {
+                        Lane::RawResume rr;
+                        rr.done = true;
+                        try {
+                            const std::string files[2] = {o.in1, o.in2};
+                            rr = l->run_raw(files, paired ? 2 : 1, (int)pack_n, spare, pool);
+                        } catch (...) {
+                            raw_p.set_value(rr);
+                            throw;
+                        }
+                        raw_p.set_value(rr);
+                    }
                     l->run(o, text_mode, pool, acc, acc_m);
                 } catch (const Stopped&) {  // (the stage that failed reports)
                 } catch (...) {
@@ -1093,7 +1399,13 @@ int run_tool(int argc, char** argv) {
                     if (pk->seq_no != k) throw std::runtime_error("packs reached the formatter out of order");
                     const fq_params p = o.to_params(pk->max_cycles);
                     if (pk->text_mode) {  // the engine wrote the output text
-                        if (o.adapter_trimming) ac.add(*pk, pk->res.data(), p, &pool);
+                        if (o.adapter_trimming) {
+                            if (pk->raw)
+                                for (int m = 0; m < (paired ? 2 : 1); ++m)
+                                    ac.add_entries(m, pk->ad[m].data(), pk->rout.adapter_bytes[m], p);
+                            else
+                                ac.add(*pk, pk->res.data(), p, &pool);
+                        }
                         format_s += since(f0);
                         reads += (uint64_t)pk->n * (paired ? 2 : 1);
                         // the writers recycle the pack once its output text is written
@@ -1117,6 +1429,7 @@ int run_tool(int argc, char** argv) {
         for (auto& l : lanes) l->t.join();
         formatter.join();
         reader.join();
+        const double pipeline_done_s = since(t0);
         double tiles_s = 0, submit_s = 0, wait_s = 0;
         std::exception_ptr lane_err;
         for (auto& l : lanes) {
@@ -1161,11 +1474,16 @@ int run_tool(int argc, char** argv) {
             std::ofstream hs(o.html_file, std::ios::binary);
             hs << build_html(o, acc, ac, html_time_now());
         }
+        teardown.logged = std::chrono::steady_clock::now();
         log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s)" +
-            (text_mode ? " (text packs: GPU ingest/egress)" : "") + ", wall " +
+            (raw_mode ? " (raw stream: GPU record indexing, ingest/egress: " + std::to_string(lanes[0]->raw_pairs) + " pairs in " +
+                            std::to_string(lanes[0]->raw_packs) + " packs, ended: " + lanes[0]->raw_end + ")"
+                      : text_mode ? " (text packs: GPU ingest/egress)" : "") + ", wall " +
             std::to_string(since(t0)) + " s, engine submit " + std::to_string(submit_s) + " s, wait " + std::to_string(wait_s) + " s; pre-pass " +
             std::to_string(prepass_s) + " s, adapter detection (concurrent) " + std::to_string(detect_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +
             " s, tiles " + std::to_string(tiles_s) + " s, reader waiting " + std::to_string(spare_wait_s) +
+            " s, first pack submitted at " + std::to_string(lanes[0]->first_submit) + " s, pipeline done at " +
+            std::to_string(pipeline_done_s) +
             " s; JSON report " + o.json_file + ", HTML report " + o.html_file);
     } catch (const std::exception& e) {
         if (det.valid()) det.wait();  // the pre-pass's messages come first, as in the reference

@@ -2,6 +2,7 @@
 #include "report.h"
 
 #include <algorithm>
+#include <cstring>
 #include <numeric>
 #include <string_view>
 #include <unordered_map>
@@ -30,12 +31,92 @@ void HostAcc::add(const uint64_t* acc, int max_cycles) {
     for (int j = 0; j < FQ_ACC_TAIL_WORDS; ++j) tail_[j] += t[j];
 }
 
+namespace {
+uint64_t hash_bytes(const char* s, size_t n) {  // FNV-1a 64 over 8-byte words, then a final mix
+    uint64_t h = 0xcbf29ce484222325ull ^ n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, s + i, 8);
+        h = (h ^ w) * 0x100000001b3ull;
+    }
+    uint64_t w = 0;
+    if (i < n) std::memcpy(&w, s + i, n - i);
+    h = (h ^ w) * 0x100000001b3ull;
+    h ^= h >> 29;
+    h *= 0xbf58476d1ce4e5b9ull;
+    return h ^ (h >> 32);
+}
+}  // namespace
+
+// one shard: open addressing over (hash, string) with the strings in a byte arena
+struct AdapterCounts::Shard {
+    struct Slot {
+        uint64_t h = 0;
+        uint64_t off = 0;
+        uint32_t len = 0;
+        uint32_t used = 0;
+        size_t count = 0;
+    };
+    std::vector<Slot> slots = std::vector<Slot>(256);
+    std::string arena;
+    size_t n = 0;
+    void bump(uint64_t h, const char* s, uint32_t len, size_t c) {
+        size_t mask = slots.size() - 1, i = (h >> 6) & mask;
+        for (;; i = (i + 1) & mask) {
+            Slot& x = slots[i];
+            if (!x.used) break;
+            if (x.h == h && x.len == len && std::memcmp(arena.data() + x.off, s, len) == 0) {
+                x.count += c;
+                return;
+            }
+        }
+        Slot& x = slots[i];
+        x.used = 1;
+        x.h = h;
+        x.len = len;
+        x.off = arena.size();
+        x.count = c;
+        arena.append(s, len);
+        if (++n * 2 > slots.size()) grow();
+    }
+    void grow() {
+        std::vector<Slot> old(slots.size() * 2);
+        old.swap(slots);
+        const size_t mask = slots.size() - 1;
+        for (const Slot& x : old)
+            if (x.used) {
+                size_t i = (x.h >> 6) & mask;
+                while (slots[i].used) i = (i + 1) & mask;
+                slots[i] = x;
+            }
+    }
+};
+
+AdapterCounts::AdapterCounts() {
+    for (int m = 0; m < 2; ++m)
+        for (int k = 0; k < kShards; ++k) shards_[m].emplace_back(new Shard);
+}
+AdapterCounts::~AdapterCounts() = default;
+
+void AdapterCounts::add(int mate, const std::string& a, size_t count) {
+    const uint64_t h = hash_bytes(a.data(), a.size());
+    shards_[mate][h % kShards]->bump(h, a.data(), (uint32_t)a.size(), count);
+}
+
 void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_params& p, Pool* pool) {
     const int mates = pk.paired ? 2 : 1;
     const int parts = pool ? std::max(1, std::min(pool->size() * 2, (pk.n + 16383) / 16384)) : 1;
-    std::vector<std::unordered_map<std::string_view, size_t>> local((size_t)parts * 2);
-    auto work = [&](int k) {
+    struct Item {
+        uint64_t h;
+        const char* s;
+        uint32_t len;
+    };
+    // items[part][mate * kShards + shard]: the part's trimmed tails of that shard
+    std::vector<std::vector<std::vector<Item>>> items((size_t)parts, std::vector<std::vector<Item>>((size_t)(2 * kShards)));
+    auto hash_part = [&](int k) {
         const int i0 = (int)((int64_t)pk.n * k / parts), i1 = (int)((int64_t)pk.n * (k + 1) / parts);
+        auto& it = items[(size_t)k];
         for (int i = i0; i < i1; ++i) {
             for (int m = 0; m < mates; ++m) {
                 const fq_read_result& r = res[(size_t)i * mates + m];
@@ -43,15 +124,54 @@ void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_para
                 const char* s = (r.flags & FQ_RF_AD_NEG)
                                     ? reinterpret_cast<const char*>(m ? p.adapter2 : p.adapter1) + r.ad_pos
                                     : pk.seq_text(m, (size_t)i) + r.ad_pos;
-                ++local[(size_t)(2 * k + m)][std::string_view(s, r.ad_len)];
+                const uint64_t h = hash_bytes(s, r.ad_len);
+                it[(size_t)(m * kShards) + h % kShards].push_back(Item{h, s, r.ad_len});
             }
         }
     };
-    if (pool) pool->run(parts, work);
-    else work(0);
-    for (int k = 0; k < parts; ++k)
-        for (int m = 0; m < mates; ++m)
-            for (const auto& kv : local[(size_t)(2 * k + m)]) (m ? r2 : r1)[std::string(kv.first)] += kv.second;
+    auto merge_shard = [&](int j) {  // j = mate * kShards + shard
+        Shard& sh = *shards_[j / kShards][(size_t)(j % kShards)];
+        for (int k = 0; k < parts; ++k)
+            for (const Item& x : items[(size_t)k][(size_t)j]) sh.bump(x.h, x.s, x.len, 1);
+    };
+    if (pool) {
+        pool->run(parts, hash_part);
+        pool->run(mates * kShards, merge_shard);
+    } else {
+        hash_part(0);
+        for (int j = 0; j < mates * kShards; ++j) merge_shard(j);
+    }
+}
+
+void AdapterCounts::add_entries(int m, const char* d, size_t bytes, const fq_params& p) {
+    const char* ad = reinterpret_cast<const char*>(m ? p.adapter2 : p.adapter1);
+    for (size_t o = 0; o + 3 <= bytes;) {
+        const uint32_t len = (uint8_t)d[o] | ((uint32_t)(uint8_t)d[o + 1] << 8);
+        const char* s;
+        if (d[o + 2]) {
+            const uint32_t pos = (uint8_t)d[o + 3] | ((uint32_t)(uint8_t)d[o + 4] << 8);
+            s = ad + pos;
+            o += 5;
+        } else {
+            s = d + o + 3;
+            o += 3 + (size_t)len;
+        }
+        const uint64_t h = hash_bytes(s, len);
+        shards_[m][h % kShards]->bump(h, s, len, 1);
+    }
+}
+
+AdapterCounts::Report AdapterCounts::report(int m) const {
+    Report r;
+    for (const auto& sh : shards_[m])
+        for (const Shard::Slot& x : sh->slots)
+            if (x.used) r.total += x.count;
+    if (r.total == 0) return r;
+    const double dt = (double)r.total;
+    for (const auto& sh : shards_[m])
+        for (const Shard::Slot& x : sh->slots)
+            if (x.used && !(x.count / dt < 0.01)) r.top[sh->arena.substr(x.off, x.len)] = x.count;
+    return r;
 }
 
 namespace {
@@ -134,14 +254,13 @@ Summary summarize(const HostAcc& a, int k) {
 namespace {
 
 // FilterResult::reportAdaptersJsonDetails, src/filterresult.cpp:231-251 (null when no adapters)
-Json adapter_details(const std::map<std::string, size_t>& m) {
-    size_t total = 0;
-    for (auto& e : m) total += e.second;
+Json adapter_details(const AdapterCounts::Report& rep) {
+    const size_t total = rep.total;
     Json j;
     if (total == 0) return j;
     const double dt = (double)total;
     size_t reported = 0;
-    for (auto& e : m) {
+    for (auto& e : rep.top) {
         if (e.second / dt < 0.01) continue;
         j[e.first] = Json::u(e.second);
         reported += e.second;
@@ -247,8 +366,8 @@ Json build_report(const Options& o, const HostAcc& a, const AdapterCounts& ac) {
         at["AdapterTrimmedBases"] = Json::u(a.head()[FQ_ACC_ADAPTER_BASES]);
         at["Read1AdapterSequence"] = Json::s(!o.adapter1.empty() ? o.adapter1 : o.detected_adapter1);
         if (paired) at["Read2AdapterSequence"] = Json::s(!o.adapter2.empty() ? o.adapter2 : o.detected_adapter2);
-        at["Read1AdapterCounts"] = adapter_details(ac.r1);
-        if (paired) at["Read2AdapterCounts"] = adapter_details(ac.r2);
+        at["Read1AdapterCounts"] = adapter_details(ac.report(0));
+        if (paired) at["Read2AdapterCounts"] = adapter_details(ac.report(1));
         rep["AdapterTrim"] = at;
     }
 

@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -52,14 +53,33 @@ class HostAcc {
     uint64_t tail_[FQ_ACC_TAIL_WORDS] = {};
 };
 
-// FilterResult's adapter string -> count maps (src/filterresult.cpp:138-177)
-// FilterResult's adapter-string counts (src/filterresult.cpp:138-177): each trimmed tail's text is
-// sliced from the pack; ranges of a pack are counted on the pool in hash maps of views into
-// the pack, then merged into the ordered maps the report walks.
+// FilterResult's adapter-string counts (src/filterresult.cpp:138-177).  Every trimmed tail's text
+// is sliced from the pack and counted exactly, keyed by its bytes, in a table split into shards by
+// hash: a pack's ranges are hashed on the pool, then each shard takes its entries of every range
+// (no serial merge).  The reports only print the strings holding >= 1 % of a mate's total, plus
+// "Others" (src/filterresult.cpp:231-251); report() returns those, in the map order the
+// reference prints, with the total.
 class Pool;
-struct AdapterCounts {
-    std::map<std::string, size_t> r1, r2;
+class AdapterCounts {
+   public:
+    static constexpr int kShards = 64;
+    AdapterCounts();
+    ~AdapterCounts();
+    AdapterCounts(const AdapterCounts&) = delete;
+    AdapterCounts& operator=(const AdapterCounts&) = delete;
     void add(const Pack& pk, const fq_read_result* res, const fq_params& p, Pool* pool = nullptr);
+    void add(int mate, const std::string& adapter, size_t count);  // one string (tests, report API)
+    // a raw pack's trimmed-adapter entries of one mate (fq_raw_out, include/fqengine.h)
+    void add_entries(int mate, const char* entries, size_t bytes, const fq_params& p);
+    struct Report {
+        std::map<std::string, size_t> top;  // the strings at >= 1 % of total (FilterResult's test)
+        size_t total = 0;                   // adapter-trimmed reads of the mate
+    };
+    Report report(int mate) const;
+
+   private:
+    struct Shard;
+    std::vector<std::unique_ptr<Shard>> shards_[2];
 };
 
 // Stats::summarize + reportJson for accumulator stats block k (src/stats.cpp:147-228, :392-430)

@@ -382,10 +382,62 @@ typedef struct fq_text_out {
 int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result* results, fq_text_out* out,
                           uint64_t seq_no);
 
-/* Page-locked host memory for packs and records (hipHostMalloc, portable across devices).
- * FQ_E_NO_DEVICE without a HIP device: callers then use ordinary memory. */
+/* ---- raw FASTQ streams: record indexing on the GPU ------------------------------------------
+ * Replaces the reader too (FqReader::read over its 1 MiB buffers and FqReaderPair::read,
+ * src/fqreader.cpp:90-195, :254-267) for the plain part of an input, on top of the text-pack
+ * path above.  The caller hands each mate's input bytes over in consecutive windows of any size
+ * (fq_engine_raw_enqueue; page-locked or registered host memory, fq_host_register, makes the copy
+ * asynchronous).  On the device each window's text is the previous window's bytes after its last
+ * taken record followed by the new bytes; the line terminators ('\n' and '\r') are indexed and
+ * record i is lines 4i .. 4i+3 while records are "plain": all four lines end in '\n' and are
+ * non-empty, the first starts with '@', quality and sequence are equally long, name/strand lines
+ * are < 65536 bytes and the sequence <= the engine's max_stride and max_cycles.  On plain records
+ * the reference reader is exactly "four lines per record" (no '@' search, no "\r\n" folding at its
+ * buffer ends, no length error).  A window's pack is the leading plain records (PE: pairs, the
+ * minimum over the mates), up to max_batch; fq_engine_raw_launch runs it as a text pack.
+ *   fq_raw_result.stop != 0: a complete record that is not plain follows the pack (or the carry
+ *   overflowed): the caller continues with its own reader at each mate's stream offset
+ *   (end of the window's bytes) - carry[m].  The same applies when the input ended (every mate's
+ *   last window enqueued) with carry left, or a window takes no pairs.
+ * Protocol: fq_engine_raw_begin; enqueue window 0; then for k = 0, 1, ...: enqueue window k+1
+ * (optional), fq_engine_raw_launch (window k: waits for its index), poll as for other packs.  At
+ * most two windows are enqueued and not launched; a window's host bytes must stay valid until its
+ * pack is reported by fq_engine_poll.  Options as for text packs (no -m, -c, UMI, index filter).
+ * The trimmed-adapter strings (FilterResult::addAdapterTrimmed, src/filterresult.cpp:138-157) come
+ * back as entries "u16 ad_len (little endian), u8 neg, then ad_len bytes of the read (neg 0) or
+ * u16 ad_pos (neg 1: the string is adapter[ad_pos, ad_pos + ad_len) of the mate's adapter
+ * parameter)", copied by fq_engine_poll into out->adapters[m] (exact size, <= adapter_cap[m]). */
+typedef struct fq_raw_window {
+    const char* bytes[2]; /* mate m's next input bytes (bytes[1]: PE only) */
+    uint64_t n[2];        /* their count, <= the window capacity given to fq_engine_raw_begin */
+} fq_raw_window;
+typedef struct fq_raw_result {
+    int32_t pairs;      /* records (PE: pairs) in the window's pack */
+    int32_t stop;       /* nonzero: the GPU path cannot continue after this pack (see above) */
+    int32_t max_len;    /* longest sequence of the pack */
+    int32_t pad;
+    uint64_t carry[2];  /* mate m's bytes after the pack's last record (they stay on the device) */
+    uint64_t text_bytes[2]; /* mate m's text bytes the pack's records span */
+} fq_raw_result;
+typedef struct fq_raw_out {
+    fq_text_out text;          /* text[m]: >= carry capacity + window capacity + 16 bytes */
+    char* adapters[2];         /* trimmed-adapter entries of mate m */
+    uint64_t adapter_cap[2];
+    uint64_t adapter_bytes[2]; /* set by fq_engine_poll */
+} fq_raw_out;
+int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap);
+int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w);
+int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64_t seq_no);
+
+/* Page-locked host memory for packs and records (portable across devices; transparent huge
+ * pages registered with the runtime, hipHostMalloc as fallback).  FQ_E_NO_DEVICE without a HIP
+ * device: callers then use ordinary memory. */
 int fq_host_alloc(size_t bytes, void** out);
 int fq_host_free(void* p);
+/* Page-lock an existing host range (e.g. of a read-only file mapping, page-aligned) so copies
+ * from it are asynchronous DMA; fq_host_unregister releases it. */
+int fq_host_register(const void* p, size_t bytes);
+int fq_host_unregister(const void* p);
 
 /* Accumulators */
 size_t fq_engine_acc_words(const fq_engine* e);

@@ -116,3 +116,35 @@ def test_split_with_several_workers(case, host, oracle, tmp_path):
         assert sorted(records(one, mate)) == sorted(records(three, mate))
     names = sorted(os.path.basename(f) for f in glob.glob(str(three / "0*")))
     assert names[0].startswith("0001.") and len(names) >= len(glob.glob(str(one / "0*")))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", E.ok_cases())
+def test_fqtool_raw_stream_small_windows_matches_reference(case, tmp_path):
+    """GPU record indexing (fq_engine_raw_*) under stress: gzip inputs are decompressed to plain
+    files so every case with plain outputs takes the raw stream, the first window is 4 KiB and packs
+    hold 7 pairs, so records straddle windows (the device carry), the mates' windows are sized
+    apart, and irregular records (CR line ends, empty lines, long or lowercase reads, lines without
+    '@') stop the stream mid-file for the host reader to resume at the reported offsets.  Outputs
+    and JSON must still equal the reference's -w 1 outputs."""
+    import gzip
+    import shutil
+
+    ind, outd = tmp_path / "in", tmp_path / "out"
+    ind.mkdir()
+    outd.mkdir()
+    argv = E.argv_for(abi.FQTOOL_BIN, case, str(outd))
+    for k, a in enumerate(argv):
+        if a.startswith(E.INPUTS) and a.endswith(".fq.gz"):
+            plain = ind / os.path.basename(a)[:-3]
+            with gzip.open(a, "rb") as f, open(plain, "wb") as g:
+                shutil.copyfileobj(f, g)
+            argv[k] = str(plain)
+    argv += ["--pack_pairs", "7"]
+    env = dict(os.environ, FQ_RAW_WINDOW0="4096")
+    p = subprocess.run(argv, capture_output=True, cwd=outd, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    if case in ("td_pe_qag", "td_pe_plain", "td_pe_detect", "synth_pe_c3", "synth_pe_c5", "synth_se_c2", "polygr_pe",
+                "edge_pe_dup", "td_se_q"):
+        assert "raw stream" in p.stderr.decode(), p.stderr.decode()[-1000:]
+    E.check_outputs(case, str(outd))

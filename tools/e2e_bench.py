@@ -86,13 +86,19 @@ def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
            "-J", o["r.json"], "-H", o["r.html"], *extra]
     if cfg == "C4":
         cmd += ["--merge_output", o["m.fq"]]
+    env = dict(os.environ, FQ_TIMING="1")
+    for tok in [t for t in cmd if re.fullmatch(r"[A-Z_]+=\S*", t)]:  # KEY=VALUE extras: environment
+        k, v = tok.split("=", 1)
+        env[k] = v
+        cmd.remove(tok)
     t0 = time.perf_counter()
-    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
     wall = time.perf_counter() - t0
     if p.returncode != 0:
         raise SystemExit(f"{tag} failed rc={p.returncode}: {p.stderr[-2000:]}")
     m = re.search(r"fqtool-amd: (.*)", p.stderr)
-    return wall, (m.group(1) if m else None), o
+    t = re.search(r"fqtool-amd timing: (.*)", p.stderr)
+    return wall, (m.group(1) if m else None) + ((" | " + t.group(1)) if t else ""), o
 
 
 def main():
@@ -103,6 +109,8 @@ def main():
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--devices", default=None, help="--devices of the fqtool-amd run (e.g. 0,0,0,0)")
     ap.add_argument("--repeat", type=int, default=1, help="runs of the fqtool-amd binary (all printed)")
+    ap.add_argument("--extra", default="", help="extra fqtool-amd options (space separated)")
+    ap.add_argument("--variants", default=None, help="';'-separated list of --extra strings, each run in turn")
     ap.add_argument("--null-out", action="store_true", help="FASTQ outputs to /dev/null (as bench.py's e2e leg)")
     ap.add_argument("--workers-list", default=None, help="comma list of -w values to run (overrides --workers)")
     args = ap.parse_args()
@@ -114,13 +122,14 @@ def main():
         print(f"[e2e] wrote {args.pairs} pairs ({gb:.2f} GB FASTQ) in {time.perf_counter() - t0:.1f}s", flush=True)
         reads = 2 * args.pairs
         ours = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
-        extra = ["--devices", args.devices] if args.devices else []
+        variants = args.variants.split(";") if args.variants else [args.extra]
         wl = [int(x) for x in args.workers_list.split(",")] if args.workers_list else [args.workers]
-        for _, w in [(r, w) for w in wl for r in range(args.repeat)]:
+        for _, w, v in [(r, w, v) for v in variants for w in wl for r in range(args.repeat)]:
+            extra = (["--devices", args.devices] if args.devices else []) + v.split()
             wall, inner, o_ours = run(ours, r1, r2, tmp, "amd", args.config, w, extra, args.null_out)
             line = {"tool": "fqtool-amd", "config": args.config, "pairs": args.pairs, "fastq_GB": round(gb, 3),
                     "wall_s": round(wall, 3), "Mreads_s": round(reads / wall / 1e6, 3),
-                    "fastq_GB_s": round(gb / wall, 3), "workers": w, "devices": args.devices,
+                    "fastq_GB_s": round(gb / wall, 3), "workers": w, "devices": args.devices, "extra": v,
                     "text_mode": os.environ.get("FQ_TEXT_MODE", "1") != "0", "tool_log": inner}
             print(json.dumps(line), flush=True)
         ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")

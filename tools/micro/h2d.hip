@@ -74,7 +74,42 @@ int main(int argc, char** argv) {
     printf("(b) register + pinned H2D: %.3f s (register %.3f s), %.1f GB/s\n", t, treg, size / t / 1e9);
 
     std::vector<char*> pin(2);
-    for (auto& p : pin) CK(hipHostMalloc((void**)&p, chunk, hipHostMallocDefault));
+    {
+        double a0 = now();
+        for (auto& p : pin) CK(hipHostMalloc((void**)&p, chunk, hipHostMallocDefault));
+        double a = now() - a0;
+        printf("hipHostMalloc 2 x %zu MB: %.3f s (%.2f s per GB)\n", chunk >> 20, a, a / (2.0 * chunk / 1e9));
+        char* big = nullptr;
+        a0 = now();
+        CK(hipHostMalloc((void**)&big, (size_t)1 << 30, hipHostMallocPortable));
+        double a1 = now();
+        memset(big, 1, (size_t)1 << 30);
+        double a2 = now();
+        CK(hipHostFree(big));
+        printf("hipHostMalloc 1 GiB portable: alloc %.3f s, first touch %.3f s, free %.3f s\n", a1 - a0, a2 - a1, now() - a2);
+        for (int huge = 0; huge < 2; ++huge) {
+            const size_t G = (size_t)1 << 30;
+            double b0 = now();
+            char* m = (char*)mmap(nullptr, G, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (huge) madvise(m, G, MADV_HUGEPAGE);
+            memset(m, 0, G);
+            double b1 = now();
+            hipError_t e = hipHostRegister(m, G, hipHostRegisterPortable);
+            double b2 = now();
+            CK(hipMemcpyAsync(dev, m, chunk, hipMemcpyHostToDevice, s));
+            CK(hipStreamSynchronize(s));
+            double b3 = now();
+            CK(hipMemcpyAsync(dev, m, chunk, hipMemcpyHostToDevice, s));
+            CK(hipStreamSynchronize(s));
+            double b4 = now();
+            (void)hipHostUnregister(m);
+            double b5 = now();
+            munmap(m, G);
+            printf("anon 1 GiB%s: mmap+touch %.3f s, register %.3f s (%s), H2D %zu MB %.1f GB/s, unregister %.3f s, munmap %.3f s\n",
+                   huge ? " (THP)" : "", b1 - b0, b2 - b1, hipGetErrorString(e), chunk >> 20, chunk / (b4 - b3) / 1e9, b5 - b4, now() - b5);
+            (void)b3;
+        }
+    }
     auto par = [&](char* dst, size_t o, size_t n, bool use_pread) {
         std::vector<std::thread> th;
         const size_t per = (n + T - 1) / T;
