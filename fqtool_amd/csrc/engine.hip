@@ -56,6 +56,7 @@ struct Slot {
     bool raw_ready = false;
     hipEvent_t ev_idx = nullptr;
     fq_raw_out* raw_out = nullptr;  // the pending raw pack's output descriptor
+    uint64_t raw_n[2] = {0, 0};     // the window's raw bytes
     int* d_err = nullptr;  // this pack's device error word (cleared at submit, set by its kernels)
     int* h_err = nullptr;  // pinned: d_err as of this pack's kernels
     bool busy = false;      // events recorded and not yet waited for
@@ -647,6 +648,8 @@ int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w) {
             HIP_TRY(e, hipMemcpyAsync(s.d_text[m] + e->raw_ccap, w->bytes[m], w->n[m], hipMemcpyHostToDevice, e->s_in));
     HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
     HIP_TRY(e, hipStreamWaitEvent(e->s_idx, s.ev_in, 0));
+    s.raw_n[0] = w->n[0];
+    s.raw_n[1] = pe ? w->n[1] : 0;
     fq_raw_text_args a{};
     const Slot* ps = e->raw_prev_slot >= 0 ? &e->slots[e->raw_prev_slot] : nullptr;
     for (int m = 0; m < 2; ++m) {
@@ -688,7 +691,8 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     r->pairs = n;
     for (int m = 0; m < mates; ++m) {
         const fq_raw_state& st = s.h_rstate[m];
-        r->carry[m] = st.avail - st.consumed;
+        // (after an overflow every byte of the carry and the window is still to be read)
+        r->carry[m] = st.overflow ? (uint64_t)st.carry_in + s.raw_n[m] : (uint64_t)(st.avail - st.consumed);
         r->text_bytes[m] = st.consumed;
         r->max_len = std::max(r->max_len, st.max_len);
         if (st.overflow || st.first_bad == n) r->stop = 1;

@@ -55,13 +55,13 @@ __global__ void raw_carry_kernel(fq_raw_text_args a) {
     const int m = blockIdx.y;
     const fq_raw_state* ps = a.prev_state ? a.prev_state + m : nullptr;
     uint32_t carry = ps ? ps->avail - ps->consumed : 0u;
-    const bool over = carry > a.carry_cap;
-    if (over) carry = 0;
+    const bool over = carry > a.carry_cap || (ps && ps->overflow);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // (an overflow indexes nothing: the host resumes before the carried bytes)
         fq_raw_state& s = a.state[m];
-        s.text_start = a.carry_cap - carry;
+        s.text_start = a.carry_cap - (over ? 0u : carry);
         s.carry_in = carry;
-        s.avail = carry + a.raw_bytes[m];
+        s.avail = over ? 0u : carry + a.raw_bytes[m];
         s.overflow = over ? 1u : 0u;
         s.first_bad = INT_MAX;
         s.complete = 0;
@@ -70,7 +70,7 @@ __global__ void raw_carry_kernel(fq_raw_text_args a) {
         s.consumed = 0;
         s.n = 0;
     }
-    if (!ps || !carry) return;
+    if (!ps || !carry || over) return;
     const char* src = a.prev_text[m] + ps->text_start + ps->consumed;
     char* dst = a.text[m] + (a.carry_cap - carry);
     for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) * 16u; i < carry; i += gridDim.x * blockDim.x * 16u) {

@@ -883,6 +883,7 @@ struct Lane {
     std::vector<std::unique_ptr<Stage>> stages;
     Queue<int> free_stages{64};
     uint64_t raw_pairs = 0, raw_packs = 0;  // what the raw stream took
+    double raw_read_s = 0, raw_stage_wait_s = 0, raw_ready_wait_s = 0;  // window reader: preads, waits
     std::string raw_end;                    // why it ended
 
     RawResume run_raw(const std::string* files, int mates, int target, Queue<std::unique_ptr<Pack>>& spare, Pool& pool) {
@@ -949,6 +950,9 @@ struct Lane {
                     for (const Win& q : made)
                         for (int m = 0; m < mates; ++m) held[m] += q.n[m];
                     for (int m = 0; m < mates; ++m) pairs_held = std::min(pairs_held, b[m] > 0 ? held[m] / b[m] : 0.0);
+                    // the packs of the windows still queued take up to `target` pairs each before
+                    // this window's pack: what they leave over is the new window's carry
+                    const double queued_pairs = (double)target * (double)made.size();
                     Win w;
                     w.id = id;
                     for (int m = 0; m < mates; ++m) {
@@ -956,7 +960,7 @@ struct Lane {
                         if (b[m] <= 0) {
                             want = w0;
                         } else {
-                            const double after = held[m] - std::min(pairs_held, (double)target) * b[m];
+                            const double after = held[m] - std::min(pairs_held, queued_pairs) * b[m];
                             const double need = target * b[m] * 1.02 - std::max(0.0, after);
                             want = need <= 0 ? 0 : (uint64_t)need;
                         }
@@ -964,7 +968,10 @@ struct Lane {
                         w.n[m] = std::min(std::min<uint64_t>((want + 4095) / 4096 * 4096, wcap), size[m] - pos[m]);
                         pos[m] += w.n[m];
                     }
+                    const auto s0 = std::chrono::steady_clock::now();
                     if (!free_stages.pop(w.stage)) break;
+                    raw_stage_wait_s += since(s0);
+                    const auto r0 = std::chrono::steady_clock::now();
                     Stage& st = *stages[(size_t)w.stage];
                     const uint64_t piece = (uint64_t)4 << 20;
                     int pieces[2] = {0, 0};
@@ -988,6 +995,7 @@ struct Lane {
                         }
                     });
                     if (short_read) throw std::runtime_error("input file changed while reading");
+                    raw_read_s += since(r0);
                     made.push_back(w);
                     if (!ready.push(w)) break;
                 }
@@ -998,23 +1006,28 @@ struct Lane {
         });
         std::deque<Win> wins;  // enqueued, not launched
         bool input_done = false;
-        auto enqueue_next = [&]() -> bool {
-            Win w;
-            if (input_done || !ready.pop(w)) {
-                input_done = true;
-                return false;
-            }
-            Stage& st = *stages[(size_t)w.stage];
+        auto enqueue_window = [&](const Win& w) {  // (stage -1: an empty window)
             fq_raw_window rw{};
             for (int m = 0; m < mates; ++m) {
-                rw.bytes[m] = st.buf[m].data();
+                rw.bytes[m] = w.stage >= 0 ? stages[(size_t)w.stage]->buf[m].data() : nullptr;
                 rw.n[m] = w.n[m];
             }
             if (fq_engine_raw_enqueue(e, &rw) != FQ_OK) {
-                free_stages.push(w.stage);
+                if (w.stage >= 0) free_stages.push(w.stage);
                 throw std::runtime_error(std::string("fq_engine_raw_enqueue: ") + fq_engine_last_error(e));
             }
             wins.push_back(w);
+        };
+        auto enqueue_next = [&]() -> bool {
+            Win w;
+            const auto q0 = std::chrono::steady_clock::now();
+            const bool got = !input_done && ready.pop(w);
+            raw_ready_wait_s += since(q0);
+            if (!got) {
+                input_done = true;
+                return false;
+            }
+            enqueue_window(w);
             return true;
         };
         uint64_t seq = 0;
@@ -1075,11 +1088,24 @@ struct Lane {
                     ++seq;
                     if (wins.empty()) enqueue_next();
                     const bool last = wins.empty() && input_done;
-                    bool left = false;
-                    for (int m = 0; m < mates; ++m) left = left || r.carry[m] > 0;
+                    bool left = false, exhausted = false;  // (exhausted: a mate has sent all its bytes)
+                    for (int m = 0; m < mates; ++m) {
+                        left = left || r.carry[m] > 0;
+                        const uint64_t sent = wins.empty() ? w.start[m] + w.n[m] : wins.back().start[m] + wins.back().n[m];
+                        exhausted = exhausted || sent == size[m];
+                    }
+                    if (last && left && r.pairs > 0 && !r.stop) {  // all input is on the device: drain its carry
+                        Win d;
+                        for (int m = 0; m < mates; ++m) d.start[m] = size[m];
+                        enqueue_window(d);
+                        raw_pairs += (uint64_t)r.pairs;
+                        ++raw_packs;
+                        continue;
+                    }
                     raw_pairs += (uint64_t)r.pairs;
                     ++raw_packs;
-                    if (r.stop || r.pairs == 0 || last) {
+                    // (no pairs while every mate still has bytes to send: the windows were too small)
+                    if (r.stop || (r.pairs == 0 && exhausted) || last) {
                         rr.done = last && !left && !r.stop;
                         raw_end = rr.done ? "end of input"
                                           : std::string(r.stop ? "irregular record" : r.pairs == 0 ? "no pairs" : "bytes left at the end") +
@@ -1402,7 +1428,7 @@ int run_tool(int argc, char** argv) {
                         if (o.adapter_trimming) {
                             if (pk->raw)
                                 for (int m = 0; m < (paired ? 2 : 1); ++m)
-                                    ac.add_entries(m, pk->ad[m].data(), pk->rout.adapter_bytes[m], p);
+                                    ac.add_entries(m, pk->ad[m].data(), pk->rout.adapter_bytes[m], p, &pool);
                             else
                                 ac.add(*pk, pk->res.data(), p, &pool);
                         }
@@ -1477,7 +1503,10 @@ int run_tool(int argc, char** argv) {
         teardown.logged = std::chrono::steady_clock::now();
         log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s)" +
             (raw_mode ? " (raw stream: GPU record indexing, ingest/egress: " + std::to_string(lanes[0]->raw_pairs) + " pairs in " +
-                            std::to_string(lanes[0]->raw_packs) + " packs, ended: " + lanes[0]->raw_end + ")"
+                            std::to_string(lanes[0]->raw_packs) + " packs, ended: " + lanes[0]->raw_end + "; window reads " +
+                            std::to_string(lanes[0]->raw_read_s) + " s, reader waiting for a stage " +
+                            std::to_string(lanes[0]->raw_stage_wait_s) + " s, dispatcher waiting for windows " +
+                            std::to_string(lanes[0]->raw_ready_wait_s) + " s)"
                       : text_mode ? " (text packs: GPU ingest/egress)" : "") + ", wall " +
             std::to_string(since(t0)) + " s, engine submit " + std::to_string(submit_s) + " s, wait " + std::to_string(wait_s) + " s; pre-pass " +
             std::to_string(prepass_s) + " s, adapter detection (concurrent) " + std::to_string(detect_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +

@@ -143,21 +143,44 @@ void AdapterCounts::add(const Pack& pk, const fq_read_result* res, const fq_para
     }
 }
 
-void AdapterCounts::add_entries(int m, const char* d, size_t bytes, const fq_params& p) {
+void AdapterCounts::add_entries(int m, const char* d, size_t bytes, const fq_params& p, Pool* pool) {
     const char* ad = reinterpret_cast<const char*>(m ? p.adapter2 : p.adapter1);
+    auto next = [&](size_t o) { return o + (d[o + 2] ? 5 : 3 + ((uint8_t)d[o] | ((size_t)(uint8_t)d[o + 1] << 8))); };
+    // ranges of 8192 entries (one pass over the lengths), hashed on the pool, then merged per shard
+    std::vector<size_t> cuts{0};
+    size_t k = 0;
     for (size_t o = 0; o + 3 <= bytes;) {
-        const uint32_t len = (uint8_t)d[o] | ((uint32_t)(uint8_t)d[o + 1] << 8);
+        o = next(o);
+        if (++k % 8192 == 0 && o < bytes) cuts.push_back(o);
+    }
+    cuts.push_back(bytes);
+    const int parts = (int)cuts.size() - 1;
+    struct Item {
+        uint64_t h;
         const char* s;
-        if (d[o + 2]) {
-            const uint32_t pos = (uint8_t)d[o + 3] | ((uint32_t)(uint8_t)d[o + 4] << 8);
-            s = ad + pos;
-            o += 5;
-        } else {
-            s = d + o + 3;
-            o += 3 + (size_t)len;
+        uint32_t len;
+    };
+    std::vector<std::vector<std::vector<Item>>> items((size_t)parts, std::vector<std::vector<Item>>((size_t)kShards));
+    auto hash_part = [&](int q) {
+        auto& it = items[(size_t)q];
+        for (size_t o = cuts[(size_t)q]; o + 3 <= cuts[(size_t)q + 1]; o = next(o)) {
+            const uint32_t len = (uint8_t)d[o] | ((uint32_t)(uint8_t)d[o + 1] << 8);
+            const char* s = d[o + 2] ? ad + ((uint8_t)d[o + 3] | ((uint32_t)(uint8_t)d[o + 4] << 8)) : d + o + 3;
+            const uint64_t h = hash_bytes(s, len);
+            it[h % kShards].push_back(Item{h, s, len});
         }
-        const uint64_t h = hash_bytes(s, len);
-        shards_[m][h % kShards]->bump(h, s, len, 1);
+    };
+    auto merge_shard = [&](int j) {
+        Shard& sh = *shards_[m][(size_t)j];
+        for (int q = 0; q < parts; ++q)
+            for (const Item& x : items[(size_t)q][(size_t)j]) sh.bump(x.h, x.s, x.len, 1);
+    };
+    if (pool && parts > 1) {
+        pool->run(parts, hash_part);
+        pool->run(kShards, merge_shard);
+    } else {
+        for (int q = 0; q < parts; ++q) hash_part(q);
+        for (int j = 0; j < kShards; ++j) merge_shard(j);
     }
 }
 

@@ -70,7 +70,7 @@ class AdapterCounts {
     void add(const Pack& pk, const fq_read_result* res, const fq_params& p, Pool* pool = nullptr);
     void add(int mate, const std::string& adapter, size_t count);  // one string (tests, report API)
     // a raw pack's trimmed-adapter entries of one mate (fq_raw_out, include/fqengine.h)
-    void add_entries(int mate, const char* entries, size_t bytes, const fq_params& p);
+    void add_entries(int mate, const char* entries, size_t bytes, const fq_params& p, Pool* pool = nullptr);
     struct Report {
         std::map<std::string, size_t> top;  // the strings at >= 1 % of total (FilterResult's test)
         size_t total = 0;                   // adapter-trimmed reads of the mate
