@@ -151,6 +151,8 @@ def write_fastq_fast(planes, n, first_index, d, tag=""):
                 files[m].write(rec)  # (buffer protocol: no extra copy)
     finally:
         for f in files:
+            f.flush()
+            os.fsync(f.fileno())  # (written back before any timed run reads them: no writeback in the timing)
             f.close()
     return paths
 

@@ -119,8 +119,7 @@ class FqRawResult(ctypes.Structure):  # fq_raw_result
 
 
 class FqRawOut(ctypes.Structure):  # fq_raw_out
-    _fields_ = [("text", FqTextOut), ("adapters", ctypes.c_void_p * 2), ("adapter_cap", ctypes.c_uint64 * 2),
-                ("adapter_bytes", ctypes.c_uint64 * 2)]
+    _fields_ = [("text", FqTextOut), ("adapter_bytes", ctypes.c_uint64 * 2)]
 
 
 # Batch planes hold rows in chunk-interleaved tiles (include/fqengine.h): byte j of read i at

@@ -70,7 +70,8 @@ struct Pending {
     int err;
 };
 
-static const int kSlots = 3;  // H2D(k+1) || kernels(k) || D2H(k-1)
+static const int kSlots = 3;     // host packs: H2D(k+1) || kernels(k) || D2H(k-1)
+static const int kRawSlots = 8;  // raw windows: up to 3 enqueued + 5 launched, copies queued each way
 
 struct fq_engine {
     fq_params p;
@@ -84,7 +85,7 @@ struct fq_engine {
     size_t acc_words = 0;
     int* err = nullptr;
     // host-memory path: pipeline slots and their streams
-    Slot slots[kSlots];
+    Slot slots[kRawSlots];  // (host packs use the first kSlots)
     std::deque<Pending> pending;
     hipStream_t s_in = nullptr, s_out = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -345,16 +346,12 @@ static int retire_slot(fq_engine* e, int k) {
         s.text_out->bytes[1] = s.h_total[1];
         s.text_out = nullptr;
     }
-    if (s.raw_out) {  // a raw pack: its trimmed-adapter entries, exactly sized, before the slot is reused
+    if (s.raw_out) {  // a raw pack: its trimmed-adapter entries follow the output text
         fq_raw_out* o = s.raw_out;
         s.raw_out = nullptr;
         for (int m = 0; m < 2; ++m) {
-            const uint64_t b = s.h_total[2 + m];
-            o->adapter_bytes[m] = 0;
-            if (!b) continue;
-            if (b > o->adapter_cap[m] || !o->adapters[m]) return fail(e, FQ_E_INVALID, "raw pack: adapter buffer too small");
-            HIP_TRY(e, hipMemcpy(o->adapters[m], s.d_ad[m], b, hipMemcpyDeviceToHost));
-            o->adapter_bytes[m] = b;
+            o->adapter_bytes[m] = s.h_total[2 + m];
+            if (o->adapter_bytes[m] == ~0ull) return fail(e, FQ_E_INVALID, "raw pack: adapter entries exceed the output copy");
         }
     }
     return FQ_OK;
@@ -582,15 +579,14 @@ static int ensure_raw(fq_engine* e, Slot& s) {
         s.d_ad[m] = nullptr;
         if (m == 1 && !pe) continue;
         HIP_TRY(e, hipMalloc(&s.d_text[m], text));
-        HIP_TRY(e, hipMalloc(&s.d_out[m], text));
+        HIP_TRY(e, hipMalloc(&s.d_out[m], text + 4 * recs + 64));  // (+ the adapter entries' slack)
         HIP_TRY(e, hipMalloc(&s.d_trec[m], recs * sizeof(fq_text_rec)));
         HIP_TRY(e, hipMalloc(&s.d_tsize[m], recs * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&s.d_toff[m], recs * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&s.d_lines[m], cap_lines * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&s.d_bcnt[m], (size_t)e->raw_nblocks * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&s.d_bbase[m], (size_t)e->raw_nblocks * sizeof(uint32_t)));
-        s.ad_cap = recs * (size_t)(3 + e->max_stride);
-        HIP_TRY(e, hipMalloc(&s.d_ad[m], s.ad_cap));
+
     }
     s.text_cap[0] = s.text_cap[1] = 0;  // (not the text-pack sizes: ensure_text re-allocates)
     s.trec_cap = 0;
@@ -632,12 +628,12 @@ int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap) {
 int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w) {
     if (!e || !w) return FQ_E_INVALID;
     if (!e->raw) return fail(e, FQ_E_INVALID, "fq_engine_raw_enqueue before fq_engine_raw_begin");
-    if (e->raw_queued.size() >= 2) return fail(e, FQ_E_INVALID, "two raw windows are already waiting for fq_engine_raw_launch");
+    if (e->raw_queued.size() >= 3) return fail(e, FQ_E_INVALID, "three raw windows are already waiting for fq_engine_raw_launch");
     const bool pe = e->p.paired;
     for (int m = 0; m < (pe ? 2 : 1); ++m)
         if (w->n[m] > e->raw_wcap || (w->n[m] && !w->bytes[m])) return fail(e, FQ_E_INVALID, "raw window exceeds its capacity");
     HIP_TRY(e, hipSetDevice(e->device));
-    const int k = (e->raw_prev_slot + 1) % kSlots;
+    const int k = (e->raw_prev_slot + 1) % kRawSlots;
     int rc = retire_slot(e, k);
     if (rc != FQ_OK) return rc;
     Slot& s = e->slots[k];
@@ -724,18 +720,23 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     int rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false, seq_no, s.d_err);
     if (rc != FQ_OK) return rc;
     HIP_TRY(e, hipMemsetAsync(s.d_total, 0, 4 * sizeof(unsigned long long), e->stream));
+    // each mate's copy back: its output text (<= the input it spans) and the adapter entries after
+    // it (per record, output + entry <= input + 3 bytes)
+    size_t back[2] = {0, 0};
+    for (int m = 0; m < mates; ++m) back[m] = (size_t)r->text_bytes[m] + kTextSlack + 3 * (size_t)n;
     for (int m = 0; m < mates; ++m) {
         HIP_TRY(e, fq_launch_text_out(s.d_text[m], s.d_trec[m], s.d_res, n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
                                       s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, e->stream));
         if (e->p.adapter_trimming)
             HIP_TRY(e, fq_launch_raw_adapters(s.d_text[m], s.d_trec[m], s.d_res, n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
-                                              s.d_scan, s.scan_bytes, s.d_ad[m], s.d_total + 2 + m, e->stream));
+                                              s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, back[m], s.d_total + 2 + m,
+                                              e->stream));
     }
     HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
     HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
     HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
     for (int m = 0; m < mates; ++m)
-        HIP_TRY(e, hipMemcpyAsync(out->text.text[m], s.d_out[m], r->text_bytes[m] + kTextSlack, hipMemcpyDeviceToHost, e->s_out));
+        HIP_TRY(e, hipMemcpyAsync(out->text.text[m], s.d_out[m], back[m], hipMemcpyDeviceToHost, e->s_out));
     HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
     HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
     s.busy = true;

@@ -75,6 +75,9 @@ struct fq_raw_text_args {
 size_t fq_raw_scan_temp_bytes(int nblocks, int n);
 hipError_t fq_launch_raw_index(const fq_raw_text_args& a, int mates, int cap_batch, void* d_temp, size_t temp_bytes,
                                hipStream_t s);
+// trimmed-adapter entries of mate m appended to its output text (at *d_text_total, within cap bytes
+// of d_out; *d_total = the entries' bytes, ~0 if they would not fit)
 hipError_t fq_launch_raw_adapters(const char* d_text, const fq_text_rec* d_rec, const fq_read_result* d_res, int n,
                                   int paired, int m, uint32_t* d_size, uint32_t* d_off, void* d_temp, size_t temp_bytes,
-                                  char* d_out, unsigned long long* d_total, hipStream_t s);
+                                  char* d_out, const unsigned long long* d_text_total, unsigned long long cap,
+                                  unsigned long long* d_total, hipStream_t s);

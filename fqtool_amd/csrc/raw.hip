@@ -199,12 +199,17 @@ __global__ void raw_ad_size_kernel(const fq_read_result* __restrict__ res, int n
 __global__ void raw_ad_write_kernel(const char* __restrict__ text, const fq_text_rec* __restrict__ rec,
                                     const fq_read_result* __restrict__ res, int n, int paired, int m,
                                     const uint32_t* __restrict__ size, const uint32_t* __restrict__ off,
-                                    char* __restrict__ out, unsigned long long* __restrict__ total) {
+                                    char* __restrict__ out, const unsigned long long* __restrict__ text_total,
+                                    unsigned long long cap, unsigned long long* __restrict__ total) {
+    // the entries follow the pack's output text in the same buffer (copied back with it); they
+    // fit: per record, output + entry <= input + 3 bytes, and the copy spans input + 3n + 16
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == n - 1) *total = (unsigned long long)off[i] + size[i];
-    if (i >= n || size[i] == 0) return;
+    const unsigned long long base = *text_total;
+    const unsigned long long end = base + (unsigned long long)off[n - 1] + size[n - 1];
+    if (i == n - 1) *total = end <= cap ? end - base : ~0ull;
+    if (i >= n || size[i] == 0 || end > cap) return;
     const fq_read_result& r = res[paired ? 2 * (size_t)i + m : (size_t)i];
-    char* d = out + off[i];
+    char* d = out + base + off[i];
     d[0] = (char)(r.ad_len & 0xFF);
     d[1] = (char)(r.ad_len >> 8);
     if (r.flags & FQ_RF_AD_NEG) {
@@ -247,7 +252,8 @@ hipError_t fq_launch_raw_index(const fq_raw_text_args& a, int mates, int cap_bat
 
 hipError_t fq_launch_raw_adapters(const char* d_text, const fq_text_rec* d_rec, const fq_read_result* d_res, int n,
                                   int paired, int m, uint32_t* d_size, uint32_t* d_off, void* d_temp, size_t temp_bytes,
-                                  char* d_out, unsigned long long* d_total, hipStream_t s) {
+                                  char* d_out, const unsigned long long* d_text_total, unsigned long long cap,
+                                  unsigned long long* d_total, hipStream_t s) {
     if (n <= 0) return hipMemsetAsync(d_total, 0, sizeof(unsigned long long), s);
     const dim3 g((n + 255) / 256), b(256);
     hipLaunchKernelGGL(raw_ad_size_kernel, g, b, 0, s, d_res, n, paired, m, d_size);
@@ -256,6 +262,7 @@ hipError_t fq_launch_raw_adapters(const char* d_text, const fq_text_rec* d_rec, 
     size_t tb = temp_bytes;
     e = hipcub::DeviceScan::ExclusiveSum(d_temp, tb, d_size, d_off, n, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(raw_ad_write_kernel, g, b, 0, s, d_text, d_rec, d_res, n, paired, m, d_size, d_off, d_out, d_total);
+    hipLaunchKernelGGL(raw_ad_write_kernel, g, b, 0, s, d_text, d_rec, d_res, n, paired, m, d_size, d_off, d_out,
+                       d_text_total, cap, d_total);
     return hipGetLastError();
 }

@@ -224,8 +224,7 @@ struct Pack {
           flags(pinned),
           res(pinned),
           trec{PodBuf<fq_text_rec>(pinned), PodBuf<fq_text_rec>(pinned)},
-          out_text{ByteBuf(pinned), ByteBuf(pinned)},
-          ad{ByteBuf(pinned), ByteBuf(pinned)} {}
+          out_text{ByteBuf(pinned), ByteBuf(pinned)} {}
     int n = 0;
     int stride = 0;
     bool paired = false;
@@ -251,10 +250,10 @@ struct Pack {
     int max_len[2] = {0, 0};
 
     // raw-stream pack (fq_engine_raw_*): the engine cut the records from the input bytes; its
-    // trimmed-adapter entries land in ad[m]; its staging window is recycled once the pack is reported
+    // trimmed-adapter entries follow the output text in out_text[m]; its staging window is recycled
+    // once the pack is reported
     bool raw = false;
     fq_raw_out rout{};
-    ByteBuf ad[2];
     int stage = -1;  // the raw driver's staging window of the pack's input bytes
 
     // -c: pairs whose bases the engine corrected read their seq/qual from a corrected copy

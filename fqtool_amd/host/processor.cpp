@@ -824,13 +824,15 @@ struct Lane {
         fq_engine_reset_acc(e);
     }
 
-    void complete_oldest() {
-        std::unique_ptr<Pack> pk = std::move(inflight.front());
-        inflight.pop_front();
+    // the oldest pack in flight, once complete, to the formatter; wait == false: only if it is done
+    bool complete_oldest(bool wait = true) {
         uint64_t seq = 0;
         const auto e0 = std::chrono::steady_clock::now();
-        const int rc = fq_engine_poll(e, 1, &seq);
+        const int rc = fq_engine_poll(e, wait ? 1 : 0, &seq);
         wait_s += since(e0);
+        if (rc == 0 && !wait) return false;
+        std::unique_ptr<Pack> pk = std::move(inflight.front());
+        inflight.pop_front();
         if (rc != 1) throw std::runtime_error(std::string("fq_engine_poll: ") + fq_engine_last_error(e));
         if (seq != pk->seq_no) throw std::runtime_error("engine completed packs out of order");
         if (pk->raw) {  // its input window was copied: recycle the staging; the output sizes are in
@@ -839,6 +841,7 @@ struct Lane {
             pk->tout = pk->rout.text;
         }
         if (!out.push(std::move(pk))) throw Stopped();
+        return true;
     }
 
     void submit(Pack& pk, bool as_text) {
@@ -884,6 +887,7 @@ struct Lane {
     Queue<int> free_stages{64};
     uint64_t raw_pairs = 0, raw_packs = 0;  // what the raw stream took
     double raw_read_s = 0, raw_stage_wait_s = 0, raw_ready_wait_s = 0;  // window reader: preads, waits
+    double raw_pack_wait_s = 0, raw_enqueue_s = 0;  // dispatcher: waiting for a spare pack, enqueue calls
     std::string raw_end;                    // why it ended
 
     RawResume run_raw(const std::string* files, int mates, int target, Queue<std::unique_ptr<Pack>>& spare, Pool& pool) {
@@ -907,10 +911,14 @@ struct Lane {
             size[m] = (uint64_t)st.st_size;
             (void)posix_fadvise(fd[m], 0, 0, POSIX_FADV_SEQUENTIAL);
         }
-        const uint64_t wcap = (uint64_t)128 << 20, ccap = (uint64_t)32 << 20;
+        // windows of up to 64 MiB per mate (a pack of `target` 2x150 pairs is ~45 MiB), 16 MiB of
+        // carry (partial records, the mates' imbalance); six windows in the engine at once
+        const uint64_t wcap = (uint64_t)64 << 20, ccap = (uint64_t)16 << 20;
+        const int raw_depth = 4;  // packs launched and not yet polled
+        const size_t raw_ahead = 3;  // windows enqueued ahead of their launch (the copy-in queue)
         if (fq_engine_raw_begin(e, wcap, ccap) != FQ_OK)
             throw std::runtime_error(std::string("fq_engine_raw_begin: ") + fq_engine_last_error(e));
-        const int kStages = depth + 4;  // enqueued (2) + in flight (depth) + being filled
+        const int kStages = raw_depth + (int)raw_ahead + 2;  // in flight + enqueued + being filled
         while ((int)stages.size() < kStages) {
             stages.emplace_back(new Stage);
             free_stages.push((int)stages.size() - 1);
@@ -925,8 +933,20 @@ struct Lane {
         double bpr[2] = {0, 0};      // text bytes per record of the packs so far
         uint64_t carry[2] = {0, 0};  // after the last launched window
         uint64_t launched = 0;       // windows launched
-        Queue<Win> ready(2);
+        Queue<Win> ready(3);
         std::exception_ptr rd_err;
+        const char* pc_env = std::getenv("FQ_RAW_PIECE_MB");  // (profiling: pread piece size)
+        const uint64_t piece_bytes = (uint64_t)(pc_env ? std::max(1, atoi(pc_env)) : 1) << 20;
+        const char* cp_env = std::getenv("FQ_RAW_COPY");
+        const char* mp[2] = {nullptr, nullptr};
+        if (cp_env && std::string(cp_env) == "mmap")
+            for (int m = 0; m < mates; ++m) {
+                void* a = mmap(nullptr, (size_t)size[m], PROT_READ, MAP_PRIVATE, fd[m], 0);
+                if (a != MAP_FAILED) {
+                    madvise(a, (size_t)size[m], MADV_SEQUENTIAL);
+                    mp[m] = static_cast<const char*>(a);
+                }
+            }
         const char* w0_env = std::getenv("FQ_RAW_WINDOW0");  // first window's bytes (tests: tiny windows)
         const uint64_t w0 = w0_env ? std::max<uint64_t>(4096, std::strtoull(w0_env, nullptr, 10)) : (uint64_t)4 << 20;
         std::thread rd([&] {  // the window reader
@@ -973,7 +993,7 @@ struct Lane {
                     raw_stage_wait_s += since(s0);
                     const auto r0 = std::chrono::steady_clock::now();
                     Stage& st = *stages[(size_t)w.stage];
-                    const uint64_t piece = (uint64_t)4 << 20;
+                    const uint64_t piece = piece_bytes;
                     int pieces[2] = {0, 0};
                     for (int m = 0; m < mates; ++m) {
                         st.buf[m].resize_uninit((size_t)std::max<uint64_t>(w.n[m], 1));
@@ -984,6 +1004,10 @@ struct Lane {
                         const int m = k < pieces[0] ? 0 : 1;
                         const uint64_t o = (uint64_t)(m ? k - pieces[0] : k) * piece;
                         const uint64_t len = std::min(piece, w.n[m] - o);
+                        if (mp[m]) {  // (FQ_RAW_COPY=mmap: copy from a read-only mapping)
+                            std::memcpy(st.buf[m].data() + o, mp[m] + w.start[m] + o, (size_t)len);
+                            return;
+                        }
                         uint64_t got = 0;
                         while (got < len) {
                             const ssize_t r = pread(fd[m], st.buf[m].data() + o + got, (size_t)(len - got), (off_t)(w.start[m] + o + got));
@@ -1012,7 +1036,10 @@ struct Lane {
                 rw.bytes[m] = w.stage >= 0 ? stages[(size_t)w.stage]->buf[m].data() : nullptr;
                 rw.n[m] = w.n[m];
             }
-            if (fq_engine_raw_enqueue(e, &rw) != FQ_OK) {
+            const auto q0 = std::chrono::steady_clock::now();
+            const int qrc = fq_engine_raw_enqueue(e, &rw);
+            raw_enqueue_s += since(q0);
+            if (qrc != FQ_OK) {
                 if (w.stage >= 0) free_stages.push(w.stage);
                 throw std::runtime_error(std::string("fq_engine_raw_enqueue: ") + fq_engine_last_error(e));
             }
@@ -1040,11 +1067,14 @@ struct Lane {
         try {
             if (enqueue_next()) {
                 for (;;) {
-                    if (wins.size() < 2) enqueue_next();
+                    while (wins.size() < raw_ahead && enqueue_next()) {
+                    }
                     const Win w = wins.front();
                     wins.pop_front();
                     std::unique_ptr<Pack> pk;
+                    const auto p0 = std::chrono::steady_clock::now();
                     if (!spare.pop(pk)) throw Stopped();
+                    raw_pack_wait_s += since(p0);
                     pk->clear();
                     pk->raw = true;
                     pk->text_mode = true;
@@ -1057,13 +1087,10 @@ struct Lane {
                         cin[0] = carry[0];
                         cin[1] = carry[1];
                     }
-                    for (int m = 0; m < 2; ++m) {
-                        const size_t cap = m < mates ? (size_t)(cin[m] + w.n[m] + 64) : 0;
+                    for (int m = 0; m < 2; ++m) {  // (output text, then the adapter entries)
+                        const size_t cap = m < mates ? (size_t)(cin[m] + w.n[m] + 4 * (uint64_t)target + 64) : 0;
                         pk->out_text[m].resize_uninit(cap);
-                        pk->ad[m].resize_uninit(cap);
                         pk->rout.text.text[m] = m < mates ? pk->out_text[m].data() : nullptr;
-                        pk->rout.adapters[m] = m < mates ? pk->ad[m].data() : nullptr;
-                        pk->rout.adapter_cap[m] = cap;
                     }
                     fq_raw_result r{};
                     const auto e0 = std::chrono::steady_clock::now();
@@ -1083,7 +1110,10 @@ struct Lane {
                         }
                         launched = w.id + 1;
                     }
-                    if ((int)inflight.size() >= depth) complete_oldest();
+                    // completed packs go on at once; wait only when the pipeline is full
+                    while (!inflight.empty() && complete_oldest(false)) {
+                    }
+                    if ((int)inflight.size() >= raw_depth) complete_oldest();
                     inflight.push_back(std::move(pk));
                     ++seq;
                     if (wins.empty()) enqueue_next();
@@ -1134,6 +1164,8 @@ struct Lane {
             throw;
         }
         close_all();
+        for (int m = 0; m < mates; ++m)
+            if (mp[m]) munmap(const_cast<char*>(mp[m]), (size_t)size[m]);
         rr.next_seq = seq;
         return rr;
     }
@@ -1261,6 +1293,11 @@ Options prepare_options(int argc, char** argv, bool detect_adapters) {
 }
 
 int run_tool(int argc, char** argv) {
+    // Eight hardware queues instead of HIP's default four: the engine's copy-in, index, compute
+    // and copy-out streams plus the concurrent adapter detection's stream each get their own, so
+    // the DMA copies of one direction do not queue behind those of the other (unless the caller
+    // chose a value; read when HIP initialises, before any engine exists)
+    setenv("GPU_MAX_HW_QUEUES", "8", 0);
     Options o;
     const auto t0 = std::chrono::steady_clock::now();
     try {
@@ -1312,7 +1349,8 @@ int run_tool(int argc, char** argv) {
     } teardown{t0, t0, std::getenv("FQ_TIMING") != nullptr};
     try {
         const bool paired = o.paired();
-        const size_t pack_n = o.pack_pairs ? o.pack_pairs : std::max<size_t>(o.max_reads_in_pack, 262144);
+        // (raw streams: packs of 128 Ki pairs keep six windows' copies queued in 64 MiB windows)
+        const size_t pack_n = o.pack_pairs ? o.pack_pairs : std::max<size_t>(o.max_reads_in_pack, 131072);
         int est = std::max(o.est_seq_len1, paired ? o.est_seq_len2 : 0);
         const std::vector<int> devices = o.device_list();
         const int G = (int)devices.size();
@@ -1320,7 +1358,7 @@ int run_tool(int argc, char** argv) {
         // -w host threads (the reference's worker count) pack tiles, format and compress
         Pool pool(std::max(0, o.threads - 1));
         // (before the outputs: their writer threads hand text packs back to it until they close)
-        const int n_packs = G * (depth + 1) + 4;
+        const int n_packs = G * (depth + 1) + 6;  // (a raw stream keeps 4 in flight)
         Queue<std::unique_ptr<Pack>> spare((size_t)n_packs);
         for (int i = 0; i < n_packs; ++i) spare.push(std::unique_ptr<Pack>(new Pack(true)));
         Sink outs(o, &pool);
@@ -1428,7 +1466,7 @@ int run_tool(int argc, char** argv) {
                         if (o.adapter_trimming) {
                             if (pk->raw)
                                 for (int m = 0; m < (paired ? 2 : 1); ++m)
-                                    ac.add_entries(m, pk->ad[m].data(), pk->rout.adapter_bytes[m], p, &pool);
+                                    ac.add_entries(m, pk->out_text[m].data() + pk->tout.bytes[m], pk->rout.adapter_bytes[m], p, &pool);
                             else
                                 ac.add(*pk, pk->res.data(), p, &pool);
                         }
@@ -1506,7 +1544,8 @@ int run_tool(int argc, char** argv) {
                             std::to_string(lanes[0]->raw_packs) + " packs, ended: " + lanes[0]->raw_end + "; window reads " +
                             std::to_string(lanes[0]->raw_read_s) + " s, reader waiting for a stage " +
                             std::to_string(lanes[0]->raw_stage_wait_s) + " s, dispatcher waiting for windows " +
-                            std::to_string(lanes[0]->raw_ready_wait_s) + " s)"
+                            std::to_string(lanes[0]->raw_ready_wait_s) + " s, for a pack " + std::to_string(lanes[0]->raw_pack_wait_s) +
+                            " s, in enqueue " + std::to_string(lanes[0]->raw_enqueue_s) + " s)"
                       : text_mode ? " (text packs: GPU ingest/egress)" : "") + ", wall " +
             std::to_string(since(t0)) + " s, engine submit " + std::to_string(submit_s) + " s, wait " + std::to_string(wait_s) + " s; pre-pass " +
             std::to_string(prepass_s) + " s, adapter detection (concurrent) " + std::to_string(detect_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +

@@ -401,12 +401,15 @@ int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*
  *   last window enqueued) with carry left, or a window takes no pairs.
  * Protocol: fq_engine_raw_begin; enqueue window 0; then for k = 0, 1, ...: enqueue window k+1
  * (optional), fq_engine_raw_launch (window k: waits for its index), poll as for other packs.  At
- * most two windows are enqueued and not launched; a window's host bytes must stay valid until its
- * pack is reported by fq_engine_poll.  Options as for text packs (no -m, -c, UMI, index filter).
+ * most three windows are enqueued and not launched, and eight windows are in the engine (enqueued,
+ * launched or not yet polled: a ninth enqueue waits for the oldest pack's copies); a window's
+ * host bytes must stay valid until its pack is reported by fq_engine_poll.  Options as for text packs (no -m, -c, UMI, index filter).
  * The trimmed-adapter strings (FilterResult::addAdapterTrimmed, src/filterresult.cpp:138-157) come
- * back as entries "u16 ad_len (little endian), u8 neg, then ad_len bytes of the read (neg 0) or
- * u16 ad_pos (neg 1: the string is adapter[ad_pos, ad_pos + ad_len) of the mate's adapter
- * parameter)", copied by fq_engine_poll into out->adapters[m] (exact size, <= adapter_cap[m]). */
+ * back after the output text, at out->text.text[m] + out->text.bytes[m], adapter_bytes[m] bytes of
+ * entries "u16 ad_len (little endian), u8 neg, then ad_len bytes of the read (neg 0) or u16
+ * ad_pos (neg 1: the string is adapter[ad_pos, ad_pos + ad_len) of the mate's adapter parameter)";
+ * one copy back per mate, of the pack's text_bytes[m] + 3 * pairs + 16 bytes (a record's output
+ * plus its entry is at most its input + 3 bytes). */
 typedef struct fq_raw_window {
     const char* bytes[2]; /* mate m's next input bytes (bytes[1]: PE only) */
     uint64_t n[2];        /* their count, <= the window capacity given to fq_engine_raw_begin */
@@ -420,10 +423,8 @@ typedef struct fq_raw_result {
     uint64_t text_bytes[2]; /* mate m's text bytes the pack's records span */
 } fq_raw_result;
 typedef struct fq_raw_out {
-    fq_text_out text;          /* text[m]: >= carry capacity + window capacity + 16 bytes */
-    char* adapters[2];         /* trimmed-adapter entries of mate m */
-    uint64_t adapter_cap[2];
-    uint64_t adapter_bytes[2]; /* set by fq_engine_poll */
+    fq_text_out text;          /* text[m]: >= carry capacity + window bytes + 4 * max_batch + 16 */
+    uint64_t adapter_bytes[2]; /* set by fq_engine_poll: entries after the output text */
 } fq_raw_out;
 int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap);
 int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w);
