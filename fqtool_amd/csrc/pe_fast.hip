@@ -138,7 +138,7 @@ constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
 constexpr int kInsW = (512 + 1 + 1) & ~1;                 // insert-size histogram, u32 per workgroup
 // per-read scalars are spread over kScalCopies LDS copies (lane % copies), each
 // [4 stats][reads, length_sum, q20, q30] u64; the merge variant keeps 8 (LDS budget)
-constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4;
+constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4 + 16;  // adapter bytes of both mates + adseq_search's window words
 constexpr int kScalStride = FQ_SCAL_PAD ? 17 : 16;  // u64 per scalar copy (17: copies on distinct LDS bank pairs)
 constexpr int kPfW = FQ_PREFETCH ? 64 : 0;             // LDS-DMA prefetch sink (never read)
 // Every variant re-reads qualities from the rows in L2 (no LDS quality rows) and runs 16 waves
@@ -479,6 +479,78 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
     }
 }
 
+// AdapterTrimmer::trimBySequence (src/adaptertrimmer.cpp:29-90): the first pos in [start, n - 4)
+// whose window holds at most min(n - pos, alen) / 8 byte mismatches against the adapter.  The
+// reference tests every pos byte by byte; here a code-level lower bound over the first (up to) 16
+// compared positions rejects almost every pos without touching bytes, and only survivors get the
+// reference's exact byte test, in pos order.  The bound counts code mismatches only (an N or a
+// lowercase base shares its code with some upper-case letter), so it never exceeds the byte
+// count: a pos it rejects has more mismatches than allowed.  Valid for adapters of >= 20 upper-case
+// ACGT bytes (start = -4, and the windows of every negative pos lie inside the adapter's first 20
+// positions); the kernel start sets adw[5] and the window words (see pe_fast_kernel).
+//  * pos in [0, n - 16]: full 16-position windows, all at once (ov_candidates; bound < alen/8 + 1,
+//    a superset of every pos's own allowance);
+//  * pos in -4..-1 and [n - 15, n - 5]: one masked window each against that pos's allowance.
+// Read 2's column is the reverse complement (forward position j of the read window at column
+// kMaxLen - 1 - st - j), so its windows run down the column and its adapter words are stored
+// reversed and complemented; `fixed` word k = codes of adapter positions k .. k + 15.
+template <class SQ>
+__device__ inline bool adseq_search(const uint32_t* col, int c, bool rc, int st, int n, const uint32_t* adw, SQ r,
+                                    const uint8_t* ad, int alen, int& pos_out) {
+    auto exact = [&](int pos) -> bool {  // the reference's inner loop at one pos
+        const int cmplen = min(n - pos, alen), allowed = cmplen / 8;
+        int mm = 0;
+        for (int i = max(0, -pos); i < cmplen; ++i)
+            if (ad[i] != r(i + pos) && ++mm > allowed) return false;
+        return true;
+    };
+    // the 16-position window of forward read positions [j0, j0 + 16) against adapter word k, the
+    // first m read positions compared
+    auto bound = [&](int j0, int k, int m) -> int {
+        const int s = rc ? kMaxLen - 16 - st - j0 : st + j0;
+        const uint32_t mask = rc ? 0x55555555u & ~posmask(16 - m) : posmask(m);
+        return __popc(fold2(field_window(col, kFC, c, s) ^ adw[k]) & mask);
+    };
+    for (int pos = -4; pos < 0; ++pos) {
+        if (pos >= n - 4) return false;
+        if (bound(0, -pos, min(n, 16)) <= min(n - pos, alen) / 8 && exact(pos)) {
+            pos_out = pos;
+            return true;
+        }
+    }
+    if (n >= 16) {
+        uint32_t cand[kOvBlocks];
+        ov_candidates(col, c, rc ? kMaxLen - st - n : st, adw[0], alen / 8 + 1, n - 15, cand);
+        for (;;) {  // candidates in pos order: read 1 from the lowest offset, read 2 from the highest
+            int k = -1;
+            if (!rc) {
+#pragma unroll
+                for (int bk = kOvBlocks - 1; bk >= 0; --bk)
+                    if (cand[bk]) k = 32 * bk + __ffs(cand[bk]) - 1;
+            } else {
+#pragma unroll
+                for (int bk = 0; bk < kOvBlocks; ++bk)
+                    if (cand[bk]) k = 32 * bk + 31 - __clz(cand[bk]);
+            }
+            if (k < 0) break;
+            cand[k >> 5] &= ~(1u << (k & 31));
+            const int pos = rc ? n - 16 - k : k;
+            if (exact(pos)) {
+                pos_out = pos;
+                return true;
+            }
+        }
+    }
+    for (int pos = max(0, n - 15); pos < n - 4; ++pos) {
+        const int m = n - pos;  // < 16 <= alen: every compared position is in the window
+        if (bound(pos, 0, m) <= m / 8 && exact(pos)) {
+            pos_out = pos;
+            return true;
+        }
+    }
+    return false;
+}
+
 
 // PolyX::trimPolyG (src/polyx.cpp:14-38) on the code columns, one pass over 16-position groups
 // of scan indices (scan index i = forward position e - i, e = the window's last base).  A group
@@ -722,7 +794,7 @@ __device__ __forceinline__ int slot_class(int s) { return (0x67431 >> (4 * s)) &
 // (original - corrected) at the base's cycle (pre = kept + removed), and the per-read pre Q20/Q30
 // scalar gets the negated deltas.  Host side: the FASTQ text is corrected from the read-2 record's
 // (offset, overlap length, window length), flags FQ_RF_CORRECTED.
-__device__ inline void correct_pair_fast(const fq_params& p, uint32_t* col, uint32_t* lds, const fq_batch& b, size_t roff,
+__device__ inline bool correct_pair_fast(const fq_params& p, uint32_t* col, uint32_t* lds, const fq_batch& b, size_t roff,
                                          int mate, int lane_x, int mlane, int st1, int st2, int n2, const Overlap& ov,
                                          const uint8_t* Q, fq_read_result& rr, uint32_t& q20, uint32_t& q30,
                                          uint32_t& lowf, uint32_t& tqf, uint32_t& nbf, uint32_t limq,
@@ -789,7 +861,7 @@ __device__ inline void correct_pair_fast(const fq_params& p, uint32_t* col, uint
             atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + rcell(P, sn)), 0ull - (kCount1 | (unsigned long long)xn));
         }
     }
-    if (!corrected) return;
+    if (!corrected) return false;
     if (d20 | d30) atomicAdd(pre_q, 0ull - (unsigned long long)((long long)d20 * 4294967296LL + (long long)d30));
     if (mate ? cr2 : cr1) rr.flags |= FQ_RF_CORRECTED;
     if (mate) {  // what the host needs to correct the text (as fq_pack_kernel's correct_pair)
@@ -801,6 +873,7 @@ __device__ inline void correct_pair_fast(const fq_params& p, uint32_t* col, uint
         atomicAdd(&tail[FQ_ACC_TAIL_CORRECTED_READS], (cr1 && cr2) ? 2ull : 1ull);
         atomicAdd(&tail[FQ_ACC_TAIL_CORRECTED_BASES], (unsigned long long)corrected);
     }
+    return true;  // (pair-uniform: both lanes walk the same mismatches)
 }
 
 // XTRA: the -c / UMI / -e instantiation of the full variants (kept apart so the other variants'
@@ -827,6 +900,27 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
     for (int i = threadIdx.x; i < LY::kHistRegW + kSmallW + kInsW + LY::kScalW; i += kThreads) hist[i] = 0;
     for (int i = threadIdx.x; i < 2 * FQ_MAX_ADAPTER; i += kThreads)
         adp[i] = i < FQ_MAX_ADAPTER ? p.adapter1[i] : p.adapter2[i - FQ_MAX_ADAPTER];
+    // adseq_search's words: [mate * 8 + k] = 2-bit codes of adapter positions k .. k + 15 (k < 5;
+    // read 2: reversed and complemented, column order), [mate * 8 + 5] = 1 when the filter applies
+    // (>= 20 upper-case ACGT bytes)
+    uint32_t* adw = reinterpret_cast<uint32_t*>(adp) + 2 * FQ_MAX_ADAPTER / 4;
+    if (threadIdx.x < 12) {
+        const int m = threadIdx.x / 6, k = threadIdx.x % 6;
+        const uint8_t* a = m ? p.adapter2 : p.adapter1;
+        const int alen = m ? p.adapter2_len : p.adapter1_len;
+        uint32_t w = 0;
+        if (k < 5) {
+            for (int j = 0; j < 16; ++j) w |= (uint32_t)((a[k + j] >> 1) & 3) << (2 * j);  // A C T G -> 0 1 2 3
+            if (m) w = pairrev(w) ^ 0xAAAAAAAAu;
+        } else {
+            w = alen >= 20 && alen <= FQ_MAX_ADAPTER;
+            for (int j = 0; j < alen && j < FQ_MAX_ADAPTER; ++j) {
+                const uint8_t ch = a[j];
+                if (ch != 'A' && ch != 'C' && ch != 'G' && ch != 'T') w = 0;
+            }
+        }
+        adw[8 * m + k] = w;
+    }
     __syncthreads();
 
     // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
@@ -1194,7 +1288,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         // AdapterTrimmer::trimBySequence, src/adaptertrimmer.cpp:29-90
         auto by_sequence = [&]() {
             int pos;
-            if (trim_by_sequence_t(at(seq, st), n, my_ad, my_alen, pos)) {
+            const uint32_t* my_adw = adw + 8 * mate;
+            if (my_adw[5] ? adseq_search(col, lane, rc, st, n, my_adw, at(seq, st), my_ad, my_alen, pos)
+                          : trim_by_sequence_t(at(seq, st), n, my_ad, my_alen, pos)) {
                 int ad_len;
                 if (pos < 0) {
                     ad_len = my_alen + pos;
@@ -1274,7 +1370,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
         Overlap ov1{0, 0, 0, 0};  // (merge) the first analysis and the windows it saw
         int n1a = -1, n2a = -1;
-        bool ad_ov = false;
+        bool ad_ov = false, corr = false;  // (corr: -c changed a base of the pair)
         if (PAIRED && both && !(abl & 1)) {
             const Overlap ov = pair_overlap();
             const int n_o = xor32(n);
@@ -1294,7 +1390,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 // BaseCorrector::correctByOverlapAnalysis (src/basecorrector.cpp:14-70), pair-uniform
                 if (p.correction_enabled && ov.diff > 0 && ov.diff <= 5) {
                     const int st_o = xor32(st);
-                    correct_pair_fast(p, col, lds, b, roff, mate, lane_x, mlane, mate ? st_o : st, mate ? st : st_o, n2,
+                    corr = correct_pair_fast(p, col, lds, b, roff, mate, lane_x, mlane, mate ? st_o : st, mate ? st : st_o, n2,
                                       ov, Q, rr, q20, q30, lowf, tqf, nbf, limq,
                                       scal + kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 1,
                                       LY::kColsW + mate * (kRSlots * 32 * kChunks), acc);
@@ -1344,7 +1440,10 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             // bases at offset 0, the first offset phase 1 tries, so {1, 0, ol, diff}.
             const int n_o = xor32(n);
             const int n1c = mate ? n_o : n, n2c = mate ? n : n_o;
-            const bool same = n1a >= 0 && n1c == n1a && n2c == n2a;
+            // (-c: a corrected pair compares other bases than the first analysis did, so the same
+            // windows are analysed again; the derived case still holds: its offset 0 compares the
+            // overlap the first analysis accepted, with mismatches only removed by the correction)
+            const bool same = !corr && n1a >= 0 && n1c == n1a && n2c == n2a;
             const bool derived = n1a >= 0 && ad_ov && n1c == ov1.len && n2c == ov1.len && ov1.len == n2a + ov1.offset;
             Overlap ov2 = same ? ov1 : Overlap{1, 0, ov1.len, ov1.diff};
             if (!same && !derived) ov2 = pair_overlap();  // pair-uniform branch (the mate lanes swap values)
@@ -1899,9 +1998,10 @@ using namespace long320;
 
 #if FQ_MAXLEN == 160
 bool fq_pe_fast_supported(const fq_params& p) {
-    // -c with -m, front trimming or UMI, and UMI with -m run on the general kernel (fq_pack_kernel)
-    // -c: paired, no merge, no front trimming (its Stats fix-up is the removed-mode block's)
-    const bool corr_ok = !p.correction_enabled || (p.paired && !p.merge_enabled && p.trim_front1 == 0 &&
+    // -c with front trimming or UMI, and UMI with -m run on the general kernel (fq_pack_kernel)
+    // -c: paired, no front trimming (its Stats fix-up is the removed-mode block's); with -m the
+    // merge variant's -c instantiation (160-position rows)
+    const bool corr_ok = !p.correction_enabled || (p.paired && p.trim_front1 == 0 &&
                                                    p.trim_front2 == 0 && !p.cut_front && p.umi_front1 <= 0 &&
                                                    p.umi_front2 <= 0);
     // UMI trims with -m stay on the general kernel (the merge variant assumes reads from 0)
@@ -1948,6 +2048,7 @@ hipError_t FQ_PREPARE() {
     if ((e = set_lds<false, false, false, true>()) != hipSuccess) return e;
 #if FQ_MAXLEN == 160
     if ((e = set_lds<false, true, true, false>()) != hipSuccess) return e;
+    if ((e = set_lds<false, true, true, true>()) != hipSuccess) return e;
     return fq_pe_fast_long_prepare();
 #else
     return hipSuccess;
@@ -1984,7 +2085,9 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
     const bool xtra = p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0 || p.avg_qual_limit > 0;
     const int pad = p.reserved[2] > 0 && p.reserved[2] <= 4096 ? p.reserved[2] : 0;  // profiling: extra LDS (LEAN)
 #if FQ_MAXLEN == 160
-    if (p.merge_enabled)
+    if (p.merge_enabled && p.correction_enabled)  // -c -m: the merge variant with the -c code
+        launch_variant<false, true, true, true>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
+    else if (p.merge_enabled)
         launch_variant<false, true, true, false>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
     else
 #endif

@@ -107,6 +107,51 @@ def edge_pack(n, paired, stride=160, seed=7):
     return pk
 
 
+def adapter_pack(n, paired, ad1, ad2, stride=160, seed=5):
+    """Reads holding a copy of their mate's adapter at every kind of offset trimBySequence tests
+    (src/adaptertrimmer.cpp:29-90): its tail at the read start (pos -1 .. -6), anywhere inside,
+    cut off by the read end (pos up to L - 5 and beyond), with 0 .. allowance + 2 substitutions
+    (another base, 'N', the same letter in lower case), decoys with too many mismatches ahead of a
+    real copy, random lengths 0-stride.  Mates are independent random sequence, so almost no pair
+    overlaps and the by-sequence search runs on nearly every read."""
+    rng = random.Random(seed)
+    pk = Pack(n, stride, paired)
+    lens = [0, 1, 4, 5, 6, 8, 15, 16, 17, 19, 20, 21, 31, 32, 33, 40, 63, 64, 65, 100, 127, 145, 149, 150, 151, stride]
+    for i in range(n):
+        for m in ((1, 2) if paired else (1,)):
+            ad = (ad1 if m == 1 else ad2).encode()
+            L = rng.choice(lens)
+            seq = bytearray(rng.choice(b"ACGT") for _ in range(L))
+            copies = rng.choice([0, 1, 1, 1, 2])
+            for c in range(copies):
+                if L == 0 or not ad:
+                    break
+                pos = rng.randint(-min(6, len(ad) - 1), L - 1) if rng.random() < 0.6 else rng.randint(max(-6, L - 20), L - 1)
+                start = max(0, -pos)
+                piece = bytearray(ad[start:])
+                at = max(0, pos)
+                piece = piece[: L - at]
+                if not piece:
+                    continue
+                allowed = min(L - pos, len(ad)) // 8
+                subs = rng.randint(0, allowed + 2) if c == copies - 1 else allowed + 1 + rng.randint(0, 3)
+                for _ in range(subs):
+                    k = rng.randrange(len(piece))
+                    kind = rng.random()
+                    if kind < 0.6:
+                        piece[k] = rng.choice([b for b in b"ACGT" if b != piece[k]])
+                    elif kind < 0.8:
+                        piece[k] = ord("N")
+                    else:
+                        piece[k] = piece[k] | 0x20
+                seq[at:at + len(piece)] = piece
+            if L and rng.random() < 0.05:
+                seq[rng.randrange(L)] = ord("N")
+            qual = bytes(33 + rng.randint(10, 40) for _ in range(L))
+            pk.set(i, m, bytes(seq), qual)
+    return pk
+
+
 def polyx_pack(n, paired, stride=160, seed=11):
     """Reads ending in a homopolymer tail (A, T, C, G or N) of 1-24 bases with 0-3 substitutions at
     random tail positions, ahead of which sits random sequence: polyX scans that break before, at
@@ -219,6 +264,11 @@ def config(name, max_cycles=256):
         p.correction_enabled = 1
         p.merge_enabled = 1
         p.cut_right = 1
+    elif name == "PE_correct_merge":  # -c with the config-4 options (the merge variant's -c instantiation)
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.cut_right = 1
+        p.merge_enabled = 1
+        p.correction_enabled = 1
     elif name == "PE_correct_x":  # -c with the config-5 options (the fast kernels' -c variant)
         p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
         abi.set_adapter(p, 1, AD1)
@@ -258,7 +308,7 @@ def config(name, max_cycles=256):
 
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
                "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR2", "PE_cutR5", "PE_cutRF", "PE_merge_q",
-               "PE_correct", "PE_correct_all", "PE_correct_x", "PE_umi", "PE_umi_x", "SE_umi"]
+               "PE_correct", "PE_correct_all", "PE_correct_merge", "PE_correct_x", "PE_umi", "PE_umi_x", "SE_umi"]
 
 
 def run_oracle(oracle, p, pk):

@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 from fqtool_amd import abi
-from batch_util import AD1, AD2, ALL_CONFIGS, Pack, config, edge_pack, polyx_pack, polyx_params, run_oracle, synth_pack
+from batch_util import (AD1, AD2, ALL_CONFIGS, Pack, adapter_pack, config, edge_pack, polyx_pack, polyx_params, run_oracle,
+                        synth_pack)
 
 pytestmark = pytest.mark.gpu
 
@@ -79,6 +80,26 @@ def test_polyx_tails(eng_lib, oracle, paired, mask, max_mm, per, req):
     p = polyx_params(paired, mask, max_mm, per, req)
     pk = polyx_pack(4000, paired, seed=mask * 131 + max_mm * 7 + per + req)
     res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
+@pytest.mark.parametrize("stride", [160, 336])
+@pytest.mark.parametrize("ads", [(AD1, AD2), (AD1[:20], AD2[:21]), (AD1[:19], AD2[:16]),
+                                 ("AGATCGGAAGAGCNCACGTCTG", "agatcggaagagcgtcgtgtag"), (AD1 + AD2, AD2[:8])])
+@pytest.mark.parametrize("name", ["C3b", "SE_adapter", "PE_correct_x", "PE_merge_q"])
+def test_adapter_by_sequence(eng_lib, oracle, name, ads, stride):
+    """trimBySequence at every offset kind (adapter_pack) with adapters the fast kernels filter
+    on the code columns (>= 20 upper-case ACGT bytes) and ones they search byte by byte (shorter,
+    with an N, lower case), on both column builds."""
+    p = config(name, max_cycles=512)
+    abi.set_adapter(p, 1, ads[0])
+    if p.paired:
+        abi.set_adapter(p, 2, ads[1])
+    pk = adapter_pack(5003, bool(p.paired), ads[0], ads[1], stride=stride, seed=len(ads[0]) * 7 + len(ads[1]) + stride)
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    flags = res_o["flags"]
+    assert ((flags & abi.FQ_RF_AD_SEQ) != 0).sum() > pk.n // 20
     res_e, acc_e = run_engine(eng_lib, p, pk)
     assert_same(p, res_o, acc_o, res_e, acc_e)
 
@@ -155,7 +176,8 @@ def test_dense_per_pair_handoff(eng_lib, oracle, name, stride):
 
 
 @pytest.mark.parametrize("stride", [160, 336])
-@pytest.mark.parametrize("name", ["C3", "C3b", "C4", "C5", "PE_all", "PE_correct", "PE_umi_x", "C2", "SE_all"])
+@pytest.mark.parametrize("name", ["C3", "C3b", "C4", "C5", "PE_all", "PE_correct", "PE_correct_merge", "PE_umi_x", "C2",
+                                  "SE_all"])
 def test_lowercase_bases(eng_lib, oracle, name, stride):
     """Soft-masked reads: lowercase a c g t stay on the fast kernels (a per-base flag beside the
     codes) -- stretches anywhere in either mate, lowercase polyG / polyX tails, lowercase adapter

@@ -32,6 +32,9 @@ for cfg in os.environ.get("CONFIGS", "C3").split():
     p = bench.config_params(abi, cfg)
     p.correction_enabled = int(os.environ.get("CORRECT", 0))  # -c on top of the config
     p.umi_front1 = p.umi_front2 = int(os.environ.get("UMI", 0))  # UMI cut from both reads
+    if os.environ.get("ADAPTERS"):  # explicit adapters (trimBySequence), as bench's c3b_adapter_seq
+        abi.set_adapter(p, 1, "AGATCGGAAGAGCACACGTCTGAACTCCAGTCA")
+        abi.set_adapter(p, 2, "AGATCGGAAGAGCGTCGTGTAGGGAAAGAGTGT")
     p.reserved[0] = int(os.environ.get("ABL", 0))  # ablation bits (pe_fast.hip; results invalid when set)
     if cfg == "C2":
         b.seq2 = b.qual2 = None
