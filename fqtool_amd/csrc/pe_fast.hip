@@ -150,7 +150,9 @@ struct Layout {
     // quality rows staged in LDS (off: rows are re-read from L2); profiling switch for the merge variant
     static constexpr bool kQLds = MERGE && FQ_MERGE_QLDS;
     static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160) ? 1 : MERGE ? FQ_MERGE_BLOCKS : LEAN ? FQ_LEAN_BLOCKS : 2;
-    static constexpr int kWaves = MERGE ? (kQLds ? 7 : FQ_MERGE_WAVES) : (LEAN && kMaxLen <= 160) ? FQ_LEAN_WAVES : 8;
+    // (the long build's merge variant: its 320-position columns and 640-cycle merged Stats fit 4 waves)
+    static constexpr int kWaves = MERGE ? (kQLds ? 7 : kMaxLen > 160 ? 4 : FQ_MERGE_WAVES)
+                                        : (LEAN && kMaxLen <= 160) ? FQ_LEAN_WAVES : 8;
     static constexpr int kWavesPerEU = (kWaves * kBlocksPerCU + 3) / 4;
     static constexpr int kThreads = 64 * kWaves;
     static constexpr int kWaveW = kCodeW + (kQLds ? 64 * kQS : 0);
@@ -1998,15 +2000,14 @@ using namespace long320;
 
 #if FQ_MAXLEN == 160
 bool fq_pe_fast_supported(const fq_params& p) {
-    // -c with front trimming or UMI, and UMI with -m run on the general kernel (fq_pack_kernel)
+    // -c with front trimming or UMI runs on the general kernel (fq_pack_kernel)
     // -c: paired, no front trimming (its Stats fix-up is the removed-mode block's); with -m the
     // merge variant's -c instantiation (160-position rows)
     const bool corr_ok = !p.correction_enabled || (p.paired && p.trim_front1 == 0 &&
                                                    p.trim_front2 == 0 && !p.cut_front && p.umi_front1 <= 0 &&
                                                    p.umi_front2 <= 0);
-    // UMI trims with -m stay on the general kernel (the merge variant assumes reads from 0)
-    const bool umi_ok = (p.umi_front1 <= 0 && p.umi_front2 <= 0) || !p.merge_enabled;
-    return p.insert_size_max <= 512 && p.insert_size_max >= 0 && corr_ok && umi_ok &&
+    // (UMI with -m: the merge variant's -c / UMI instantiation, whose Stats run in pre/post mode)
+    return p.insert_size_max <= 512 && p.insert_size_max >= 0 && corr_ok &&
            (!p.merge_enabled || (p.paired && !p.complexity_enabled));
 }
 
@@ -2051,7 +2052,8 @@ hipError_t FQ_PREPARE() {
     if ((e = set_lds<false, true, true, true>()) != hipSuccess) return e;
     return fq_pe_fast_long_prepare();
 #else
-    return hipSuccess;
+    if ((e = set_lds<false, true, true, false>()) != hipSuccess) return e;
+    return set_lds<false, true, true, true>();
 #endif
 }
 
@@ -2073,7 +2075,7 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
                      int* slow_tiles, int* slow_count, int grid, hipStream_t stream) {
 #if FQ_MAXLEN == 160
     // rows longer than 160 bytes: the 320-position build (reads beyond 320 bp are handed off per tile)
-    if (b.stride > kMaxLen && !p.merge_enabled)
+    if (b.stride > kMaxLen)
         return fq_launch_pe_fast_long(p, b, res, acc, slow_tiles, slow_count, grid, stream);
 #endif
     const bool lean = p.trim_front1 == 0 && p.trim_tail1 == 0 && p.trim_front2 == 0 && p.trim_tail2 == 0 &&
@@ -2084,13 +2086,11 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
     // -c, UMI and -e (the whole-read quality total) run on the XTRA instantiations (lean is false then)
     const bool xtra = p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0 || p.avg_qual_limit > 0;
     const int pad = p.reserved[2] > 0 && p.reserved[2] <= 4096 ? p.reserved[2] : 0;  // profiling: extra LDS (LEAN)
-#if FQ_MAXLEN == 160
-    if (p.merge_enabled && p.correction_enabled)  // -c -m: the merge variant with the -c code
+    if (p.merge_enabled && (p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0))  // -c / UMI with -m
         launch_variant<false, true, true, true>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
     else if (p.merge_enabled)
         launch_variant<false, true, true, false>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
     else
-#endif
     if (p.paired && lean)
         launch_variant<true, true, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, pad, stream);
     else if (p.paired && xtra)

@@ -283,6 +283,11 @@ def config(name, max_cycles=256):
         abi.set_adapter(p, 2, AD2)
         p.cut_right = 1
         p.umi_front1, p.umi_front2 = 8, 12
+    elif name == "PE_umi_merge":  # UMI in both reads with the config-4 options (pre/post Stats in the merge variant)
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.cut_right = 1
+        p.merge_enabled = 1
+        p.umi_front1, p.umi_front2 = 9, 6
     elif name == "SE_umi":
         p.polyg_enabled = 1
         p.cut_tail = 1
@@ -308,7 +313,7 @@ def config(name, max_cycles=256):
 
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
                "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR2", "PE_cutR5", "PE_cutRF", "PE_merge_q",
-               "PE_correct", "PE_correct_all", "PE_correct_merge", "PE_correct_x", "PE_umi", "PE_umi_x", "SE_umi"]
+               "PE_correct", "PE_correct_all", "PE_correct_merge", "PE_correct_x", "PE_umi", "PE_umi_x", "PE_umi_merge", "SE_umi"]
 
 
 def run_oracle(oracle, p, pk):

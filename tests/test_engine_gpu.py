@@ -406,7 +406,7 @@ def test_async_submit_poll_pipeline(eng_lib, oracle):
 @pytest.mark.parametrize("L,stride", [(250, 256), (300, 304)])
 def test_long_read_parity(eng_lib, oracle, name, L, stride):
     """2x250 / 2x300 rows run on the 320-position build of the fast kernels (pe_fast_long.hip;
-    -m keeps the general kernel for them)."""
+    -m on its 4-wave merge variant)."""
     p = config(name, max_cycles=640)
     pk = synth_pack(oracle, 3000, bool(p.paired), first=777, L=L, stride=stride)
     res_o, acc_o = run_oracle(oracle, p, pk)

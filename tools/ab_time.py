@@ -8,13 +8,14 @@ import bench
 
 lib = abi.load_engine()
 dev = torch.device("cuda:0")
-n, stride = int(os.environ.get("PAIRS", 20_000_000)), 160
+n, stride = int(os.environ.get("PAIRS", 20_000_000)), int(os.environ.get("STRIDE", 160))
+RL = int(os.environ.get("L", 150))  # read length (long rows: STRIDE 256 / 304 with L 250 / 300)
 bufs = [torch.empty(abi.batch_bytes(n, stride), dtype=torch.uint8, device=dev) for _ in range(4)]
 lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
 b = abi.FqBatch(); b.n, b.stride = n, stride
 b.seq1, b.qual1, b.seq2, b.qual2 = [t.data_ptr() for t in bufs]
 b.len1, b.len2 = lens[0].data_ptr(), lens[1].data_ptr()
-assert lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 0, 150, None) == 0
+assert lib.fq_synth_fill_device(ctypes.byref(b), 20261015, 0, RL, None) == 0
 res = torch.empty(n * 32, dtype=torch.uint8, device=dev)
 fe = int(os.environ.get("INDEX_EVERY", 0))
 if fe:  # every fe-th pair dropped by the host's index filter (fq_batch.flags)
@@ -30,6 +31,7 @@ torch.cuda.synchronize()
 tag = os.environ.get("TAG", "")
 for cfg in os.environ.get("CONFIGS", "C3").split():
     p = bench.config_params(abi, cfg)
+    p.max_cycles = max(p.max_cycles, 2 * RL + 16)
     p.correction_enabled = int(os.environ.get("CORRECT", 0))  # -c on top of the config
     p.umi_front1 = p.umi_front2 = int(os.environ.get("UMI", 0))  # UMI cut from both reads
     if os.environ.get("ADAPTERS"):  # explicit adapters (trimBySequence), as bench's c3b_adapter_seq
