@@ -800,7 +800,7 @@ __device__ inline bool correct_pair_fast(const fq_params& p, uint32_t* col, uint
                                          int mate, int lane_x, int mlane, int st1, int st2, int n2, const Overlap& ov,
                                          const uint8_t* Q, fq_read_result& rr, uint32_t& q20, uint32_t& q30,
                                          uint32_t& lowf, uint32_t& tqf, uint32_t& nbf, uint32_t limq,
-                                         unsigned long long* pre_q, int rem_block, unsigned long long* acc) {
+                                         unsigned long long* pre_q, int rem_block, bool removed, unsigned long long* acc) {
     const int ol = ov.len;
     const int start1 = max(0, ov.offset), start2 = n2 - max(0, -ov.offset) - 1;
     const int a0 = st1 + start1;                  // read 1's forward position at overlap index 0
@@ -857,10 +857,18 @@ __device__ inline bool correct_pair_fast(const fq_params& p, uint32_t* col, uint
             tqf += xn - xo;
             nbf += nN - oN;
             // forward codes (read 2's column holds complements; N stays code 3) -> removed slots
+            // (removed mode), or the pre block's slots A C T G N with the +128 quality bias
+            // (pre/post mode: front trimming, UMI)
             const uint32_t fo = mate && !oN ? ocode ^ 2u : ocode, fn = mate && !nN ? ncode ^ 2u : ncode;
-            const int so = oN ? kRNSlot : (int)fo, sn = nN ? kRNSlot : (int)fn;
-            atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + rcell(P, so)), kCount1 | (unsigned long long)xo);
-            atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + rcell(P, sn)), 0ull - (kCount1 | (unsigned long long)xn));
+            if (removed) {
+                const int so = oN ? kRNSlot : (int)fo, sn = nN ? kRNSlot : (int)fn;
+                atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + rcell(P, so)), kCount1 | (unsigned long long)xo);
+                atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + rcell(P, sn)), 0ull - (kCount1 | (unsigned long long)xn));
+            } else {
+                const int so = oN ? 4 : (int)fo, sn = nN ? 4 : (int)fn;
+                atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + cell(P, so)), kCount1 | (unsigned long long)(xo | 0x80u));
+                atomicAdd(reinterpret_cast<unsigned long long*>(lds + rem_block + cell(P, sn)), 0ull - (kCount1 | (unsigned long long)(xn | 0x80u)));
+            }
         }
     }
     if (!corrected) return false;
@@ -1395,7 +1403,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                     corr = correct_pair_fast(p, col, lds, b, roff, mate, lane_x, mlane, mate ? st_o : st, mate ? st : st_o, n2,
                                       ov, Q, rr, q20, q30, lowf, tqf, nbf, limq,
                                       scal + kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 1,
-                                      LY::kColsW + mate * (kRSlots * 32 * kChunks), acc);
+                                      removed_mode ? LY::kColsW + mate * (kRSlots * 32 * kChunks) : LY::kColsW + mate * kHistW,
+                                      removed_mode, acc);
                 }
             }
             if (p.adapter_trimming) {
@@ -2000,12 +2009,9 @@ using namespace long320;
 
 #if FQ_MAXLEN == 160
 bool fq_pe_fast_supported(const fq_params& p) {
-    // -c with front trimming or UMI runs on the general kernel (fq_pack_kernel)
-    // -c: paired, no front trimming (its Stats fix-up is the removed-mode block's); with -m the
-    // merge variant's -c instantiation (160-position rows)
-    const bool corr_ok = !p.correction_enabled || (p.paired && p.trim_front1 == 0 &&
-                                                   p.trim_front2 == 0 && !p.cut_front && p.umi_front1 <= 0 &&
-                                                   p.umi_front2 <= 0);
+    // -c: paired (the XTRA instantiations; with -m the merge variant's); its Stats fix-up goes to
+    // the removed-mode block, or with front trimming / UMI to the pre block
+    const bool corr_ok = !p.correction_enabled || p.paired;
     // (UMI with -m: the merge variant's -c / UMI instantiation, whose Stats run in pre/post mode)
     return p.insert_size_max <= 512 && p.insert_size_max >= 0 && corr_ok &&
            (!p.merge_enabled || (p.paired && !p.complexity_enabled));

@@ -269,6 +269,17 @@ def config(name, max_cycles=256):
         p.cut_right = 1
         p.merge_enabled = 1
         p.correction_enabled = 1
+    elif name == "PE_correct_front":  # -c with front trimming (pre/post Stats: the fix-up in the pre block)
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.correction_enabled = 1
+        p.cut_front, p.cut_front_window, p.cut_front_quality = 1, 4, 20
+        p.trim_front1, p.trim_tail1, p.trim_front2 = 2, 1, 5
+    elif name == "PE_correct_umi_merge":  # -c, UMI in both reads and -m (the merge variant's -c/UMI code)
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.correction_enabled = 1
+        p.merge_enabled = 1
+        p.cut_right = 1
+        p.umi_front1, p.umi_front2 = 8, 4
     elif name == "PE_correct_x":  # -c with the config-5 options (the fast kernels' -c variant)
         p.adapter_trimming = p.polyg_enabled = p.polyx_enabled = 1
         abi.set_adapter(p, 1, AD1)
@@ -313,7 +324,8 @@ def config(name, max_cycles=256):
 
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
                "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR2", "PE_cutR5", "PE_cutRF", "PE_merge_q",
-               "PE_correct", "PE_correct_all", "PE_correct_merge", "PE_correct_x", "PE_umi", "PE_umi_x", "PE_umi_merge", "SE_umi"]
+               "PE_correct", "PE_correct_all", "PE_correct_merge", "PE_correct_x", "PE_umi", "PE_umi_x", "PE_umi_merge",
+               "PE_correct_front", "PE_correct_umi_merge", "SE_umi"]
 
 
 def run_oracle(oracle, p, pk):
