@@ -1591,10 +1591,36 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
             tq += xor32(tq);
             w20 += xor32(w20);
             w30 += xor32(w30);
-            // (OverlapAnalysis::merge returns NULL for ol 0; the complexity filter is excluded
-            // from the merge variant)
+            // Filter::passLowComplexityFliter of the merged read (src/filter.cpp:54-67): adjacent
+            // differences within read 1's part (bytes as they are), within read 2's part (its
+            // bytes complemented, util::complement: upper-cased, so compared upper-cased), and
+            // across the junction (read 1's last byte against the complement of read 2's byte at
+            // the part's high end, which comes first in the merged read)
+            int cdiff = 0;
+            if (p.complexity_enabled) {
+                int d = 0;
+                for (int i = 0; i + 1 < wn; ++i) {
+                    const int x = seq(ws + i), y = seq(ws + i + 1);
+                    d += mate ? (x & 0xDF) != (y & 0xDF) : x != y;
+                }
+                int edge = 0;
+                if (wn > 0) {
+                    const int x = seq(ws + wn - 1);
+                    if (!mate) edge = x;
+                    else switch (x & 0xDF) {
+                        case 'A': edge = 'T'; break;
+                        case 'C': edge = 'G'; break;
+                        case 'G': edge = 'C'; break;
+                        case 'T': edge = 'A'; break;
+                        default: edge = 'N';
+                    }
+                }
+                const int d_o = xor32(d), e_o = xor32(edge);
+                cdiff = d + d_o + ((m1 > 0 && m2 > 0 && edge != e_o) ? 1 : 0);
+            }
+            // (OverlapAnalysis::merge returns NULL for ol 0)
             code = (mol == 0 || mlen == 0) ? FQ_FAIL_LENGTH
-                                           : filter_verdict(p, mlen, low, nb, tq - 33 * mlen, [&]() { return 0; });
+                                           : filter_verdict(p, mlen, low, nb, tq - 33 * mlen, [&]() { return cdiff; });
         }
         const int code_o = PAIRED ? xor32(code) : code;
         const bool pair_pass = both && code == FQ_PASS_FILTER && code_o == FQ_PASS_FILTER;
@@ -2014,7 +2040,7 @@ bool fq_pe_fast_supported(const fq_params& p) {
     const bool corr_ok = !p.correction_enabled || p.paired;
     // (UMI with -m: the merge variant's -c / UMI instantiation, whose Stats run in pre/post mode)
     return p.insert_size_max <= 512 && p.insert_size_max >= 0 && corr_ok &&
-           (!p.merge_enabled || (p.paired && !p.complexity_enabled));
+           (!p.merge_enabled || p.paired);
 }
 
 // profiling aid (tools/ablate.py --phases): read and clear the per-phase cycle totals

@@ -269,6 +269,11 @@ def config(name, max_cycles=256):
         p.cut_right = 1
         p.merge_enabled = 1
         p.correction_enabled = 1
+    elif name == "PE_merge_complexity":  # -m with the low-complexity filter (merged reads: both parts + junction)
+        p.adapter_trimming = p.polyg_enabled = 1
+        p.merge_enabled = 1
+        p.complexity_enabled, p.complexity_threshold = 1, 0.745
+        p.n_base_limit = 2
     elif name == "PE_correct_front":  # -c with front trimming (pre/post Stats: the fix-up in the pre block)
         p.adapter_trimming = p.polyg_enabled = 1
         p.correction_enabled = 1
@@ -325,7 +330,7 @@ def config(name, max_cycles=256):
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
                "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR2", "PE_cutR5", "PE_cutRF", "PE_merge_q",
                "PE_correct", "PE_correct_all", "PE_correct_merge", "PE_correct_x", "PE_umi", "PE_umi_x", "PE_umi_merge",
-               "PE_correct_front", "PE_correct_umi_merge", "SE_umi"]
+               "PE_correct_front", "PE_correct_umi_merge", "PE_merge_complexity", "SE_umi"]
 
 
 def run_oracle(oracle, p, pk):

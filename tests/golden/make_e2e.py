@@ -13,7 +13,7 @@ For every case in CASES: exit status, sha256 + line count of each (decompressed)
 JSON report text (gzip) are written under tests/golden/e2e/.  The Software block of the JSON
 (command line, cwd) is environment-dependent and is compared with those values masked.
 
-Run from the repo root:  python3 tests/golden/make_e2e.py
+Run from the repo root:  python3 tests/golden/make_e2e.py [case ...]
 """
 import ctypes
 import gzip
@@ -81,6 +81,15 @@ CASES = {
                    "--unpaired_read2 {out}/u2.fq --failed_out {out}/failed.fq",
     "edge_pe_merge": "-i {in}/edge_r1.fq -I {in}/edge_r2.fq -o {out}/o1.fq -O {out}/o2.fq -q -a -g -m "
                      "--merge_output {out}/merged.fq",
+    # -m with the low-complexity filter (merged reads), -c with front trimming, -c + UMI + -m
+    "td_pe_merge_complexity": "-i {in}/r1.fq.gz -I {in}/r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -q -a -g -y -Y 0.45 "
+                              "-m --merge_output {out}/merged.fq",
+    "edge_pe_merge_complexity": "-i {in}/edge_r1.fq -I {in}/edge_r2.fq -o {out}/o1.fq -O {out}/o2.fq -y -Y 0.3 -m "
+                                "--merge_output {out}/merged.fq",
+    "edge_pe_correct_front": "-i {in}/edge_r1.fq -I {in}/edge_r2.fq -o {out}/o1.fq -O {out}/o2.fq -c -q -a -f 3 -F 2 "
+                             "--enable_cut_front --cut_front_window 5 --cut_front_mean_qual 22",
+    "synth_pe_correct_umi_merge": "-i {in}/synth_r1.fq.gz -I {in}/synth_r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -c -q -a "
+                                  "-g -u --umi_location 6 --umi_length 6 -m --merge_output {out}/merged.fq",
     "edge_se_all": "-i {in}/edge_r1.fq -o {out}/o1.fq -q -a -g -x -y -l --enable_cut_front --enable_cut_tail "
                    "--failed_out {out}/failed.fq",
     "edge64_pe": "-i {in}/edge64_r1.fq -I {in}/edge64_r2.fq --phred64 -o {out}/o1.fq -O {out}/o2.fq -q -a -g",
@@ -253,9 +262,15 @@ def main():
         sys.exit("build the reference first: make -f oracle/Makefile.ref")
     make_inputs()
     os.makedirs(OUT, exist_ok=True)
+    only = sys.argv[1:]  # case names: regenerate just these, keeping the other fixtures as they are
     manifest = {}
+    if only:
+        with open(os.path.join(OUT, "manifest.json")) as f:
+            manifest = json.load(f)
     with tempfile.TemporaryDirectory() as tmp:
         for name, args in CASES.items():
+            if only and name not in only:
+                continue
             r = run_case(REF_BIN, name, args, tmp)
             if r["json"] is not None:
                 with gzip.GzipFile(os.path.join(OUT, name + ".json.gz"), "wb", compresslevel=9, mtime=0) as f:
