@@ -441,7 +441,7 @@ class HipRunner:
 
     def paths_leg(self, pairs):
         """Off the BASELINE configs: C3's options with explicit adapter sequences (C3b, trimBySequence),
-        with UMI (8 + 8), with -c, and with 1 % of the
+        with UMI (8 + 8), with -c, C4's with -c, and with 1 % of the
         pairs holding a lowercase base (handed to the general kernel one by one), on the first
         `pairs` pairs of the resident shard; kernel ms per launch from HIP events on the launch
         stream (median of 3 after a warm-up).  Runs after every check: -c rewrites corrected
@@ -486,6 +486,9 @@ class HipRunner:
         p = config_params(abi, "C3")
         p.correction_enabled = 1
         timed(p, "c3_correct")
+        p = config_params(abi, "C4")  # -m with -c: the merge variant's -c instantiation
+        p.correction_enabled = 1
+        timed(p, "c4_correct")
         i = torch.arange(0, n, 100, device=self.dev, dtype=torch.int64)
         self.planes[0][(i // abi.TILE_READS) * abi.TILE_READS * STRIDE + (i % abi.TILE_READS) * 16 + 5] = ord("a")
         timed(config_params(abi, "C3"), "c3_lowercase_1pct")

@@ -411,6 +411,9 @@ static int validate_host_batch(fq_engine* e, const fq_batch* hb) {
         return fail(e, FQ_E_INVALID, "batch exceeds the engine's max_batch/max_stride (or stride % 16 != 0)");
     if (!hb->seq1 || !hb->qual1 || !hb->len1 || (pe && (!hb->seq2 || !hb->qual2 || !hb->len2)))
         return fail(e, FQ_E_INVALID, "missing batch arrays");
+    // -c hands the host the overlap offset of a corrected pair in a 16-bit signed record field
+    if (e->p.correction_enabled && hb->stride > 32768)
+        return fail(e, FQ_E_INVALID, "-c takes reads of at most 32767 bases (the record's overlap offset is 16-bit)");
     // (read lengths are checked on the device: a read longer than max_cycles or the stride sets
     // the pack's error word, which fq_engine_poll reports as FQ_E_TOO_LONG)
     return FQ_OK;
@@ -794,6 +797,8 @@ int fq_engine_process_device(fq_engine* e, const fq_batch* db, fq_read_result* d
     if (db->n < 0 || db->stride <= 0 || (db->stride & 15) || !db->seq1 || !db->qual1 || !db->len1 ||
         (e->p.paired && (!db->seq2 || !db->qual2 || !db->len2)))
         return fail(e, FQ_E_INVALID, "bad device batch");
+    if (e->p.correction_enabled && db->stride > 32768)
+        return fail(e, FQ_E_INVALID, "-c takes reads of at most 32767 bases (the record's overlap offset is 16-bit)");
     HIP_TRY(e, hipSetDevice(e->device));
     // NULL is the HIP default stream
     return launch(e, *db, dres, (hipStream_t)stream, e->scratch, true, true, e->calls++, e->err);
