@@ -9,8 +9,11 @@
 #include <cstring>
 #include <deque>
 #include <emmintrin.h>
+#include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <thread>
+#include <unistd.h>
 #include <exception>
 #include <iostream>
 #include <memory>
@@ -231,10 +234,141 @@ bool FqReader::read(std::string& name, std::string& seq, std::string& strand, st
     return true;
 }
 
+// ---- BGZF input ----
+// A .gz regular file whose members all carry BGZF's 'BC' size field (bgzip, samtools, this tool's
+// own writer) is inflated member by member on several threads: the member chain is walked from
+// the headers alone when the file is opened (it must cover the file exactly), then batches of
+// members are inflated in parallel into one buffer at their prefix-summed offsets, each checked
+// against its CRC32 and ISIZE.  The byte stream is the one gzread would give; any other .gz goes
+// through zlib's stream reader as in the reference (src/fqreader.cpp:3-16).
+class BgzfSource {
+   public:
+    static std::unique_ptr<BgzfSource> open(const std::string& path) {
+        const int fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) return nullptr;
+        struct stat st;
+        if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < 28) {
+            ::close(fd);
+            return nullptr;
+        }
+        void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+        ::close(fd);
+        if (m == MAP_FAILED) return nullptr;
+        std::unique_ptr<BgzfSource> b(new BgzfSource(static_cast<const unsigned char*>(m), (size_t)st.st_size));
+        if (!b->walk()) return nullptr;
+        madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
+        return b;
+    }
+    ~BgzfSource() { munmap(const_cast<unsigned char*>(map_), size_); }
+    // up to `want` more bytes of the decompressed stream into dst; false on corrupt data
+    bool read(char* dst, size_t want, size_t& got) {
+        got = 0;
+        while (got < want) {
+            if (pos_ == buf_.size()) {
+                if (next_ == members_.size()) break;
+                if (!inflate_batch()) return false;
+                continue;
+            }
+            const size_t n = std::min(want - got, buf_.size() - pos_);
+            std::memcpy(dst + got, buf_.data() + pos_, n);
+            pos_ += n;
+            got += n;
+        }
+        return true;
+    }
+
+   private:
+    struct Member {
+        size_t data, clen;  // deflate payload offset and length
+        uint32_t crc, isize;
+    };
+    BgzfSource(const unsigned char* m, size_t n) : map_(m), size_(n) {}
+    static uint32_t le16(const unsigned char* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
+    static uint32_t le32(const unsigned char* p) { return le16(p) | le16(p + 2) << 16; }
+    // the member chain from the headers (RFC 1952 header, BGZF 'BC' extra subfield)
+    bool walk() {
+        for (size_t o = 0; o < size_;) {
+            const unsigned char* h = map_ + o;
+            if (size_ - o < 28 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4) || (h[3] & 0xe0)) return false;
+            const size_t xlen = le16(h + 10);
+            if (12 + xlen > size_ - o) return false;
+            size_t bsize = 0;
+            for (size_t x = 12; x + 4 <= 12 + xlen;) {
+                const size_t slen = le16(h + x + 2);
+                if (h[x] == 'B' && h[x + 1] == 'C' && slen == 2 && x + 6 <= 12 + xlen) bsize = le16(h + x + 4) + 1;
+                x += 4 + slen;
+            }
+            size_t p = 12 + xlen;
+            auto skipz = [&]() {
+                while (o + p < size_ && h[p]) ++p;
+                ++p;
+            };
+            if (h[3] & 8) skipz();   // FNAME
+            if (h[3] & 16) skipz();  // FCOMMENT
+            if (h[3] & 2) p += 2;    // FHCRC
+            if (!bsize || bsize > size_ - o || p + 8 > bsize) return false;
+            members_.push_back(Member{o + p, bsize - p - 8, le32(h + bsize - 8), le32(h + bsize - 4)});
+            o += bsize;
+        }
+        return !members_.empty();
+    }
+    // the next batch of members (~64 MB of output) inflated on up to kThreads threads
+    bool inflate_batch() {
+        static const int kThreads = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2));
+        size_t end = next_, total = 0;
+        std::vector<size_t> at;
+        while (end < members_.size() && (total < ((size_t)64 << 20) || end == next_)) {
+            at.push_back(total);
+            total += members_[end].isize;
+            ++end;
+        }
+        buf_.resize(total);
+        pos_ = 0;
+        const size_t first = next_, cnt = end - first;
+        next_ = end;
+        std::atomic<bool> ok{true};
+        const int nt = (int)std::min<size_t>((size_t)kThreads, cnt);
+        auto work = [&](int t) {
+            z_stream z;
+            std::memset(&z, 0, sizeof z);
+            if (inflateInit2(&z, -15) != Z_OK) {
+                ok = false;
+                return;
+            }
+            for (size_t i = cnt * (size_t)t / nt; i < cnt * (size_t)(t + 1) / nt && ok; ++i) {
+                const Member& mb = members_[first + i];
+                inflateReset(&z);
+                z.next_in = const_cast<Bytef*>(map_ + mb.data);
+                z.avail_in = (uInt)mb.clen;
+                Bytef* out = reinterpret_cast<Bytef*>(&buf_[0]) + at[i];
+                unsigned char dummy;
+                z.next_out = mb.isize ? out : &dummy;
+                z.avail_out = mb.isize ? (uInt)mb.isize : 1u;
+                if (inflate(&z, Z_FINISH) != Z_STREAM_END || z.total_out != mb.isize ||
+                    (uint32_t)crc32(crc32(0, nullptr, 0), out, mb.isize) != mb.crc)
+                    ok = false;
+            }
+            inflateEnd(&z);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+        if (nt > 0) work(0);
+        for (auto& x : th) x.join();
+        return ok;
+    }
+    const unsigned char* map_;
+    size_t size_;
+    std::vector<Member> members_;
+    size_t next_ = 0;
+    std::string buf_;
+    size_t pos_ = 0;
+};
+
 // ---- FqBulkReader ----
 FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     : phred64_(phred64), bsize_((uint64_t)buf_size) {
     if (ends_with(path, ".gz")) {
+        if ((bgzf_ = BgzfSource::open(path))) return;
         gz_ = gzopen(path.c_str(), "r");
         if (!gz_) throw std::runtime_error("Failed to open file: " + path);
         gzbuffer(gz_, 1 << 20);
@@ -303,7 +437,9 @@ void FqBulkReader::read_more() {
     size_t want = (size_t)(want_end - total_);
     char* dst = text_->extend(want);
     size_t got = 0;
-    if (gz_) {
+    if (bgzf_) {
+        if (!bgzf_->read(dst, want, got)) reader_stderr("Error to read gzip file\n");
+    } else if (gz_) {
         while (got < want) {
             const unsigned ask = (unsigned)std::min<size_t>(want - got, 1u << 30);
             const int r = gzread(gz_, dst + got, ask);
@@ -915,22 +1051,52 @@ Writer::Writer(const std::string& path, int level) : gzip_(ends_with(path, ".gz"
 }
 
 namespace {
-// one complete gzip member holding `s` (src/writer.cpp:36-47 writes through gzwrite at level -z)
+// `s` as BGZF members (blocked gzip, SAM/BAM spec 4.1: each member of at most 65280 input bytes
+// carries its compressed size in a 'BC' extra field), so readers -- this tool's included -- can
+// inflate the members on several threads; any gzip reader reads them as a plain multi-member
+// stream.  (src/writer.cpp:36-47 writes one gzwrite stream at level -z; the decompressed text is
+// what parity compares.)  An empty `s` gives one empty member.
 std::string gzip_member(const std::string& s, int level) {
+    constexpr size_t kIn = 0xff00;
     z_stream z;
     std::memset(&z, 0, sizeof z);
-    if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+    if (deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK)
         throw std::runtime_error("deflateInit2 failed");
     std::string out;
-    out.resize(deflateBound(&z, (uLong)s.size()) + 64);
-    z.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(s.data()));
-    z.avail_in = (uInt)s.size();
-    z.next_out = reinterpret_cast<Bytef*>(&out[0]);
-    z.avail_out = (uInt)out.size();
-    const int rc = deflate(&z, Z_FINISH);
+    std::string tmp(deflateBound(&z, (uLong)kIn) + 64, '\0');
+    int cur = level;
+    size_t o = 0;
+    do {
+        const size_t n = std::min(kIn, s.size() - o);
+        const Bytef* in = reinterpret_cast<const Bytef*>(s.data() + o);
+        size_t clen = 0;
+        for (int lvl : {level, 0}) {  // (a member that does not shrink enough is stored)
+            deflateReset(&z);
+            if (lvl != cur) {
+                if (deflateParams(&z, lvl, Z_DEFAULT_STRATEGY) != Z_OK) throw std::runtime_error("deflateParams failed");
+                cur = lvl;
+            }
+            z.next_in = const_cast<Bytef*>(in);
+            z.avail_in = (uInt)n;
+            z.next_out = reinterpret_cast<Bytef*>(&tmp[0]);
+            z.avail_out = (uInt)tmp.size();
+            if (deflate(&z, Z_FINISH) != Z_STREAM_END) throw std::runtime_error("deflate failed");
+            clen = z.total_out;
+            if (clen + 26 <= 65536) break;
+        }
+        if (clen + 26 > 65536) throw std::runtime_error("deflate: BGZF block too large");
+        const uint32_t bsize = (uint32_t)(clen + 25), crc = (uint32_t)crc32(crc32(0, nullptr, 0), in, (uInt)n);
+        const unsigned char hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0,
+                                       (unsigned char)(bsize & 0xff), (unsigned char)(bsize >> 8)};
+        out.append(reinterpret_cast<const char*>(hdr), 18);
+        out.append(tmp.data(), clen);
+        const unsigned char tr[8] = {(unsigned char)crc, (unsigned char)(crc >> 8), (unsigned char)(crc >> 16),
+                                     (unsigned char)(crc >> 24), (unsigned char)n, (unsigned char)(n >> 8),
+                                     (unsigned char)(n >> 16), (unsigned char)(n >> 24)};
+        out.append(reinterpret_cast<const char*>(tr), 8);
+        o += n;
+    } while (o < s.size());
     deflateEnd(&z);
-    if (rc != Z_STREAM_END) throw std::runtime_error("deflate failed");
-    out.resize(z.total_out);
     return out;
 }
 }  // namespace

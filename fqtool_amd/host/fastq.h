@@ -105,6 +105,8 @@ struct Rec {
     size_t qual_off() const { return strand_off() + strand_len + gap[2]; }
 };
 
+class BgzfSource;
+
 class FqReader {
    public:
     // buf_size: the reference's read buffer (1 MiB, src/fqreader.cpp:10); smaller only in tests
@@ -179,6 +181,7 @@ class FqBulkReader {
     bool skip_ok(uint64_t g) const;
     void read_more();
     gzFile gz_ = nullptr;
+    std::unique_ptr<BgzfSource> bgzf_;  // BGZF input: members inflated on several threads
     FILE* fp_ = nullptr;
     bool phred64_;
     uint64_t bsize_;

@@ -7,8 +7,11 @@ behaviour (exit status + message) of the real binary, which fails before touchin
 GPU: the real `fqtool` binary, engine on MI355X, byte-identical outputs and JSON.
 """
 import ctypes
+import gzip
 import os
+import struct
 import subprocess
+import zlib
 
 import pytest
 
@@ -46,6 +49,53 @@ def test_host_pipeline_threaded(case, host, oracle, tmp_path):
         argv[2] = "4"
     report = E.run_session_with_oracle(host, oracle, argv, max_n=700)
     E.check_outputs(case, str(tmp_path), report)
+
+
+def bgzf(raw, level=6, member=0xff00):
+    """BGZF (SAM/BAM spec 4.1) members of `member` input bytes each, then the empty EOF member."""
+    out = bytearray()
+    for o in range(0, len(raw), member):
+        blk = raw[o:o + member]
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        d = c.compress(blk) + c.flush()
+        out += bytes([0x1F, 0x8B, 8, 4, 0, 0, 0, 0, 0, 0xFF, 6, 0, 66, 67, 2, 0]) + struct.pack("<H", len(d) + 25)
+        out += d + struct.pack("<II", zlib.crc32(blk), len(blk))
+    c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    d = c.compress(b"") + c.flush()
+    out += bytes([0x1F, 0x8B, 8, 4, 0, 0, 0, 0, 0, 0xFF, 6, 0, 66, 67, 2, 0]) + struct.pack("<H", len(d) + 25)
+    return bytes(out + d + struct.pack("<II", 0, 0))
+
+
+@pytest.mark.parametrize("case,kind", [("td_pe_qag", "bgzf"), ("td_pe_gz", "bgzf"), ("td_se_q", "bgzf"),
+                                       ("td_pe_split_num_gz", "bgzf"), ("td_pe_qag", "multi"), ("td_pe_qag", "bgzf_bad")])
+def test_bgzf_and_multi_member_inputs(case, kind, host, oracle, tmp_path):
+    """The testdata inputs recompressed as BGZF (members inflated on several threads by the bulk
+    reader), as plain multi-member gzip (zlib's stream reader), and as BGZF whose last member's
+    size field is off by one (not a BGZF chain: zlib's reader): the same outputs and JSON as the
+    reference run on the original files.  The tool's own .gz outputs are BGZF."""
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    out.mkdir()
+    for name in ("r1.fq.gz", "r2.fq.gz"):
+        with open(os.path.join(E.INPUTS, name), "rb") as f:
+            raw = gzip.decompress(f.read())
+        if kind == "multi":
+            data = b"".join(gzip.compress(raw[o:o + 100_000], 6) for o in range(0, len(raw), 100_000))
+        else:
+            data = bgzf(raw, member=30_000 if kind == "bgzf_bad" else 0xFF00)
+            if kind == "bgzf_bad":  # BSIZE of the EOF member one too large: the chain overruns the file
+                data = bytearray(data)
+                data[-28 + 16] += 1
+                data = bytes(data)
+        (inp / name).write_bytes(data)
+    argv = [a.replace(E.INPUTS, str(inp)) for a in E.argv_for("fqtool", case, str(out))]
+    report = E.run_session_with_oracle(host, oracle, argv)
+    E.check_outputs(case, str(out), report)
+    for name in os.listdir(out):
+        if name.endswith(".gz"):
+            with open(out / name, "rb") as f:
+                head = f.read(18)
+            assert head[:4] == bytes([0x1F, 0x8B, 8, 4]) and head[12:14] == b"BC", name
 
 
 @pytest.mark.parametrize("case", E.err_cases())
