@@ -594,10 +594,14 @@ bool FqBulkReader::read(Rec& r) {  // FqReader::read, src/fqreader.cpp:160-195
 // first irregular record, or where a record is not complete inside the region; read() continues
 // from there with the exact rules.  Phred64 conversion is applied to the kept records only.
 size_t FqBulkReader::read_fast(std::vector<Rec>& out, size_t max_n, Pool* pool) {
-    if (!map_ || !pool || max_n < 1024 || pos_ >= map_size_) return 0;
-    char* d = map_;
+    if ((!map_ && !text_) || !pool || max_n < 1024) return 0;
     const size_t r0 = pos_, avg = avg_rec_ ? avg_rec_ : 512;
-    const size_t r1 = std::min(map_size_, r0 + max_n * avg + max_n * avg / 16 + (1u << 16));
+    const size_t want = r0 + max_n * avg + max_n * avg / 16 + (1u << 16);
+    if (!map_)  // a stream (BGZF, gzip, pipe): the arena first holds the region, as far as the input goes
+        while (!eof_ && sz() < want) read_more();
+    if (pos_ >= sz()) return 0;
+    char* d = dat();
+    const size_t r1 = std::min(sz(), want);
     const size_t words = (r1 - r0 + 63) >> 6;
     std::vector<uint64_t> bm(words + 1, 0);  // bit i of word w: byte r0 + 64 w + i is '\r' / '\n'
     const int K = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool->size() * 2, (r1 - r0) >> 20));

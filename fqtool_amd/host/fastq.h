@@ -160,9 +160,10 @@ class FqBulkReader {
     // next record into the arena given to begin(); false at end of input or on a
     // quality/sequence length mismatch (message in error())
     bool read(Rec& r);
-    // Parallel fast path of read() for a mapped regular file: appends up to max_n records to `out`
-    // from the "plain" stretch at the read position (see fastq.cpp) and returns their count;
-    // read() then continues exactly where it stopped.  0 when the input is not mapped.
+    // Parallel fast path of read(): appends up to max_n records to `out` from the "plain" stretch
+    // at the read position (see fastq.cpp) and returns their count; read() then continues exactly
+    // where it stopped.  A mapped file is parsed in place; a stream (BGZF, gzip, pipe) once the
+    // arena holds the region.
     size_t read_fast(std::vector<Rec>& out, size_t max_n, Pool* pool);
     // the arena is done: unconsumed bytes are carried to the next begin(); returns the base
     // the records' offsets refer to (the arena, or the file mapping)

@@ -101,6 +101,45 @@ def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
     return wall, (m.group(1) if m else None) + ((" | " + t.group(1)) if t else ""), o
 
 
+def _bgzf_chunk(arg):
+    path, off, n = arg
+    import struct
+    import zlib
+    with open(path, "rb") as f:
+        f.seek(off)
+        raw = f.read(n)
+    out = bytearray()
+    for o in range(0, len(raw), 0xFF00):
+        blk = raw[o:o + 0xFF00]
+        c = zlib.compressobj(1, zlib.DEFLATED, -15)
+        d = c.compress(blk) + c.flush()
+        out += bytes([0x1F, 0x8B, 8, 4, 0, 0, 0, 0, 0, 0xFF, 6, 0, 66, 67, 2, 0]) + struct.pack("<H", len(d) + 25)
+        out += d + struct.pack("<II", zlib.crc32(blk), len(blk))
+    return bytes(out)
+
+
+def compress_inputs(paths, kind):
+    """The generated FASTQ as BGZF (level 1, on a process pool) or as one gzip stream (gzip -1)."""
+    import multiprocessing as mp
+    import subprocess
+
+    out = []
+    for p in paths:
+        gz = p + ".gz"
+        if kind == "bgzf":
+            size, step = os.path.getsize(p), 0xFF00 * 64
+            with mp.Pool(16) as pool, open(gz, "wb") as f:
+                for blob in pool.imap(_bgzf_chunk, [(p, o, min(step, size - o)) for o in range(0, size, step)], 4):
+                    f.write(blob)
+                f.write(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+        else:
+            with open(gz, "wb") as f:
+                subprocess.run(["gzip", "-1", "-c", p], stdout=f, check=True)
+        os.remove(p)
+        out.append(gz)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=2_000_000)
@@ -113,6 +152,7 @@ def main():
     ap.add_argument("--variants", default=None, help="';'-separated list of --extra strings, each run in turn")
     ap.add_argument("--null-out", action="store_true", help="FASTQ outputs to /dev/null (as bench.py's e2e leg)")
     ap.add_argument("--workers-list", default=None, help="comma list of -w values to run (overrides --workers)")
+    ap.add_argument("--gz", default=None, choices=["bgzf", "gzip"], help="compressed inputs: BGZF or one gzip stream")
     args = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="fqe2e_")
     try:
@@ -120,6 +160,11 @@ def main():
         r1, r2 = gen_fastq(args.pairs, tmp)
         gb = (os.path.getsize(r1) + os.path.getsize(r2)) / 1e9
         print(f"[e2e] wrote {args.pairs} pairs ({gb:.2f} GB FASTQ) in {time.perf_counter() - t0:.1f}s", flush=True)
+        if args.gz:
+            t0 = time.perf_counter()
+            r1, r2 = compress_inputs([r1, r2], args.gz)
+            gzb = (os.path.getsize(r1) + os.path.getsize(r2)) / 1e9
+            print(f"[e2e] compressed to {args.gz} ({gzb:.2f} GB) in {time.perf_counter() - t0:.1f}s", flush=True)
         reads = 2 * args.pairs
         ours = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
         variants = args.variants.split(";") if args.variants else [args.extra]
