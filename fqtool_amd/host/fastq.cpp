@@ -15,6 +15,7 @@
 #include <thread>
 #include <unistd.h>
 #include <exception>
+#include <future>
 #include <iostream>
 #include <memory>
 #include <mutex>
@@ -259,14 +260,13 @@ class BgzfSource {
         madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
         return b;
     }
-    ~BgzfSource() { munmap(const_cast<unsigned char*>(map_), size_); }
     // up to `want` more bytes of the decompressed stream into dst; false on corrupt data
     bool read(char* dst, size_t want, size_t& got) {
         got = 0;
         while (got < want) {
             if (pos_ == buf_.size()) {
-                if (next_ == members_.size()) break;
-                if (!inflate_batch()) return false;
+                if (!next_batch()) return false;
+                if (buf_.empty()) break;  // end of the stream
                 continue;
             }
             const size_t n = std::min(want - got, buf_.size() - pos_);
@@ -275,6 +275,10 @@ class BgzfSource {
             got += n;
         }
         return true;
+    }
+    ~BgzfSource() {
+        if (ahead_.valid()) ahead_.wait();
+        munmap(const_cast<unsigned char*>(map_), size_);
     }
 
    private:
@@ -312,20 +316,36 @@ class BgzfSource {
         }
         return !members_.empty();
     }
-    // the next batch of members (~64 MB of output) inflated on up to kThreads threads
-    bool inflate_batch() {
+    // the current batch is used up: take the one inflated ahead (or inflate one now), and start
+    // inflating the following batch while this one is read
+    bool next_batch() {
+        pos_ = 0;
+        bool ok = true;
+        if (ahead_.valid()) {
+            ok = ahead_.get();
+            buf_.swap(ahead_buf_);
+        } else {
+            ok = inflate_batch(buf_, next_);
+        }
+        if (ok && next_ < members_.size())
+            ahead_ = std::async(std::launch::async, [this] { return inflate_batch(ahead_buf_, next_); });
+        return ok;
+    }
+    // the members from `first` (~64 MB of output) inflated into `out` on up to kThreads threads;
+    // advances `first` past them
+    bool inflate_batch(std::string& out, size_t& first_io) {
         static const int kThreads = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2));
-        size_t end = next_, total = 0;
+        const size_t first = first_io;
+        size_t end = first, total = 0;
         std::vector<size_t> at;
-        while (end < members_.size() && (total < ((size_t)64 << 20) || end == next_)) {
+        while (end < members_.size() && (total < ((size_t)64 << 20) || end == first)) {
             at.push_back(total);
             total += members_[end].isize;
             ++end;
         }
-        buf_.resize(total);
-        pos_ = 0;
-        const size_t first = next_, cnt = end - first;
-        next_ = end;
+        out.resize(total);
+        const size_t cnt = end - first;
+        first_io = end;
         std::atomic<bool> ok{true};
         const int nt = (int)std::min<size_t>((size_t)kThreads, cnt);
         auto work = [&](int t) {
@@ -340,12 +360,12 @@ class BgzfSource {
                 inflateReset(&z);
                 z.next_in = const_cast<Bytef*>(map_ + mb.data);
                 z.avail_in = (uInt)mb.clen;
-                Bytef* out = reinterpret_cast<Bytef*>(&buf_[0]) + at[i];
+                Bytef* o = reinterpret_cast<Bytef*>(&out[0]) + at[i];
                 unsigned char dummy;
-                z.next_out = mb.isize ? out : &dummy;
+                z.next_out = mb.isize ? o : &dummy;
                 z.avail_out = mb.isize ? (uInt)mb.isize : 1u;
                 if (inflate(&z, Z_FINISH) != Z_STREAM_END || z.total_out != mb.isize ||
-                    (uint32_t)crc32(crc32(0, nullptr, 0), out, mb.isize) != mb.crc)
+                    (uint32_t)crc32(crc32(0, nullptr, 0), o, mb.isize) != mb.crc)
                     ok = false;
             }
             inflateEnd(&z);
@@ -359,9 +379,10 @@ class BgzfSource {
     const unsigned char* map_;
     size_t size_;
     std::vector<Member> members_;
-    size_t next_ = 0;
-    std::string buf_;
+    size_t next_ = 0;          // first member not yet inflated (or being inflated ahead)
+    std::string buf_, ahead_buf_;
     size_t pos_ = 0;
+    std::future<bool> ahead_;  // the next batch, inflating while buf_ is read
 };
 
 // ---- FqBulkReader ----
