@@ -645,6 +645,12 @@ def run_rank(args):
                 "frac_at_profiled_clock": sq.get("valu_issue_frac"), "src": sq_src,
                 "wait_frac": sq.get("wait_frac"), "inst_stall_frac": sq.get("inst_stall_frac"),
                 "active_frac": sq.get("active_frac")}
+        act = sq["counters_per_launch"].get("SQ_ACTIVE_INST_VALU")
+        if act and sq.get("kernel_cycles"):
+            # the SIMDs' VALU issue occupancy: SQ_ACTIVE_INST_VALU (quad cycles summed over waves) x 4
+            # over SIMDs x the profiled kernel cycles -- most VOP3 ops hold a SIMD ~4.5 cycles, not 2
+            # (profiles/r03_micro_opcost.txt), so this, not `frac`, is the issue-bound measure
+            valu["issue_busy_frac"] = round(act * 4 / (SIMDS * sq["kernel_cycles"]), 4)
     bytes_per_pair = (2 if paired else 1) * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result per read
     achieved = n * bytes_per_pair / (kavg / 1e3) / 1e9 if kavg else None
     out = {

@@ -2035,11 +2035,11 @@ using namespace long320;
 
 #if FQ_MAXLEN == 160
 bool fq_pe_fast_supported(const fq_params& p) {
-    // -c: paired (the XTRA instantiations; with -m the merge variant's); its Stats fix-up goes to
-    // the removed-mode block, or with front trimming / UMI to the pre block
-    const bool corr_ok = !p.correction_enabled || p.paired;
-    // (UMI with -m: the merge variant's -c / UMI instantiation, whose Stats run in pre/post mode)
-    return p.insert_size_max <= 512 && p.insert_size_max >= 0 && corr_ok &&
+    // -c runs on the XTRA instantiations (with -m the merge variant's); its Stats fix-up goes to the
+    // removed-mode block, or with front trimming / UMI to the pre block.  Single-end -c is a no-op
+    // (SingleEndProcessor never corrects, src/seprocessor.cpp).  UMI with -m: the merge variant's
+    // -c / UMI instantiation, whose Stats run in pre/post mode.
+    return p.insert_size_max <= 512 && p.insert_size_max >= 0 &&
            (!p.merge_enabled || p.paired);
 }
 

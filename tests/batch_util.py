@@ -184,7 +184,7 @@ def polyx_params(paired, mask, max_mm, per, compare_req, max_cycles=512):
 
 def config(name, max_cycles=256):
     """Parameter presets: the BASELINE configs plus extra option coverage."""
-    paired = name not in ("C2", "SE_adapter", "SE_all", "SE_umi")
+    paired = name not in ("C2", "SE_adapter", "SE_all", "SE_umi", "SE_correct")
     p = abi.default_params(paired=paired, max_cycles=max_cycles)
     p.qual_filter_enabled = 1  # every config has -q
     if name == "C2":
@@ -304,6 +304,10 @@ def config(name, max_cycles=256):
         p.cut_right = 1
         p.merge_enabled = 1
         p.umi_front1, p.umi_front2 = 9, 6
+    elif name == "SE_correct":  # -c on single-end input: a no-op, as in SingleEndProcessor
+        p.adapter_trimming = p.polyg_enabled = 1
+        abi.set_adapter(p, 1, AD1)
+        p.correction_enabled = 1
     elif name == "SE_umi":
         p.polyg_enabled = 1
         p.cut_tail = 1
@@ -330,7 +334,7 @@ def config(name, max_cycles=256):
 ALL_CONFIGS = ["C2", "C3", "C3b", "C4", "C5", "PE_all", "PE_merge_discard", "SE_adapter", "SE_all",
                "PE_cut1", "PE_cut4", "PE_cut11", "PE_cut40", "PE_cutR1", "PE_cutR2", "PE_cutR5", "PE_cutRF", "PE_merge_q",
                "PE_correct", "PE_correct_all", "PE_correct_merge", "PE_correct_x", "PE_umi", "PE_umi_x", "PE_umi_merge",
-               "PE_correct_front", "PE_correct_umi_merge", "PE_merge_complexity", "SE_umi"]
+               "PE_correct_front", "PE_correct_umi_merge", "PE_merge_complexity", "SE_correct", "SE_umi"]
 
 
 def run_oracle(oracle, p, pk):

@@ -86,6 +86,7 @@ CASES = {
                               "-m --merge_output {out}/merged.fq",
     "edge_pe_merge_complexity": "-i {in}/edge_r1.fq -I {in}/edge_r2.fq -o {out}/o1.fq -O {out}/o2.fq -y -Y 0.3 -m "
                                 "--merge_output {out}/merged.fq",
+    "td_se_correct": "-i {in}/r1.fq.gz -o {out}/o1.fq -c -q -g",
     "edge_pe_correct_front": "-i {in}/edge_r1.fq -I {in}/edge_r2.fq -o {out}/o1.fq -O {out}/o2.fq -c -q -a -f 3 -F 2 "
                              "--enable_cut_front --cut_front_window 5 --cut_front_mean_qual 22",
     "synth_pe_correct_umi_merge": "-i {in}/synth_r1.fq.gz -I {in}/synth_r2.fq.gz -o {out}/o1.fq -O {out}/o2.fq -c -q -a "
