@@ -11,7 +11,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/round_profiles
 OUT=gpurun_out/round_profiles
 export TMPDIR=/tmp
-ARGS="--config $CFG --pairs $PAIRS --steps 5 --warmup 1 --no-cpu-baseline"
+ARGS="--config $CFG --pairs $PAIRS --steps 5 --warmup 1 --no-cpu-baseline --paths-pairs 0"
 rm -rf gpurun_out/kt_$CFG gpurun_out/pmc_fetch gpurun_out/pmc_write
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_$CFG -o kt -- python3 bench.py $ARGS \
     > gpurun_out/kt_$CFG.log 2>&1 || { echo "kernel trace failed rc=$?"; exit 1; }
