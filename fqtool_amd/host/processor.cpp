@@ -918,10 +918,33 @@ struct Lane {
         const size_t raw_ahead = 3;  // windows enqueued ahead of their launch (the copy-in queue)
         if (fq_engine_raw_begin(e, wcap, ccap) != FQ_OK)
             throw std::runtime_error(std::string("fq_engine_raw_begin: ") + fq_engine_last_error(e));
-        const int kStages = raw_depth + (int)raw_ahead + 2;  // in flight + enqueued + being filled
-        while ((int)stages.size() < kStages) {
-            stages.emplace_back(new Stage);
-            free_stages.push((int)stages.size() - 1);
+        // in flight + enqueued + being filled, and four more so the window reader can run ahead
+        // of the packs (a stage comes back only when its pack completes)
+        const char* st_env = std::getenv("FQ_RAW_STAGES");  // (profiling)
+        const int kStages = std::max(raw_depth + (int)raw_ahead + 2, st_env ? std::atoi(st_env) : raw_depth + (int)raw_ahead + 6);
+        // The first new stage is handed out at once; the others are made page-locked (~0.06 s/GiB)
+        // on a helper thread and handed out as they become ready, so their registration overlaps
+        // the first windows instead of stalling the reader.
+        std::thread warmer;
+        struct Joiner {
+            std::thread& t;
+            ~Joiner() {
+                if (t.joinable()) t.join();
+            }
+        } warmer_join{warmer};
+        if ((int)stages.size() < kStages) {
+            const int have = (int)stages.size();
+            while ((int)stages.size() < kStages) stages.emplace_back(new Stage);
+            free_stages.push(have);
+            warmer = std::thread([this, have, kStages, wcap, mates] {
+                try {
+                    for (int i = have + 1; i < kStages; ++i) {
+                        for (int m = 0; m < mates; ++m) stages[(size_t)i]->buf[m].reserve((size_t)wcap);
+                        if (!free_stages.push(i)) break;
+                    }
+                } catch (...) {  // (no page-locked memory left: the stages made so far suffice)
+                }
+            });
         }
         struct Win {
             uint64_t start[2] = {0, 0}, n[2] = {0, 0};
