@@ -234,15 +234,19 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             tool = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
             cmd = [tool, "-i", big[0], "-I", big[1], "-o", "/dev/null", "-O", "/dev/null", *opts, "-w", str(workers),
                    "-J", os.path.join(tmp, "amd.json"), "-H", os.path.join(tmp, "amd.html")]
-            t0 = time.perf_counter()
-            p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
-            dt = time.perf_counter() - t0
-            if p.returncode != 0:
-                raise RuntimeError("fqtool failed: " + p.stderr[-2000:])
-            tool_log = [l for l in p.stderr.splitlines() if "fqtool-amd:" in l]
+            runs = []  # three runs (the copy pipeline's run-to-run spread is wide): the median is reported
+            for _ in range(3):
+                t0 = time.perf_counter()
+                p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+                dt = time.perf_counter() - t0
+                if p.returncode != 0:
+                    raise RuntimeError("fqtool failed: " + p.stderr[-2000:])
+                runs.append((dt, [l for l in p.stderr.splitlines() if "fqtool-amd:" in l]))
+            dt, tool_log = sorted(runs, key=lambda r: r[0])[1]
             gb = (os.path.getsize(big[0]) + os.path.getsize(big[1])) / 1e9
             out["e2e"] = {"value": round(2 * e2e_pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": e2e_pairs,
                           "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
+                          "runs_wall_s": [round(r[0], 3) for r in runs],
                           "path": "fqtool binary: FASTQ (page cache) -> parse -> pinned packs -> engine (cuda:0) -> "
                                   "format -> /dev/null + JSON, C3 options",
                           "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
