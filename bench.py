@@ -60,6 +60,19 @@ def pmc_traffic(cfg, pairs):
     return int(d["traffic_bytes"]), os.path.relpath(paths[-1], REPO)
 
 
+def e2e_path(tool_log):
+    """What the e2e run did, from the tool's own log lines: the raw stream (GPU record indexing and
+    output text), text packs (host parse, device planes and text) or host packs."""
+    text = " ".join(tool_log or [])
+    if "raw stream" in text:
+        mid = "pread into page-locked windows -> GPU record indexing -> kernels -> GPU output text"
+    elif "text packs" in text:
+        mid = "host parse -> text packs -> device planes -> kernels -> GPU output text"
+    else:
+        mid = "host parse -> pinned tile packs -> kernels -> records -> host formatting"
+    return f"fqtool binary: FASTQ (page cache) -> {mid} -> /dev/null + JSON, C3 options"
+
+
 def sq_profile(cfg, pairs):
     """VALU wave-instructions per launch of the fast kernel for this workload, from the latest
     committed SQ counter profile (tools/pmc_sq.sh + tools/pmc_sq_summary.py: rocprofv3 --pmc
@@ -247,8 +260,7 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             out["e2e"] = {"value": round(2 * e2e_pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": e2e_pairs,
                           "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
                           "runs_wall_s": [round(r[0], 3) for r in runs],
-                          "path": "fqtool binary: FASTQ (page cache) -> parse -> pinned packs -> engine (cuda:0) -> "
-                                  "format -> /dev/null + JSON, C3 options",
+                          "path": e2e_path(tool_log),
                           "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
         ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
         if os.path.exists(ref):
@@ -639,6 +651,12 @@ def run_rank(args):
     traffic, traffic_src = pmc_traffic(args.config, args.pairs) if world == 1 else (None, None)
     sq, sq_src = sq_profile(args.config, args.pairs) if world == 1 else (None, None)
     valu = None
+    if sq and kavg and sq.get("kernel_ms_trace") and abs(sq["kernel_ms_trace"] / kavg - 1) > 0.05:
+        # the committed SQ counters were taken on another build (its kernel time differs from this
+        # run's by more than 5 %): not reported as this build's
+        log(f"SQ profile {sq_src} is stale ({sq['kernel_ms_trace']:.3f} ms vs this run's {kavg:.3f} ms): not used")
+        valu = {"stale_profile": sq_src, "profile_kernel_ms": sq["kernel_ms_trace"], "run_kernel_ms": round(kavg, 3)}
+        sq = None
     if sq and kavg and sq.get("counters_per_launch", {}).get("SQ_INSTS_VALU"):
         # VALU issue fraction: each wave64 VALU instruction holds a SIMD-32 for 2 cycles
         # (MI355X_MICROARCH.md); peak = 1024 SIMDs x 2.4 GHz; the instruction count is the committed
@@ -674,7 +692,12 @@ def run_rank(args):
                    "first_index": first,
                    "read_len": READ_LEN, "row_stride": STRIDE,
                    "parallelism": f"dp{world} (pairs sharded, RCCL sum of the accumulator block)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+        # frac / achieved / peak are the HBM roofline (algorithmic bytes over the kernel time);
+        # `bound` names what limits the kernel: VALU issue when the SQ counters show the SIMDs' issue
+        # busier than HBM is, else HBM
+        "roofline": {"bound": ("valu_issue" if valu and valu.get("issue_busy_frac") and achieved and
+                               valu["issue_busy_frac"] > achieved / HBM_PEAK_GBS + 0.1 else "hbm"),
+                     "frac_of": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": traffic, "traffic_unit": "bytes per launch (PMC)", "traffic_src": traffic_src,
                      "algorithmic_bytes": n * bytes_per_pair,

@@ -749,6 +749,17 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     return FQ_OK;
 }
 
+int fq_engine_raw_end(fq_engine* e) {
+    if (!e) return FQ_E_INVALID;
+    if (!e->raw) return FQ_OK;
+    HIP_TRY(e, hipSetDevice(e->device));
+    if (e->s_idx) HIP_TRY(e, hipStreamSynchronize(e->s_idx));  // (the index stream waits for the copies)
+    e->raw_queued.clear();
+    e->raw_prev_slot = -1;
+    e->raw = false;
+    return FQ_OK;
+}
+
 int fq_host_register(const void* p, size_t bytes) {
     if (!p || !bytes) return FQ_E_INVALID;
     return hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterReadOnly) == hipSuccess ? FQ_OK : FQ_E_HIP;

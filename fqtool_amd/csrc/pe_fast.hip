@@ -100,6 +100,9 @@ namespace {
 #ifndef FQ_STATS_AHEAD
 #define FQ_STATS_AHEAD 2  // removed-mode Stats: quality chunks requested this many chunks ahead
 #endif
+#ifndef FQ_PLAUNDER
+#define FQ_PLAUNDER 1  // re-read fq_params / fq_batch from the kernarg segment every tile (SGPR pressure)
+#endif
 #ifndef FQ_PREFETCH
 #define FQ_PREFETCH 0  // profiling: after staging, pull the first FQ_PREFETCH chunks of the wave's next tile
                        // toward L2 with LDS-DMA loads (0: off; measured slower at 10)
@@ -886,6 +889,33 @@ __device__ inline bool correct_pair_fast(const fq_params& p, uint32_t* col, uint
     return true;  // (pair-uniform: both lanes walk the same mismatches)
 }
 
+// Per-launch constants derived from fq_params.  With FQ_PLAUNDER the kernel derives them again at the
+// top of every tile from a re-read of the kernarg segment (see the tile loop).
+#define FQ_DERIVE_PARAMS() \
+    [[maybe_unused]] const int abl = p.reserved[0]; \
+    [[maybe_unused]] const int nchunks = FIX ? kChunks : min(kChunks, b.stride >> 4); \
+    [[maybe_unused]] const int limit = p.overlap_diff_limit; \
+    [[maybe_unused]] const int K = max(limit, 1); \
+    [[maybe_unused]] const int req = p.overlap_require; \
+    [[maybe_unused]] const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u; \
+    /* cut_right threshold 33 + q, in 0..93 (CLI range): the same SWAR below-threshold test */ \
+    [[maybe_unused]] const bool lowr_ok = p.cut_right && 33 + p.cut_right_quality >= 1 && 33 + p.cut_right_quality <= 127; \
+    [[maybe_unused]] const uint32_t limr = lowr_ok ? (uint32_t)(0x80 - (33 + p.cut_right_quality)) * 0x01010101u : 0u; \
+    /* cut_right as the only window option, window <= 4: cut_right_w4 */ \
+    /* UMI in the reads (src/umiprocessor.cpp:10-89, trimFront before trimAndCut): trimAndCut runs on */ \
+    /* the read from umi_cut(umi_front, len) on (the general path of trim_and_cut_t) */ \
+    [[maybe_unused]] const bool umi = XTRA && (p.umi_front1 > 0 || p.umi_front2 > 0); \
+    [[maybe_unused]] const bool cut_w4 = FQ_CUT_W4 && lowr_ok && !umi && !p.cut_front && !p.cut_tail && p.cut_right_window >= 1 && \
+                        p.cut_right_window <= 4; \
+    /* Without front trimming every kept window starts at 0, so each base lands in exactly one of */ \
+    /* two disjoint blocks: "kept" (inside a passing read's window; the post block) or "removed" */ \
+    /* (trimmed tails, failed pairs; the pre block), one LDS atomic per base.  At the flush */ \
+    /* pre = kept + removed and post = kept. */ \
+    [[maybe_unused]] const bool removed_mode = LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front && !umi); \
+    [[maybe_unused]] const int g_per = max(p.polyg_one_mismatch_per, 1); \
+    /* (i+1)/per as ((i+1)*inv) >> 16, exact while per * (kMaxLen + 1) < 65536; else inv = 0: division */ \
+    [[maybe_unused]] const int g_inv = g_per * (kMaxLen + 1) < 65536 ? (65536 + g_per - 1) / g_per : 0;
+
 // XTRA: the -c / UMI / -e instantiation of the full variants (kept apart so the other variants'
 // register allocation does not carry that code)
 // FIX: rows of exactly kChunks chunks (the batch stride is the column length: 160, or 320 in the long
@@ -933,34 +963,12 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
     }
     __syncthreads();
 
+    const int ntiles = PAIRED ? (b.n + 31) >> 5 : (b.n + 63) >> 6;
     // Profiling-only ablation bits (fq_params.reserved[0]; results are wrong when set):
     // 1 skip overlap, 2 skip passFilter scan, 4 skip stats pass, 8 skip polyG, 16 skip LDS atomics,
     // 32 skip the polyG counters, 64 accept the first scan candidate unchecked, 128 skip the scan,
     // 1024 skip trimAndCut (FULL), 2048 skip polyX
-    const int abl = p.reserved[0];
-    const int ntiles = PAIRED ? (b.n + 31) >> 5 : (b.n + 63) >> 6;
-    const int nchunks = FIX ? kChunks : min(kChunks, b.stride >> 4);
-    const int limit = p.overlap_diff_limit;
-    const int K = max(limit, 1);
-    const int req = p.overlap_require;
-    const uint32_t limq = (uint32_t)(0x80 - p.low_qual_limit) * 0x01010101u;
-    // cut_right threshold 33 + q, in 0..93 (CLI range): the same SWAR below-threshold test
-    const bool lowr_ok = p.cut_right && 33 + p.cut_right_quality >= 1 && 33 + p.cut_right_quality <= 127;
-    const uint32_t limr = lowr_ok ? (uint32_t)(0x80 - (33 + p.cut_right_quality)) * 0x01010101u : 0u;
-    // cut_right as the only window option, window <= 4: cut_right_w4
-    // UMI in the reads (src/umiprocessor.cpp:10-89, trimFront before trimAndCut): trimAndCut runs on
-    // the read from umi_cut(umi_front, len) on (the general path of trim_and_cut_t)
-    const bool umi = XTRA && (p.umi_front1 > 0 || p.umi_front2 > 0);
-    const bool cut_w4 = FQ_CUT_W4 && lowr_ok && !umi && !p.cut_front && !p.cut_tail && p.cut_right_window >= 1 &&
-                        p.cut_right_window <= 4;
-    // Without front trimming every kept window starts at 0, so each base lands in exactly one of
-    // two disjoint blocks: "kept" (inside a passing read's window; the post block) or "removed"
-    // (trimmed tails, failed pairs; the pre block), one LDS atomic per base.  At the flush
-    // pre = kept + removed and post = kept.
-    const bool removed_mode = LEAN || (p.trim_front1 == 0 && p.trim_front2 == 0 && !p.cut_front && !umi);
-    const int g_per = max(p.polyg_one_mismatch_per, 1);
-    // (i+1)/per as ((i+1)*inv) >> 16, exact while per * (kMaxLen + 1) < 65536; else inv = 0: division
-    const int g_inv = g_per * (kMaxLen + 1) < 65536 ? (65536 + g_per - 1) / g_per : 0;
+    FQ_DERIVE_PARAMS()
 #ifdef FQ_PHASE_STAMPS
     const bool stamps = p.reserved[1] != 0;
     unsigned long long ph[kPhases] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -986,6 +994,23 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
     constexpr int kItems = PAIRED ? 32 : 64;
     constexpr int kHole = 0x7FFFFFFF;
     for (int t = blockIdx.x * kWaves + wave; t < ntiles; t += gridDim.x * kWaves) {
+#if FQ_PLAUNDER
+        // The parameters and the batch descriptor are re-read from the kernarg segment every tile
+        // (scalar loads, cached): kept live across the tile loop they overflow the SGPR file, and the
+        // spills cost VALU (v_writelane / v_readlane) and scratch traffic inside the loop.
+        typedef const __attribute__((address_space(4))) fq_params KParams;
+        typedef const __attribute__((address_space(4))) fq_batch KBatch;
+        // (the kernel's first two arguments, at their ABI offsets in the kernarg segment: p at 0, b at
+        // the next multiple of its alignment; taking &p instead would copy p to scratch)
+        const __attribute__((address_space(4))) char* ka_ =
+            (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+        KParams* kp_ = (KParams*)ka_;
+        KBatch* kb_ = (KBatch*)(ka_ + ((sizeof(fq_params) + alignof(fq_batch) - 1) & ~(alignof(fq_batch) - 1)));
+        asm volatile("" : "+s"(kp_), "+s"(kb_));
+        const fq_params& p = *(const fq_params*)kp_;
+        const fq_batch& b = *(const fq_batch*)kb_;
+        FQ_DERIVE_PARAMS()
+#endif
         // Per-lane values are derived from an opaque copy of the lane id inside the loop: left to
         // itself the compiler hoists dozens of them out of the tile loop and spills them.
         int lane_x = lane;

@@ -260,13 +260,18 @@ class BgzfSource {
         madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
         return b;
     }
-    // up to `want` more bytes of the decompressed stream into dst; false on corrupt data
+    // up to `want` more bytes of the decompressed stream into dst; false on corrupt data, after the
+    // bytes of every member before the first bad one (in stream order) have been handed out
     bool read(char* dst, size_t want, size_t& got) {
         got = 0;
         while (got < want) {
             if (pos_ == buf_.size()) {
-                if (!next_batch()) return false;
-                if (buf_.empty()) break;  // end of the stream
+                if (bad_) return false;
+                if (!next_batch()) bad_ = true;  // buf_ holds the good members' prefix of the batch
+                if (buf_.empty()) {
+                    if (bad_) return false;
+                    break;  // end of the stream
+                }
                 continue;
             }
             const size_t n = std::min(want - got, buf_.size() - pos_);
@@ -327,12 +332,14 @@ class BgzfSource {
         } else {
             ok = inflate_batch(buf_, next_);
         }
+        if (!ok) next_ = members_.size();  // nothing after a bad member
         if (ok && next_ < members_.size())
             ahead_ = std::async(std::launch::async, [this] { return inflate_batch(ahead_buf_, next_); });
         return ok;
     }
     // the members from `first` (~64 MB of output) inflated into `out` on up to kThreads threads;
-    // advances `first` past them
+    // advances `first` past them.  A member that fails its inflate, CRC32 or ISIZE check ends the
+    // stream: `out` keeps the members before the first such one and the call returns false.
     bool inflate_batch(std::string& out, size_t& first_io) {
         static const int kThreads = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2));
         const size_t first = first_io;
@@ -346,16 +353,24 @@ class BgzfSource {
         out.resize(total);
         const size_t cnt = end - first;
         first_io = end;
-        std::atomic<bool> ok{true};
+        // bad: the lowest index (within the batch) of a member that failed; each thread stops at its
+        // own first failure, which is enough, since its later members could only raise it
+        std::atomic<size_t> bad{cnt};
         const int nt = (int)std::min<size_t>((size_t)kThreads, cnt);
+        auto fail = [&](size_t i) {
+            size_t cur = bad.load();
+            while (i < cur && !bad.compare_exchange_weak(cur, i)) {
+            }
+        };
         auto work = [&](int t) {
+            const size_t i0 = cnt * (size_t)t / nt, i1 = cnt * (size_t)(t + 1) / nt;
             z_stream z;
             std::memset(&z, 0, sizeof z);
             if (inflateInit2(&z, -15) != Z_OK) {
-                ok = false;
+                fail(i0);
                 return;
             }
-            for (size_t i = cnt * (size_t)t / nt; i < cnt * (size_t)(t + 1) / nt && ok; ++i) {
+            for (size_t i = i0; i < i1 && i < bad.load(); ++i) {
                 const Member& mb = members_[first + i];
                 inflateReset(&z);
                 z.next_in = const_cast<Bytef*>(map_ + mb.data);
@@ -365,8 +380,10 @@ class BgzfSource {
                 z.next_out = mb.isize ? o : &dummy;
                 z.avail_out = mb.isize ? (uInt)mb.isize : 1u;
                 if (inflate(&z, Z_FINISH) != Z_STREAM_END || z.total_out != mb.isize ||
-                    (uint32_t)crc32(crc32(0, nullptr, 0), o, mb.isize) != mb.crc)
-                    ok = false;
+                    (uint32_t)crc32(crc32(0, nullptr, 0), o, mb.isize) != mb.crc) {
+                    fail(i);
+                    break;
+                }
             }
             inflateEnd(&z);
         };
@@ -374,7 +391,10 @@ class BgzfSource {
         for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
         if (nt > 0) work(0);
         for (auto& x : th) x.join();
-        return ok;
+        const size_t b = bad.load();
+        if (b == cnt) return true;
+        out.resize(at[b]);  // the members before the first bad one
+        return false;
     }
     const unsigned char* map_;
     size_t size_;
@@ -382,6 +402,7 @@ class BgzfSource {
     size_t next_ = 0;          // first member not yet inflated (or being inflated ahead)
     std::string buf_, ahead_buf_;
     size_t pos_ = 0;
+    bool bad_ = false;  // a member failed: buf_ holds the last good bytes
     std::future<bool> ahead_;  // the next batch, inflating while buf_ is read
 };
 
@@ -462,7 +483,9 @@ void FqBulkReader::read_more() {
         if (!bgzf_->read(dst, want, got)) reader_stderr("Error to read gzip file\n");
     } else if (gz_) {
         while (got < want) {
-            const unsigned ask = (unsigned)std::min<size_t>(want - got, 1u << 30);
+            // calls of the reference's buffer size (src/fqreader.cpp:28-35): a corrupt member costs
+            // only the call in which gzread fails, as in the reference
+            const unsigned ask = (unsigned)std::min<size_t>(want - got, (size_t)bsize_);
             const int r = gzread(gz_, dst + got, ask);
             if (r < 0) {
                 reader_stderr("Error to read gzip file\n");

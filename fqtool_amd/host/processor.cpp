@@ -1173,14 +1173,18 @@ struct Lane {
                 rr.done = false;  // (nothing to read: the host reader reports the empty input)
             }
             while (!inflight.empty()) complete_oldest();
-            // windows enqueued after the stop are dropped once their copies are done
+            // windows enqueued after the stop are dropped once their copies are done, and the engine
+            // leaves raw mode (the host reader's packs go to it next)
             (void)fq_engine_sync(e);
+            if (fq_engine_raw_end(e) != FQ_OK)
+                throw std::runtime_error(std::string("fq_engine_raw_end: ") + fq_engine_last_error(e));
             for (const Win& w : wins) free_stages.push(w.stage);
             wins.clear();
             finish();
             if (rd_err) std::rethrow_exception(rd_err);
         } catch (...) {
             (void)fq_engine_sync(e);
+            (void)fq_engine_raw_end(e);
             inflight.clear();
             finish();
             close_all();

@@ -429,6 +429,10 @@ typedef struct fq_raw_out {
 int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap);
 int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w);
 int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64_t seq_no);
+/* Leaves raw mode: waits for the copies and indexing of windows enqueued and never launched (their
+ * host bytes may then be reused) and drops them; launched packs are polled as usual.  The engine
+ * takes other packs, or a new fq_engine_raw_begin once nothing is in flight. */
+int fq_engine_raw_end(fq_engine* e);
 
 /* Page-locked host memory for packs and records (portable across devices; transparent huge
  * pages registered with the runtime, hipHostMalloc as fallback).  FQ_E_NO_DEVICE without a HIP

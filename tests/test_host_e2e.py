@@ -198,3 +198,57 @@ def test_fqtool_raw_stream_small_windows_matches_reference(case, tmp_path):
                 "edge_pe_dup", "td_se_q"):
         assert "raw stream" in p.stderr.decode(), p.stderr.decode()[-1000:]
     E.check_outputs(case, str(outd))
+
+
+@pytest.mark.parametrize("kind", ["bgzf", "multi"])
+def test_corrupt_member_keeps_the_good_prefix(kind, host, oracle, tmp_path):
+    """A CRC32 flipped in a middle member of read 1's .gz: the tool processes exactly the bytes the
+    stream delivered before the failure and reports the error.  BGZF (members inflated in parallel):
+    every member before the bad one, in order.  Any other gzip (zlib's stream reader, read in the
+    reference's 1 MiB gzread calls, src/fqreader.cpp:28-35): every call before the one that fails.
+    Expected: the outputs of the same command on plain files holding that prefix (read 2 whole)."""
+    member, bad = 0xFF00, 40
+    raw = {}
+    for name in ("r1.fq.gz", "r2.fq.gz"):
+        with open(os.path.join(E.INPUTS, name), "rb") as f:
+            raw[name] = gzip.decompress(f.read())
+    gz, plain, out_gz, out_plain = (tmp_path / d for d in ("gz", "plain", "out_gz", "out_plain"))
+    for d in (gz, plain, out_gz, out_plain):
+        d.mkdir()
+    for name, data in raw.items():
+        if kind == "bgzf":
+            comp = bytearray(bgzf(data, member=member))
+        else:
+            comp = bytearray(b"".join(gzip.compress(data[o:o + member], 6) for o in range(0, len(data), member)))
+        keep = len(data)
+        if name == "r1.fq.gz":
+            # walk to member `bad`: BGZF headers carry BSIZE; plain members are re-compressed to find their sizes
+            off = 0
+            for k in range(bad):
+                if kind == "bgzf":
+                    off += struct.unpack("<H", bytes(comp[off + 16:off + 18]))[0] + 1
+                else:
+                    off += len(gzip.compress(data[k * member:(k + 1) * member], 6))
+            if kind == "bgzf":
+                end = off + struct.unpack("<H", bytes(comp[off + 16:off + 18]))[0] + 1
+            else:
+                end = off + len(gzip.compress(data[bad * member:(bad + 1) * member], 6))
+            comp[end - 8] ^= 0x5A  # the member's CRC32
+            stop = (bad + 1) * member  # decompressed end of the bad member
+            keep = bad * member if kind == "bgzf" else (stop - 1) // (1 << 20) * (1 << 20)
+        (gz / name).write_bytes(bytes(comp))
+        (plain / name[:-3]).write_bytes(data[:keep])
+    argv = E.argv_for("fqtool", "td_pe_qag", str(out_gz))
+    argv_gz = [a.replace(E.INPUTS, str(gz)) for a in argv]
+    argv_plain = [a.replace(E.INPUTS, str(plain)).replace(".fq.gz", ".fq") if a.startswith(E.INPUTS) else a
+                  for a in E.argv_for("fqtool", "td_pe_qag", str(out_plain))]
+    rep_gz = E.run_session_with_oracle(host, oracle, argv_gz)
+    rep_plain = E.run_session_with_oracle(host, oracle, argv_plain)
+    outs = sorted(n for n in os.listdir(out_gz) if not n.startswith("report."))
+    assert outs == sorted(n for n in os.listdir(out_plain) if not n.startswith("report."))
+    for n in outs:
+        assert E.digest(str(out_gz / n)) == E.digest(str(out_plain / n)), n
+    import json
+    a, b = json.loads(rep_gz), json.loads(rep_plain)
+    for k in ("summary", "filtering_result", "adapter_cutting", "read1_before_filtering", "read2_after_filtering"):
+        assert a.get(k) == b.get(k), k

@@ -11,6 +11,6 @@ HIPFLAGS="-std=c++17 -O3 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result"
 /opt/rocm/bin/hipcc $HIPFLAGS "$@" -c fqtool_amd/csrc/pe_fast_long.hip -o $out/pe_fast_long.o &
 wait
 objs=""
-for o in engine pe_kernel synth dup kmer text; do objs="$objs build/obj/$o.o"; done
+for o in engine pe_kernel synth dup kmer text raw; do objs="$objs build/obj/$o.o"; done
 /opt/rocm/bin/hipcc $HIPFLAGS -shared -o build/alt/lib_$name.so $objs $out/pe_fast.o $out/pe_fast_long.o
 echo built build/alt/lib_$name.so

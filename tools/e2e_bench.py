@@ -98,7 +98,7 @@ def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
         raise SystemExit(f"{tag} failed rc={p.returncode}: {p.stderr[-2000:]}")
     m = re.search(r"fqtool-amd: (.*)", p.stderr)
     t = re.search(r"fqtool-amd timing: (.*)", p.stderr)
-    return wall, (m.group(1) if m else None) + ((" | " + t.group(1)) if t else ""), o
+    return wall, (m.group(1) if m else "(no fqtool-amd summary line)") + ((" | " + t.group(1)) if t else ""), o
 
 
 def _bgzf_chunk(arg):
