@@ -76,3 +76,25 @@ clean:
 	rm -rf build $(LIBDIR) fqtool_amd/bin oracle/build
 
 .PHONY: all engine host oracle clean
+
+# ThreadSanitizer build of the host pipeline (test infrastructure, CPU only): the tool's host sources
+# instrumented, linked against oracle/cpu_engine.cpp (the oracle standing in for the engine's
+# host-pack subset) instead of the GPU engine.  tests/test_tsan_cpu.py runs it (FQ_TEXT_MODE=0).
+TSANDIR    := build/tsan
+TSANFLAGS  := -std=c++17 -O1 -g -fPIC -pthread -fsanitize=thread
+tsan: $(TSANDIR)/fqtool
+
+$(TSANDIR)/host_%.o: $(HOSTDIR)/%.cpp $(HOST_HDRS)
+	@mkdir -p $(TSANDIR)
+	$(CXX) $(TSANFLAGS) -c $< -o $@
+
+$(TSANDIR)/libfqengine.so: oracle/cpu_engine.cpp oracle/fq_oracle.c oracle/fq_oracle.h include/fqengine.h
+	@mkdir -p $(TSANDIR)
+	gcc -std=c11 -O1 -g -fPIC -fsanitize=thread -c oracle/fq_oracle.c -o $(TSANDIR)/fq_oracle.o
+	$(CXX) $(TSANFLAGS) -Iinclude -Ioracle -shared -o $@ oracle/cpu_engine.cpp $(TSANDIR)/fq_oracle.o -lm
+
+$(TSANDIR)/fqtool: $(patsubst $(HOSTDIR)/%.cpp,$(TSANDIR)/host_%.o,$(HOST_SRCS)) $(HOSTDIR)/main.cpp $(TSANDIR)/libfqengine.so
+	$(CXX) $(TSANFLAGS) -o $@ $(HOSTDIR)/main.cpp $(patsubst $(HOSTDIR)/%.cpp,$(TSANDIR)/host_%.o,$(HOST_SRCS)) \
+	    -L$(TSANDIR) -lfqengine -Wl,-rpath,'$$ORIGIN' -lz
+
+.PHONY: tsan

@@ -1,0 +1,41 @@
+"""The host pipeline under ThreadSanitizer (the reader, one dispatcher per engine, the
+formatter, the writers, the pool and the detection thread run instrumented, with the oracle standing
+in for the engine): byte-identical outputs and no TSan report.  A representative subset here; the
+full sweep over every golden case at -w 4 and -w 16 is tools/tsan_sweep.py (log under profiles/)."""
+import pytest
+
+import tsan_util as T
+
+pytestmark = pytest.mark.skipif(not T.tsan_available(), reason="libtsan not installed")
+
+
+@pytest.fixture(scope="module")
+def tsan_build():
+    T.build()
+
+
+@pytest.mark.parametrize("case,workers", [("td_pe_qag", 4), ("td_pe_gz", 16), ("td_se_split_num_many", 3),
+                                          ("td_pe_merge", 4), ("td_pe_correct", 4), ("td_pe_dup", 4),
+                                          ("td_pe_umi_perread", 16), ("synth_pe_c5", 16)])
+def test_host_pipeline_under_tsan(case, workers, tsan_build, tmp_path):
+    err, reports = T.run_case(case, str(tmp_path), workers, devices=2)
+    assert reports == 0, err[-6000:]
+
+
+@pytest.mark.parametrize("workers", [4, 16])
+def test_bgzf_inputs_under_tsan(workers, tsan_build, tmp_path):
+    """BGZF inputs: members inflated on up to 8 threads per mate, one batch ahead of the parser."""
+    import gzip
+    import os
+
+    import e2e_util as E
+    from test_host_e2e import bgzf
+
+    inp, out = tmp_path / "in", tmp_path / "out"
+    inp.mkdir()
+    out.mkdir()
+    for name in ("r1.fq.gz", "r2.fq.gz"):
+        with open(os.path.join(E.INPUTS, name), "rb") as f:
+            (inp / name).write_bytes(bgzf(gzip.decompress(f.read()), member=30_000))
+    err, reports = T.run_case("td_pe_qag", str(out), workers, devices=2, inputs=str(inp))
+    assert reports == 0, err[-6000:]

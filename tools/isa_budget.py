@@ -19,18 +19,41 @@ import sys
 from collections import defaultdict
 
 SRC = "pe_fast.hip"
-# kernel-body sections of pe_fast.hip (first line of each section; the kernel spans 894-2029)
-SECTIONS = [
-    (894, "setup"), (988, "staging"), (1251, "trim"), (1288, "polyG"), (1297, "overlap"),
-    (1427, "polyx_maxlen_merge"), (1478, "filter"), (1654, "stats"), (1776, "stats_merge"),
-    (1854, "stats_prepost"), (1907, "stats_scalars"), (1919, "store"), (1940, "flush"), (2030, None),
-]
-# phase-specific helpers of pe_fast.hip (line ranges)
-HELPERS = [
-    (276, 313, "overlap"), (315, 365, "overlap"), (376, 482, "overlap"), (484, 554, "adseq"),
-    (557, 613, "polyG"), (615, 649, "polyx_maxlen_merge"), (651, 712, "trim"), (714, 746, "staging"),
-    (786, 887, "correct"),
-]
+SRC_PATH = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "..",
+                                        "fqtool_amd", "csrc", SRC)
+# kernel-body sections: the "// ---------------- <name>" marker comments of pe_fast.hip
+MARKERS = [("staging", "staging"), ("trimAndCut", "trim"), ("polyG", "polyG"), ("overlap", "overlap"),
+           ("polyX", "polyx_maxlen"), ("merge", "merge"), ("passFilter", "filter"), ("Stats::statRead", "stats"),
+           ("flush", "flush")]
+# phase-specific helpers of pe_fast.hip (function name -> phase)
+HELPER_FUNCS = {"ov_exact": "overlap", "ov_scan": "overlap", "unzip2": "overlap", "csa": "overlap",
+                "ov_candidates": "overlap", "adseq_search": "adseq", "polyg_bits": "polyG",
+                "polyx_no_trim": "polyx_maxlen", "cut_right_w4": "trim", "lower_flags": "staging",
+                "correct_pair_fast": "correct", "count_by_value": "filter"}
+
+
+def _scan_source():
+    import re as _re
+    lines = open(SRC_PATH).read().split("\n")
+    secs, helpers = [], []
+    kstart = next(i for i, l in enumerate(lines) if "pe_fast_kernel(fq_params p" in l) + 1
+    secs.append((kstart, "setup"))
+    for i, l in enumerate(lines, 1):
+        m = _re.match(r"\s*// ---------------- (\S+)", l)
+        if m and i > kstart:
+            for key, nm in MARKERS:
+                if m.group(1).startswith(key):
+                    secs.append((i, nm))
+        m = _re.match(r"__device__.*?\b(\w+)\(", l)
+        if m and m.group(1) in HELPER_FUNCS:
+            end = next(j for j in range(i, len(lines)) if lines[j].startswith("}"))
+            helpers.append((i, end + 1, HELPER_FUNCS[m.group(1)]))
+    kend = next(j for j in range(kstart, len(lines)) if lines[j].startswith("}")) + 1
+    secs.append((kend + 1, None))
+    return secs, helpers, kstart, kend
+
+
+SECTIONS, HELPERS, KSTART, KEND = _scan_source()
 
 
 def section_of(line):
@@ -147,7 +170,7 @@ def main():
             ph = helper_of(line)
             if ph is None:
                 sec = section_of(line)
-                if sec is not None and 894 <= line < 2030:
+                if sec is not None and KSTART <= line <= KEND:
                     ph = sec
                     last_phase = sec
         if ph is None:
