@@ -100,6 +100,9 @@ namespace {
 #ifndef FQ_STATS_AHEAD
 #define FQ_STATS_AHEAD 2  // removed-mode Stats: quality chunks requested this many chunks ahead
 #endif
+#ifndef FQ_PREFIX
+#define FQ_PREFIX 1  // LEAN: per-chunk prefix counts staged in LDS, passFilter reads them (0: the trimmed-tail loop)
+#endif
 #ifndef FQ_PLAUNDER
 #define FQ_PLAUNDER 1  // re-read fq_params / fq_batch from the kernarg segment every tile (SGPR pressure)
 #endif
@@ -148,17 +151,23 @@ constexpr int kPfW = FQ_PREFETCH ? 64 : 0;             // LDS-DMA prefetch sink 
 // per CU: LEAN and FULL as 2 workgroups of 8 waves (128 VGPRs), the merge variant, whose Stats
 // blocks are larger (read 2's merged parts land at read 1's post cycles up to 319), as one
 // workgroup of 16 waves.  The long-read build (320-position columns) fits one 8-wave workgroup.
-template <bool LEAN, bool MERGE = false>
+template <bool LEAN, bool MERGE = false, bool PAIRED = true>
 struct Layout {
     // quality rows staged in LDS (off: rows are re-read from L2); profiling switch for the merge variant
     static constexpr bool kQLds = MERGE && FQ_MERGE_QLDS;
-    static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160) ? 1 : MERGE ? FQ_MERGE_BLOCKS : LEAN ? FQ_LEAN_BLOCKS : 2;
+    // LEAN: each lane's running quality / N counts at the end of every row chunk, staged in LDS (word
+    // kCodeW + chunk * 64 + lane of the wave's block), so passFilter gets a window's counts from one
+    // prefix word and one partial chunk; the LDS they take is one Stats histogram's, so the variant
+    // runs as one workgroup of 16 waves (whose waves share one histogram) instead of two of 8
+    static constexpr bool kPfx = LEAN && PAIRED && !MERGE && FQ_PREFIX && kMaxLen <= 160;  // (SE: C2 trims nothing)
+    static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160 || kPfx) ? 1 : MERGE ? FQ_MERGE_BLOCKS : LEAN ? FQ_LEAN_BLOCKS : 2;
     // (the long build's merge variant: its 320-position columns and 640-cycle merged Stats fit 4 waves)
     static constexpr int kWaves = MERGE ? (kQLds ? 7 : kMaxLen > 160 ? 4 : FQ_MERGE_WAVES)
-                                        : (LEAN && kMaxLen <= 160) ? FQ_LEAN_WAVES : 8;
+                                        : kPfx ? 16 : (LEAN && kMaxLen <= 160) ? FQ_LEAN_WAVES : 8;
     static constexpr int kWavesPerEU = (kWaves * kBlocksPerCU + 3) / 4;
     static constexpr int kThreads = 64 * kWaves;
-    static constexpr int kWaveW = kCodeW + (kQLds ? 64 * kQS : 0);
+    static constexpr int kPfxW = kPfx ? kChunks * 64 : 0;
+    static constexpr int kWaveW = kCodeW + kPfxW + (kQLds ? 64 * kQS : 0);
     // [pre1, pre2, post1 (x2 with MERGE), post2] (+ MERGE: read 2's merged parts, cycles 0..319,
     // in removed mode, which uses blocks 0-3 as the kept/removed rows of the two mates)
     static constexpr int kHists = MERGE ? 6 : 4;
@@ -921,12 +930,12 @@ __device__ inline bool correct_pair_fast(const fq_params& p, uint32_t* col, uint
 // FIX: rows of exactly kChunks chunks (the batch stride is the column length: 160, or 320 in the long
 // build), so every per-chunk offset and bound is a compile-time constant
 template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA = false, bool FIX = false>
-__global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
+__global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE, PAIRED>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    using LY = Layout<LEAN, MERGE>;
+    using LY = Layout<LEAN, MERGE, PAIRED>;
     constexpr int kWaves = LY::kWaves, kThreads = LY::kThreads;
     uint32_t* col = lds + wave * LY::kWaveW;  // code / N columns: word field*64 + lane
     uint32_t* qrows = col + kCodeW;           // full variant: quality rows, row = lane
@@ -1167,6 +1176,10 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
                 wp[kFN * 64] = fwk;
 #endif
                 wp += wstep;
+                if constexpr (LY::kPfx)  // counts through chunk k (each <= 160): q20 | q30 << 8 | low << 16 | N << 24
+                    col[kCodeW + k * 64 + lane_x] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(nbf, lowf, 0x0c0c0400u),
+                                                                          __builtin_amdgcn_perm(q30, q20, 0x0c0c0400u),
+                                                                          0x05040100u);
             }
         }
         // Lowercase a c g t (the uppercase letter | 0x20: the same 3-bit key, so the same code) stay
@@ -1504,7 +1517,38 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE>::kThreads)) __attribute__
         int code = FQ_FAIL_LENGTH;
         uint32_t w20 = 0, w30 = 0;  // Q20/Q30 of the window, for the post stats
         int low = 0, tq = 0, nb = 0;
-        if (nn && wn > 0) {
+        if (LY::kPfx && nn && wn > 0) {
+            // LEAN: the window is [0, wn) (no front trimming, no merge): the counts staged at the end
+            // of chunk c - 1 (c = wn >> 4) plus those of chunk c's bytes below wn
+            if (!(abl & 2)) {
+                const int c = wn >> 4, rb = wn & 15;
+                const uint32_t pv = col[kCodeW + max(c - 1, 0) * 64 + lane_x] & (c > 0 ? ~0u : 0u);
+                w20 = pv & 0xFFu;
+                w30 = (pv >> 8) & 0xFFu;
+                low = (int)((pv >> 16) & 0xFFu);
+                nb = (int)(pv >> 24);
+                if (__any(rb != 0) && rb != 0) {
+                    const uint4 q4 = qchunk(c);
+                    const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t bm = bytemask(rb - 4 * j), qm = qw[j] & bm;
+                        w20 += __popc((qm + 0x4A4A4A4Au) & (0x80808080u & bm));
+                        w30 += __popc(qm & 0x40404040u);
+                        low += __popc(~(qm + limq) & (0x80808080u & bm));
+                    }
+                    // N bits of the chunk's first rb positions (read 2's column is reversed)
+                    const uint32_t nw = col[(kFN + (rc ? kChunks - 1 - c : c)) * 64 + lane_x];
+                    nb += __popc(nw & (rc ? 0x55555555u & ~posmask(16 - rb) : posmask(rb)));
+                }
+            } else {
+                low = (int)lowf;
+                nb = (int)nbf;
+                w20 = q20;
+                w30 = q30;
+            }
+            code = filter_verdict(p, n, low, nb, tq - 33 * n, [&]() { return 0; });
+        } else if (nn && wn > 0) {
             // window sums = whole-read sums (from staging) minus the trimmed head [0, ws) and
             // tail [ws+wn, L): the trimmed parts are usually a few bases.  (FULL: a window
             // shorter than half the read, e.g. read 2's part of a merged read, is summed directly:
@@ -2087,7 +2131,7 @@ extern "C" __attribute__((visibility("default"))) int fq_debug_phase_cycles(unsi
 // every instantiation (and its FIX twin) may use the LDS its layout declares
 template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA>
 static hipError_t set_lds() {
-    const int bytes = Layout<LEAN, MERGE>::kLdsW * 4 + (LEAN ? 4096 : 0);  // (LEAN: + profiling pad, reserved[2])
+    const int bytes = Layout<LEAN, MERGE, PAIRED>::kLdsW * 4 + (LEAN ? 4096 : 0);  // (LEAN: + profiling pad, reserved[2])
     hipError_t e = hipFuncSetAttribute((const void*)pe_fast_kernel<LEAN, PAIRED, MERGE, XTRA, false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, bytes > 160 * 1024 ? 160 * 1024 : bytes);
     if (e != hipSuccess) return e;
@@ -2117,7 +2161,7 @@ hipError_t FQ_PREPARE() {
 template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA>
 static void launch_variant(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
                            int* slow_tiles, int* slow_count, int grid, int extra_lds, hipStream_t stream) {
-    using LY = Layout<LEAN, MERGE>;
+    using LY = Layout<LEAN, MERGE, PAIRED>;
     const dim3 g(grid * LY::kBlocksPerCU), t(LY::kThreads);
     const size_t lds = LY::kLdsW * 4 + extra_lds;
     if (b.stride == 16 * kChunks)
