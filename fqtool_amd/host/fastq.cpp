@@ -406,6 +406,89 @@ class BgzfSource {
     std::future<bool> ahead_;  // the next batch, inflating while buf_ is read
 };
 
+// ---- single-stream gzip input ----
+// zlib's stream reader (the reference's gzread, src/fqreader.cpp:28-35) on a thread of its own per
+// input, running ahead of the parser: blocks of the inflated stream queue up (at most kAhead), so
+// inflating overlaps parsing.  gzread is called with the reference's buffer size, so a corrupt
+// member costs the same bytes as in the reference: those of the call that fails.
+class GzAhead {
+   public:
+    GzAhead(gzFile gz, size_t call) : gz_(gz), call_(call), th_([this] { run(); }) {}
+    ~GzAhead() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    // up to want bytes of the stream into dst; false once the stream failed (after the bytes
+    // before the failure were handed out)
+    bool read(char* dst, size_t want, size_t& got) {
+        got = 0;
+        std::unique_lock<std::mutex> lk(m_);
+        while (got < want) {
+            cv_.wait(lk, [this] { return !q_.empty() || done_; });
+            if (q_.empty()) return !bad_;
+            std::string& b = q_.front();
+            const size_t n = std::min(want - got, b.size() - off_);
+            std::memcpy(dst + got, b.data() + off_, n);
+            got += n;
+            off_ += n;
+            if (off_ == b.size()) {
+                q_.pop_front();
+                off_ = 0;
+                cv_.notify_all();
+            }
+        }
+        return true;
+    }
+
+   private:
+    static constexpr size_t kBlock = 8u << 20;
+    static constexpr size_t kAhead = 8;
+    void run() {
+        for (;;) {
+            std::string b;
+            const size_t cap = std::max(kBlock, call_);
+            b.resize(cap);
+            size_t n = 0;
+            bool end = false, bad = false;
+            while (n + call_ <= cap) {
+                const int r = gzread(gz_, &b[n], (unsigned)call_);
+                if (r < 0) {
+                    bad = end = true;
+                    break;
+                }
+                n += (size_t)r;
+                if ((size_t)r < call_) {
+                    end = true;
+                    break;
+                }
+            }
+            b.resize(n);
+            std::unique_lock<std::mutex> lk(m_);
+            cv_.wait(lk, [this] { return stop_ || q_.size() < kAhead; });
+            if (stop_) return;
+            if (n) q_.push_back(std::move(b));
+            if (end) {
+                done_ = true;
+                bad_ = bad;
+            }
+            cv_.notify_all();
+            if (end) return;
+        }
+    }
+    gzFile gz_;
+    size_t call_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::string> q_;
+    size_t off_ = 0;
+    bool stop_ = false, done_ = false, bad_ = false;
+    std::thread th_;
+};
+
 // ---- FqBulkReader ----
 FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     : phred64_(phred64), bsize_((uint64_t)buf_size) {
@@ -415,6 +498,7 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
         if (!gz_) throw std::runtime_error("Failed to open file: " + path);
         gzbuffer(gz_, 1 << 20);
         gzrewind(gz_);
+        gz_ahead_.reset(new GzAhead(gz_, (size_t)bsize_));
         return;
     }
     fp_ = path == "/dev/stdin" ? stdin : std::fopen(path.c_str(), "rb");
@@ -437,6 +521,7 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
 
 FqBulkReader::~FqBulkReader() {
     if (map_) munmap(map_, map_size_);
+    gz_ahead_.reset();  // (its thread reads gz_)
     if (gz_) gzclose(gz_);
     if (fp_ && fp_ != stdin) std::fclose(fp_);
 }
@@ -481,19 +566,8 @@ void FqBulkReader::read_more() {
     size_t got = 0;
     if (bgzf_) {
         if (!bgzf_->read(dst, want, got)) reader_stderr("Error to read gzip file\n");
-    } else if (gz_) {
-        while (got < want) {
-            // calls of the reference's buffer size (src/fqreader.cpp:28-35): a corrupt member costs
-            // only the call in which gzread fails, as in the reference
-            const unsigned ask = (unsigned)std::min<size_t>(want - got, (size_t)bsize_);
-            const int r = gzread(gz_, dst + got, ask);
-            if (r < 0) {
-                reader_stderr("Error to read gzip file\n");
-                break;
-            }
-            got += (size_t)r;
-            if ((unsigned)r < ask) break;
-        }
+    } else if (gz_ahead_) {
+        if (!gz_ahead_->read(dst, want, got)) reader_stderr("Error to read gzip file\n");
     } else {
         got = std::fread(dst, 1, want, fp_);
     }

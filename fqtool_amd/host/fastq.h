@@ -148,6 +148,7 @@ class FqReader {
 // rule is evaluated on stream offsets.  Bytes read past the last record of a pack are carried
 // into the next pack's arena.
 class Pool;
+class GzAhead;
 
 class FqBulkReader {
    public:
@@ -183,6 +184,7 @@ class FqBulkReader {
     void read_more();
     gzFile gz_ = nullptr;
     std::unique_ptr<BgzfSource> bgzf_;  // BGZF input: members inflated on several threads
+    std::unique_ptr<GzAhead> gz_ahead_;  // other gzip: inflated on a thread of its own, ahead of the parser
     FILE* fp_ = nullptr;
     bool phred64_;
     uint64_t bsize_;
