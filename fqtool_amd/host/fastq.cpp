@@ -9,6 +9,7 @@
 #include <cstring>
 #include <deque>
 #include <emmintrin.h>
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -406,6 +407,89 @@ class BgzfSource {
     std::future<bool> ahead_;  // the next batch, inflating while buf_ is read
 };
 
+// ---- whole gzip files through libdeflate ----
+// A gzip file (one member or several, not BGZF) inflated at once with the system's libdeflate
+// (loaded at run time; its C API is stable: alloc / gzip_decompress_ex / free) into an anonymous
+// mapping, which the reader then parses like a mapped plain file (parallel parse, zero copy).
+// libdeflate inflates about 2.5x faster than zlib's stream reader on FASTQ; the price is memory for
+// the whole uncompressed text, so only inputs whose reserved output (kRatio x the compressed size)
+// fits the budget take this path.  Any failure (no libdeflate, corrupt data, output larger than the
+// reservation) leaves the file to zlib's stream reader from its start, which reproduces the
+// reference's behaviour on corrupt input.
+namespace {
+struct Libdeflate {
+    void* (*alloc)();
+    int (*gzip_ex)(void*, const void*, size_t, void*, size_t, size_t*, size_t*);
+    void (*free_)(void*);
+    bool ok = false;
+    Libdeflate() {
+        void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc = reinterpret_cast<void* (*)()>(dlsym(h, "libdeflate_alloc_decompressor"));
+        gzip_ex = reinterpret_cast<int (*)(void*, const void*, size_t, void*, size_t, size_t*, size_t*)>(
+            dlsym(h, "libdeflate_gzip_decompress_ex"));
+        free_ = reinterpret_cast<void (*)(void*)>(dlsym(h, "libdeflate_free_decompressor"));
+        ok = alloc && gzip_ex && free_;
+    }
+};
+const Libdeflate& libdeflate() {
+    static const Libdeflate l;
+    return l;
+}
+
+// the inflated text of gzip file `path` in an anonymous mapping (*out, *n bytes; munmap the
+// reserved *cap bytes), or false
+bool inflate_whole(const std::string& path, char** out, size_t* n, size_t* cap) {
+    const char* env = std::getenv("FQ_GZ_WHOLE");  // 0: always zlib's stream reader
+    if (env && std::string(env) == "0") return false;
+    const Libdeflate& ld = libdeflate();
+    if (!ld.ok) return false;
+    const int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < 18) {
+        ::close(fd);
+        return false;
+    }
+    const size_t csize = (size_t)st.st_size;
+    void* cm = mmap(nullptr, csize, PROT_READ, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    if (cm == MAP_FAILED) return false;
+    madvise(cm, csize, MADV_SEQUENTIAL);
+    constexpr size_t kRatio = 12;  // reservation per compressed byte (FASTQ inflates 3-5x)
+    const size_t phys = (size_t)sysconf(_SC_PHYS_PAGES) * (size_t)sysconf(_SC_PAGE_SIZE);
+    const size_t want = std::max<size_t>(csize * kRatio, 1 << 20);
+    bool ok = want <= std::min(phys / 8, (size_t)32 << 30);  // (resident: only the bytes written)
+    void* om = ok ? mmap(nullptr, want, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0)
+                  : MAP_FAILED;
+    ok = om != MAP_FAILED;
+    size_t in = 0, outn = 0;
+    if (ok) {
+        madvise(om, want, MADV_HUGEPAGE);
+        void* d = ld.alloc();
+        ok = d != nullptr;
+        while (ok && in < csize) {  // member by member
+            size_t ain = 0, aout = 0;
+            ok = ld.gzip_ex(d, static_cast<const char*>(cm) + in, csize - in, static_cast<char*>(om) + outn, want - outn,
+                            &ain, &aout) == 0;
+            in += ain;
+            outn += aout;
+            ok = ok && ain > 0;
+        }
+        if (d) ld.free_(d);
+    }
+    munmap(cm, csize);
+    if (!ok) {
+        if (om != MAP_FAILED) munmap(om, want);
+        return false;
+    }
+    *out = static_cast<char*>(om);
+    *n = outn;
+    *cap = want;
+    return true;
+}
+}  // namespace
+
 // ---- single-stream gzip input ----
 // zlib's stream reader (the reference's gzread, src/fqreader.cpp:28-35) on a thread of its own per
 // input, running ahead of the parser: blocks of the inflated stream queue up (at most kAhead), so
@@ -494,6 +578,11 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     : phred64_(phred64), bsize_((uint64_t)buf_size) {
     if (ends_with(path, ".gz")) {
         if ((bgzf_ = BgzfSource::open(path))) return;
+        if (inflate_whole(path, &map_, &map_size_, &map_cap_)) {  // parsed like a mapped plain file
+            total_ = map_size_;
+            eof_ = true;
+            return;
+        }
         gz_ = gzopen(path.c_str(), "r");
         if (!gz_) throw std::runtime_error("Failed to open file: " + path);
         gzbuffer(gz_, 1 << 20);
@@ -520,7 +609,7 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
 }
 
 FqBulkReader::~FqBulkReader() {
-    if (map_) munmap(map_, map_size_);
+    if (map_) munmap(map_, map_cap_ ? map_cap_ : map_size_);
     gz_ahead_.reset();  // (its thread reads gz_)
     if (gz_) gzclose(gz_);
     if (fp_ && fp_ != stdin) std::fclose(fp_);

@@ -199,6 +199,7 @@ class FqBulkReader {
     size_t tbase_ = 0, indexed_ = 0;
     char* map_ = nullptr;  // a regular file is read through a private mapping (zero copy)
     size_t map_size_ = 0;
+    size_t map_cap_ = 0;   // (an inflated .gz: the anonymous mapping's reserved size)
     size_t avg_rec_ = 0;   // mean record bytes seen by read_fast (sizes its next region)
     std::string err_;
 };
