@@ -17,10 +17,12 @@
 // of its whole 160-position row (the orientation OverlapAnalysis::analyze compares,
 // src/overlapanalysis.cpp:7-72), so rc position j of a read of length L sits at index
 // j + 160 - L.  Whole-read quality sums (Q20/Q30, below-limit count, total) are taken from the
-// quality registers; qualities are not kept: later passes re-read the row (an L2 hit).  A tile
-// with a byte outside {A,C,G,T,N}, a quality >= 128 or a read longer than 160 is handed to the
-// general kernel (pe_kernel.hip) through a device-side tile list, so everything here may assume
-// that alphabet and rebuild bases from codes.
+// quality registers, and their running values at chunk ends are staged in LDS (prefix counts for
+// passFilter's windows); qualities are not kept: later passes re-read the row (an L2 hit).
+// Lowercase a c g t stay here (a flag beside the N mask); a PAIR (single-end: a read) with any other
+// byte outside {A,C,G,T,N}, a quality >= 128, a read longer than the columns or an index-filter flag
+// is handed to the general kernel (pe_kernel.hip) through a device-side item list, its lanes running
+// on as empty lanes, so everything here may assume that alphabet and rebuild bases from codes.
 //
 // Per read, in the reference's order: trimAndCut (integer windows), polyG (bit-parallel: the
 // 3'-end scan only changes state at non-G bases, visited with find-last-set), overlap analysis
@@ -100,6 +102,15 @@ namespace {
 #ifndef FQ_STATS_AHEAD
 #define FQ_STATS_AHEAD 2  // removed-mode Stats: quality chunks requested this many chunks ahead
 #endif
+#ifndef FQ_VK
+#define FQ_VK 1  // staging: the SWAR masks and limits as VGPR values (a VALU op with an SGPR operand issues at half rate)
+#endif
+#ifndef FQ_EXO3
+#define FQ_EXO3 1  // staging: exotic bytes OR-accumulated with one v_bitop3 (full rate) instead of v_sad_u8
+#endif
+#ifndef FQ_PG2
+#define FQ_PG2 1  // polyG: group 0 decided without the loop when the break is the second non-G base
+#endif
 #ifndef FQ_PREFIX
 #define FQ_PREFIX 1  // LEAN: per-chunk prefix counts staged in LDS, passFilter reads them (0: the trimmed-tail loop)
 #endif
@@ -155,18 +166,22 @@ template <bool LEAN, bool MERGE = false, bool PAIRED = true>
 struct Layout {
     // quality rows staged in LDS (off: rows are re-read from L2); profiling switch for the merge variant
     static constexpr bool kQLds = MERGE && FQ_MERGE_QLDS;
-    // LEAN: each lane's running quality / N counts at the end of every row chunk, staged in LDS (word
-    // kCodeW + chunk * 64 + lane of the wave's block), so passFilter gets a window's counts from one
-    // prefix word and one partial chunk; the LDS they take is one Stats histogram's, so the variant
-    // runs as one workgroup of 16 waves (whose waves share one histogram) instead of two of 8
-    static constexpr bool kPfx = LEAN && PAIRED && !MERGE && FQ_PREFIX && kMaxLen <= 160;  // (SE: C2 trims nothing)
+    // Each lane's running quality / N counts (q20 | q30 << 8 | low << 16 | N << 24) at the end of every
+    // kPfxStep-th row chunk, staged in LDS (word kCodeW + (chunk / kPfxStep) * 64 + lane of the wave's
+    // block), so passFilter gets a window's counts from prefix words and at most kPfxStep chunks of
+    // bytes.  One word per chunk takes one Stats histogram's worth of LDS, so those variants run as one
+    // workgroup of 16 waves (whose waves share one histogram) instead of two of 8; the merge variant
+    // (already one workgroup, with larger histograms) has room for one word per two chunks.
+    // (LEAN single-end, C2, trims nothing; the long build has no room.)
+    static constexpr bool kPfx = FQ_PREFIX && kMaxLen <= 160 && !kQLds && (!LEAN || PAIRED);
+    static constexpr int kPfxStep = MERGE ? 2 : 1;
     static constexpr int kBlocksPerCU = (kQLds || kMaxLen > 160 || kPfx) ? 1 : MERGE ? FQ_MERGE_BLOCKS : LEAN ? FQ_LEAN_BLOCKS : 2;
     // (the long build's merge variant: its 320-position columns and 640-cycle merged Stats fit 4 waves)
     static constexpr int kWaves = MERGE ? (kQLds ? 7 : kMaxLen > 160 ? 4 : FQ_MERGE_WAVES)
                                         : kPfx ? 16 : (LEAN && kMaxLen <= 160) ? FQ_LEAN_WAVES : 8;
     static constexpr int kWavesPerEU = (kWaves * kBlocksPerCU + 3) / 4;
     static constexpr int kThreads = 64 * kWaves;
-    static constexpr int kPfxW = kPfx ? kChunks * 64 : 0;
+    static constexpr int kPfxW = kPfx ? kChunks / kPfxStep * 64 : 0;
     static constexpr int kWaveW = kCodeW + kPfxW + (kQLds ? 64 * kQS : 0);
     // [pre1, pre2, post1 (x2 with MERGE), post2] (+ MERGE: read 2's merged parts, cycles 0..319,
     // in removed mode, which uses blocks 0-3 as the kept/removed rows of the two mates)
@@ -197,6 +212,16 @@ __device__ __forceinline__ int xor32(int x) {
     return (threadIdx.x & 32) ? r[0] : r[1];
 }
 __device__ __forceinline__ uint32_t xor32(uint32_t x) { return (uint32_t)xor32((int)x); }
+
+// A uniform value kept in a VGPR (opaque to the compiler, which would otherwise keep it in an SGPR or
+// rematerialise it there): on gfx950 a full-rate VALU op (and, xor, add, bitop3, ...) with an SGPR
+// operand issues at the half rate of the VOP3 ops (profiles/r04_micro_opcost2.txt).
+__device__ __forceinline__ uint32_t vk(uint32_t x) {
+#if FQ_VK
+    asm volatile("" : "+v"(x));
+#endif
+    return x;
+}
 
 // reverse the order of the 16 two-bit fields of a word
 __device__ __forceinline__ uint32_t pairrev(uint32_t x) {
@@ -587,15 +612,34 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, in
         iend = 0;  // mismatch 0 > allowed at the very first base
     } else {
         int cum = 0;  // non-G bases before the current group
-        for (int g = 0; 16 * g < n && iend == n; ++g) {
+        const uint32_t gx = rc ? 0x55555555u : 0xFFFFFFFFu;  // (G is code 3; read 2's column holds C)
+        // spaced non-G mask (N and lowercase included) of scan indices [16g, 16g + 16), in scan order
+        auto nong = [&](int g) -> uint32_t {
             const int pos0 = rc ? kMaxLen - 1 - e + 16 * g : e - 16 * g - 15;
             // (positions outside [st, e] are scan indices >= n, dropped by `valid`)
             const uint32_t cw = field_window_masked(col, kFC, c, pos0), nw = field_window_masked(col, kFN, c, pos0);
-            // non-G (N and lowercase included; odd bits dropped by `valid`), spaced
-            uint32_t x = fold2(cw ^ (rc ? 0x55555555u : 0xFFFFFFFFu)) | nw | (nw >> 1);
-            if (!rc) x = __builtin_bitreverse32(x) >> 1;                        // forward window -> scan order
+            const uint32_t t = (cw ^ gx) | nw;
+            uint32_t x = (t | (t >> 1)) & 0x55555555u;
+            if (!rc) x = __builtin_bitreverse32(x) >> 1;  // forward window -> scan order
+            return x;
+        };
+#if FQ_PG2
+        // Group 0 decides almost every read: while the allowance is 1 (scan indices < 2 per - 1) the
+        // scan breaks at the second non-G base; the loop below runs only for the reads it leaves open
+        // (a polyG tail, or per < 8).
+        if (maxMM >= 1) {
+            const uint32_t valid = posmask(n), x = nong(0) & valid, x2 = x & (x - 1u);
+            const int s2 = (__ffs(x2) - 1) >> 1;
+            if (x2 && (maxMM == 1 || s2 + 1 < 2 * per)) {
+                iend = s2;
+                const uint32_t gm = ~x & valid & posmask(s2);  // G bases before the break
+                if (gm) lastG = (31 - __clz(gm)) >> 1;
+            }
+        }
+#endif
+        for (int g = 0; 16 * g < n && iend == n; ++g) {
             const uint32_t valid = posmask(n - 16 * g);
-            x &= valid;
+            uint32_t x = nong(g) & valid;
             uint32_t gm = ~x & valid;  // G bases of the group
             const int a0 = allowed(16 * g + 1);  // allowance at the group start
             if (cum + __popc(x) > a0) {
@@ -1066,6 +1110,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
         const bool odd = L > kMaxLen || L > p.max_cycles || L > (nchunks << 4) ||
                          (MERGE && L + xor32(L) > p.max_cycles);
         uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0, lowf = 0, tqf = 0, nbf = 0;  // whole-read sums
+        const uint32_t k80 = vk(0x80808080u), limq_v = vk(limq);  // (VGPR operands: full-rate VALU)
         uint32_t lowr = 0;  // FULL with cut_right: bit k = chunk k holds a quality below its threshold
         // column word of chunk k: k for read 1, 9-k for read 2 (stepped, not precomputed, so the
         // ten addresses are not kept live across tiles)
@@ -1137,13 +1182,19 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     const uint32_t canon = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, kk);
                     // sum of |canon - byte| (one v_sad_u8): zero iff every byte is canonical, and
                     // at most 40 dwords x 4 x 255 per tile, so it never wraps
+#if FQ_EXO3
+                    // (or the OR of byte ^ canon: nonzero iff some byte is not canonical)
+                    exo |= FULL ? (canon ^ sr) : ((canon ^ sr) & bms);
+#else
                     exo = FULL ? __builtin_amdgcn_sad_u8(canon, sr, exo)
                                : __builtin_amdgcn_sad_u8(canon & bms, sr & bms, exo);
+#endif
                     const uint32_t qm = FULL ? qw[j] : (qw[j] & bm);
                     qhi |= qm;
-                    q20 += __popc((qm + 0x4A4A4A4Au) & (0x80808080u & bm));  // q > '5'
+                    const uint32_t m80 = FULL ? k80 : (k80 & bm);
+                    q20 += __popc((qm + 0x4A4A4A4Au) & m80);  // q > '5'
                     q30 += __popc(qm & 0x40404040u);  // q > '?' (= bit 6: q < 128 here; qm already masked)
-                    lowf += __popc(~(qm + limq) & (0x80808080u & bm));        // q < limit
+                    lowf += __popc(~(qm + limq_v) & m80);        // q < limit
                     // whole-read quality total: only -e reads it (passFilter's mean quality),
                     // which runs on the XTRA instantiation (and the merge variant)
                     if (!LEAN && (XTRA || MERGE)) tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);
@@ -1177,9 +1228,10 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 #endif
                 wp += wstep;
                 if constexpr (LY::kPfx)  // counts through chunk k (each <= 160): q20 | q30 << 8 | low << 16 | N << 24
-                    col[kCodeW + k * 64 + lane_x] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(nbf, lowf, 0x0c0c0400u),
-                                                                          __builtin_amdgcn_perm(q30, q20, 0x0c0c0400u),
-                                                                          0x05040100u);
+                    if ((k + 1) % LY::kPfxStep == 0)
+                        col[kCodeW + k / LY::kPfxStep * 64 + lane_x] =
+                            __builtin_amdgcn_perm(__builtin_amdgcn_perm(nbf, lowf, 0x0c0c0400u),
+                                                  __builtin_amdgcn_perm(q30, q20, 0x0c0c0400u), 0x05040100u);
             }
         }
         // Lowercase a c g t (the uppercase letter | 0x20: the same 3-bit key, so the same code) stay
@@ -1517,37 +1569,49 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
         int code = FQ_FAIL_LENGTH;
         uint32_t w20 = 0, w30 = 0;  // Q20/Q30 of the window, for the post stats
         int low = 0, tq = 0, nb = 0;
-        if (LY::kPfx && nn && wn > 0) {
-            // LEAN: the window is [0, wn) (no front trimming, no merge): the counts staged at the end
-            // of chunk c - 1 (c = wn >> 4) plus those of chunk c's bytes below wn
-            if (!(abl & 2)) {
-                const int c = wn >> 4, rb = wn & 15;
-                const uint32_t pv = col[kCodeW + max(c - 1, 0) * 64 + lane_x] & (c > 0 ? ~0u : 0u);
-                w20 = pv & 0xFFu;
-                w30 = (pv >> 8) & 0xFFu;
-                low = (int)((pv >> 16) & 0xFFu);
-                nb = (int)(pv >> 24);
-                if (__any(rb != 0) && rb != 0) {
-                    const uint4 q4 = qchunk(c);
-                    const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+        // Prefix counts (LY::kPfx) unless -c rewrote qualities after staging or -e needs the total
+        const bool use_pfx = LY::kPfx && !(XTRA && p.correction_enabled) && !(p.avg_qual_limit > 0) && !(abl & 2);
+        if (use_pfx && nn && wn > 0) {
+            // packed counts (q20 | q30 << 8 | low << 16 | N << 24) of chunk F's first nb bytes (1..16)
+            auto chunk_counts = [&](int F, int nbytes) -> uint32_t {
+                const uint4 q4 = qchunk(F);
+                const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+                uint32_t c20 = 0, c30 = 0, cl = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const uint32_t bm = bytemask(rb - 4 * j), qm = qw[j] & bm;
-                        w20 += __popc((qm + 0x4A4A4A4Au) & (0x80808080u & bm));
-                        w30 += __popc(qm & 0x40404040u);
-                        low += __popc(~(qm + limq) & (0x80808080u & bm));
-                    }
-                    // N bits of the chunk's first rb positions (read 2's column is reversed)
-                    const uint32_t nw = col[(kFN + (rc ? kChunks - 1 - c : c)) * 64 + lane_x];
-                    nb += __popc(nw & (rc ? 0x55555555u & ~posmask(16 - rb) : posmask(rb)));
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t bm = bytemask(nbytes - 4 * j), qm = qw[j] & bm, m80 = k80 & bm;
+                    c20 += __popc((qm + 0x4A4A4A4Au) & m80);
+                    c30 += __popc(qm & 0x40404040u);
+                    cl += __popc(~(qm + limq_v) & m80);
                 }
-            } else {
-                low = (int)lowf;
-                nb = (int)nbf;
-                w20 = q20;
-                w30 = q30;
-            }
-            code = filter_verdict(p, n, low, nb, tq - 33 * n, [&]() { return 0; });
+                // N bits of the chunk's first nbytes positions (read 2's column is reversed)
+                const uint32_t nw = col[(kFN + (rc ? kChunks - 1 - F : F)) * 64 + lane_x];
+                const uint32_t cn = __popc(nw & (rc ? 0x55555555u & ~posmask(16 - nbytes) : posmask(nbytes)));
+                return c20 | c30 << 8 | cl << 16 | cn << 24;
+            };
+            // counts of forward positions [0, x): the prefix word through chunk (c / step) * step - 1,
+            // then the chunks up to c - 1 and chunk c's bytes below x (wave-uniform branches)
+            auto p_at = [&](int x) -> uint32_t {
+                const int c = x >> 4, rb = x & 15, j = c / LY::kPfxStep;
+                uint32_t v = col[kCodeW + max(j - 1, 0) * 64 + lane_x] & (j > 0 ? ~0u : 0u);
+                if (LY::kPfxStep == 2 && __any(c & 1) && (c & 1)) v += chunk_counts(c - 1, 16);
+                if (__any(rb != 0) && rb != 0) v += chunk_counts(c, rb);
+                return v;
+            };
+            // window [ws, ws + wn) (ws = 0 unless front trimming, UMI or read 2's part of a merged read)
+            uint32_t v = p_at(ws + wn);
+            if (__any(ws > 0) && ws > 0) v -= p_at(ws);
+            w20 = v & 0xFFu;
+            w30 = (v >> 8) & 0xFFu;
+            low = (int)((v >> 16) & 0xFFu);
+            nb = (int)(v >> 24);
+            if (!(MERGE && merged))
+                code = filter_verdict(p, n, low, nb, -33 * n, [&]() {
+                    if (LEAN) return 0;  // not reached: LEAN excludes the complexity filter
+                    int diff = 0;
+                    for (int i = 0; i < n - 1; ++i) diff += seq(st + i) != seq(st + i + 1);
+                    return diff;
+                });
         } else if (nn && wn > 0) {
             // window sums = whole-read sums (from staging) minus the trimmed head [0, ws) and
             // tail [ws+wn, L): the trimmed parts are usually a few bases.  (FULL: a window

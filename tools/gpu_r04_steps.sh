@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-4 GPU call: the steps named in STEPS, in order, each under its own time limit; stops at the
+# first failure.  Outputs under gpurun_out/.
+#   STEPS="ab tests prof:C3 prof:C4 e2e_gz bench sq:C3"  ALTS=..  CONFIGS=..  TESTS=..
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+for st in ${STEPS:-}; do
+  echo "== step $st $(date +%T)"
+  case $st in
+  opcost) timeout -k 10 200 ./build/micro/opcost2 > gpurun_out/opcost2.txt 2>&1 || exit 1 ;;
+  sel) timeout -k 10 200 ./build/micro/sel > gpurun_out/sel.txt 2>&1 || exit 1 ;;
+  ab) ALTS="${ALTS:-base}" CONFIGS="${CONFIGS:-C3}" REPS=${REPS:-2} bash tools/ab.sh > gpurun_out/ab.txt 2>&1 || exit 1 ;;
+  tests) timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_engine_gpu.py tests/test_fullsize_gpu.py} -x -q --timeout 300 --timeout-method thread > gpurun_out/pt.log 2>&1 || exit 1 ;;
+  prof:*) c=${st#prof:}
+    CONFIG=$c PAIRS=20000000 bash tools/valu_probe.sh > gpurun_out/vprobe_sum_$c.txt 2>&1 || exit 1
+    CONFIG=$c VARIANTS=full FQ_ENGINE_LIB=$PWD/build/alt/lib_stamps.so timeout -k 10 300 python -u tools/ablate.py > gpurun_out/stamps_$c.txt 2>&1 || exit 1 ;;
+  e2e_gz) timeout -k 10 400 python -u tools/e2e_bench.py --pairs ${GZ_PAIRS:-4000000} --gz gzip --no-ref --null-out --repeat 2 > gpurun_out/e2e_gz.txt 2>&1 || exit 1 ;;
+  e2e) timeout -k 10 500 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 ${E2E_ARGS:-} > gpurun_out/e2e.txt 2>&1 || exit 1 ;;
+  bench) timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.log || exit 1 ;;
+  sq:*) c=${st#sq:}; ROUND=r04 CONFIGS=$c timeout -k 10 900 bash tools/pmc_sq.sh > gpurun_out/pmc_sq_$c.log 2>&1 || exit 1 ;;
+  *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+echo "== steps done $(date +%T)"
