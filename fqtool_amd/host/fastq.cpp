@@ -578,16 +578,14 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     : phred64_(phred64), bsize_((uint64_t)buf_size) {
     if (ends_with(path, ".gz")) {
         if ((bgzf_ = BgzfSource::open(path))) return;
-        if (inflate_whole(path, &map_, &map_size_, &map_cap_)) {  // parsed like a mapped plain file
-            total_ = map_size_;
-            eof_ = true;
-            return;
-        }
-        gz_ = gzopen(path.c_str(), "r");
-        if (!gz_) throw std::runtime_error("Failed to open file: " + path);
-        gzbuffer(gz_, 1 << 20);
-        gzrewind(gz_);
-        gz_ahead_.reset(new GzAhead(gz_, (size_t)bsize_));
+        path_ = path;
+        // inflated whole on a thread of its own (so the mates of a pair inflate side by side), then
+        // parsed like a mapped plain file; zlib's stream reader if that fails (settle())
+        whole_ = std::async(std::launch::async, [path] {
+            Whole w;
+            w.ok = inflate_whole(path, &w.p, &w.n, &w.cap);
+            return w;
+        });
         return;
     }
     fp_ = path == "/dev/stdin" ? stdin : std::fopen(path.c_str(), "rb");
@@ -608,7 +606,29 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     }
 }
 
+void FqBulkReader::settle() {
+    if (!whole_.valid()) return;
+    const Whole w = whole_.get();
+    if (w.ok) {
+        map_ = w.p;
+        map_size_ = w.n;
+        map_cap_ = w.cap;
+        total_ = map_size_;
+        eof_ = true;
+        return;
+    }
+    gz_ = gzopen(path_.c_str(), "r");
+    if (!gz_) throw std::runtime_error("Failed to open file: " + path_);
+    gzbuffer(gz_, 1 << 20);
+    gzrewind(gz_);
+    gz_ahead_.reset(new GzAhead(gz_, (size_t)bsize_));
+}
+
 FqBulkReader::~FqBulkReader() {
+    if (whole_.valid()) {  // (never read: wait for the inflate, then unmap its output)
+        const Whole w = whole_.get();
+        if (w.ok) munmap(w.p, w.cap);
+    }
     if (map_) munmap(map_, map_cap_ ? map_cap_ : map_size_);
     gz_ahead_.reset();  // (its thread reads gz_)
     if (gz_) gzclose(gz_);
@@ -616,6 +636,7 @@ FqBulkReader::~FqBulkReader() {
 }
 
 void FqBulkReader::begin(ByteBuf& text) {
+    settle();
     if (map_) {  // the mapping is the arena: offsets are file offsets, nothing is carried
         text.clear();
         text_ = nullptr;
@@ -1045,7 +1066,7 @@ fq_batch Pack::batch() const {
     return b;
 }
 
-bool pack_text(Pack& pk, Pool* pool) {
+bool pack_text(Pack& pk, Pool* pool, bool merged) {
     const int mates = pk.paired ? 2 : 1;
     const size_t n = (size_t)pk.n;
     std::atomic<bool> ok{true};
@@ -1067,6 +1088,7 @@ bool pack_text(Pack& pk, Pool* pool) {
         pk.span_bytes[m] = 0;
         pk.max_len[m] = 0;
     }
+    if (merged && mates == 2 && n) pk.out_text[0].resize_uninit(pk.span_bytes[0] + pk.span_bytes[1] + 24 * n + 16);
     const int parts = pool ? std::max(1, std::min(pool->size() * 2, (int)((n + 16383) / 16384))) : 1;
     std::vector<int> mx((size_t)parts * 2, 0);
     auto work = [&](int k) {
@@ -1161,6 +1183,7 @@ void pack_tiles(Pack& pk, Pool* pool) {
 }
 
 void FqBulkReader::seek(uint64_t off) {
+    settle();
     if (!map_) throw std::runtime_error("FqBulkReader::seek on an unmapped input");
     pos_ = (size_t)std::min<uint64_t>(off, map_size_);
     tbase_ = pos_ >> 6;

@@ -170,7 +170,10 @@ class FqBulkReader {
     // the records' offsets refer to (the arena, or the file mapping)
     const char* end();
     const std::string& error() const { return err_; }
-    bool mapped() const { return map_ != nullptr; }
+    bool mapped() {
+        settle();
+        return map_ != nullptr;
+    }
     void seek(uint64_t off);  // mapped files: the next record is read from stream offset off
 
    private:
@@ -182,6 +185,14 @@ class FqBulkReader {
     size_t sz() const { return map_ ? map_size_ : text_->size(); }
     bool skip_ok(uint64_t g) const;
     void read_more();
+    void settle();  // a whole-file inflate started by the constructor: wait for it, or fall back
+    struct Whole {
+        bool ok = false;
+        char* p = nullptr;
+        size_t n = 0, cap = 0;
+    };
+    std::future<Whole> whole_;  // (.gz, not BGZF: libdeflate inflating the whole file on a thread)
+    std::string path_;
     gzFile gz_ = nullptr;
     std::unique_ptr<BgzfSource> bgzf_;  // BGZF input: members inflated on several threads
     std::unique_ptr<GzAhead> gz_ahead_;  // other gzip: inflated on a thread of its own, ahead of the parser
@@ -295,7 +306,9 @@ void pack_tiles(Pack& pk, Pool* pool);
 // fq_text_rec per record, the planes' stride and the output buffers; no planes are built on the
 // host.  False (the pack then goes through pack_tiles) when a span exceeds 4 GiB or a line 65535
 // bytes.
-bool pack_text(Pack& pk, Pool* pool);
+// merged: -m (PE), whose output is the merged stream in out_text[0] (both mates' text plus a
+// merged name's tag per pair; out_text[1] only takes the engine's adapter entries).
+bool pack_text(Pack& pk, Pool* pool, bool merged = false);
 
 // Reads up to max_n records (pairs) into a pack and builds its planes.  Two-file PE input is
 // parsed by two threads, one per mate, with the reference's stop rule and messages (the pair
@@ -311,7 +324,7 @@ class PackReader {
     // continue at stream offsets off1 / off2 (mapped regular files only: where the GPU's raw
     // stream stopped), numbering packs from first_seq
     void seek(uint64_t off1, uint64_t off2, uint64_t first_seq);
-    bool mapped() const { return r1_.mapped() && (!r2_ || r2_->mapped()); }
+    bool mapped() { return r1_.mapped() && (!r2_ || r2_->mapped()); }
     double parse_s = 0, tiles_s = 0;  // time spent parsing records / filling batch planes
     bool defer_tiles = false;         // next() leaves pack_tiles to the caller (another thread)
 

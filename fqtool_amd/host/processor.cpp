@@ -2,6 +2,9 @@
 #include "processor.h"
 
 #include <algorithm>
+#include <atomic>
+#include <emmintrin.h>
+#include <functional>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -551,6 +554,14 @@ void OutputSet::write_text(const char* t1, size_t n1, const char* t2, size_t n2,
     if (err) std::rethrow_exception(err);
 }
 
+void OutputSet::write_merged_text(const char* t, size_t n, std::function<void()> done) {
+    if (!wm_) {
+        done();
+        return;
+    }
+    wm_->write_raw(t, n, std::move(done));
+}
+
 void OutputSet::close() {
     std::exception_ptr first;
     for (auto* w : {&w1_, &w2_, &wu1_, &wu2_, &wf_, &wm_}) {
@@ -729,7 +740,7 @@ class SplitSink {
     bool have_ref_ = false;
 };
 
-Sink::Sink(const Options& o, Pool* pool) : o_(o), pool_(pool) {
+Sink::Sink(const Options& o, Pool* pool) : o_(o), pool_(pool), merge_(o.merge && o.paired()) {
     if (o.split()) split_.reset(new SplitSink(o, pool));
     else outs_.reset(new OutputSet(o, pool));
 }
@@ -754,7 +765,8 @@ void Sink::consume(const Pack& pk, const fq_read_result* res) {
 
 void Sink::consume_text(const Pack& pk, std::function<void()> done) {
     pairs_ += (uint64_t)pk.n;
-    outs_->write_text(pk.out_text[0].data(), pk.tout.bytes[0], pk.out_text[1].data(), pk.tout.bytes[1], std::move(done));
+    if (merge_) outs_->write_merged_text(pk.out_text[0].data(), pk.tout.bytes[0], std::move(done));
+    else outs_->write_text(pk.out_text[0].data(), pk.tout.bytes[0], pk.out_text[1].data(), pk.tout.bytes[1], std::move(done));
 }
 
 void Sink::close() {
@@ -775,6 +787,201 @@ double since(std::chrono::steady_clock::time_point t) {
 }
 
 struct Stopped {};  // another pipeline stage failed and closed the queues
+
+// Raw streams on several engines (--devices with more than one entry; fq_engine_raw_*).  The host cuts
+// the inputs into windows of whole pairs: it counts the line feeds of the bytes it preads and ends
+// every mate's window after the same number of four-line records (at most the engines' max_batch),
+// so the windows are independent of each other and go round-robin to the engines (window k to
+// engine k mod G, pack seq_no k), each engine copying, indexing and running its own.  A window's
+// pack launches only after the window before it has launched and taken all its pairs (the GPU's
+// indexing reports that at launch, fq_raw_result), so when the GPU path stops -- an irregular record
+// the line count could not see (empty or '\r'-ended lines, a read longer than the engine takes) --
+// no later window has reached a kernel or an accumulator: the engines drop the windows they hold and
+// the host reader resumes at the stopping window's offsets, pack numbers continuing (as with one
+// engine, src/fqreader.cpp:160-195).
+struct RawStage {  // one window's page-locked staging (one buffer per mate)
+    RawStage() : buf{ByteBuf(true), ByteBuf(true)} {}
+    ByteBuf buf[2];
+};
+struct RawResumeInfo {
+    bool done = false;
+    uint64_t off[2] = {0, 0};
+    uint64_t next_seq = 0;
+};
+struct RawMulti {
+    struct Win {
+        uint64_t id = 0, start[2] = {0, 0}, n[2] = {0, 0};
+        int64_t pairs = 0;
+        int stage = -1;
+        bool end = false;  // no window: the stream ends here (the host reader takes start[])
+    };
+    int G = 1, mates = 1;
+    int fd[2] = {-1, -1};
+    uint64_t size[2] = {0, 0};
+    uint64_t wcap = (uint64_t)64 << 20;
+    std::vector<std::unique_ptr<RawStage>> stages;
+    Queue<int> free_stages{1024};
+    std::vector<std::unique_ptr<Queue<Win>>> wq;  // per engine, windows in id order
+    std::mutex m;
+    std::condition_variable cv;
+    uint64_t next_launch = 0;  // the id allowed to launch next
+    bool stopped = false;      // the stream has ended; rr says where
+    RawResumeInfo rr;
+    std::string why;
+    std::atomic<uint64_t> pairs{0}, packs{0};
+    double read_s = 0, stage_wait_s = 0;
+    std::exception_ptr err;
+    std::function<void(const RawResumeInfo&)> on_end;  // called once, when `stopped` is set
+
+    ~RawMulti() {
+        for (int& f : fd)
+            if (f >= 0) ::close(f);
+    }
+    // under m: the stream ends (first caller wins)
+    void end_locked(const RawResumeInfo& r, const std::string& w) {
+        if (stopped) return;
+        stopped = true;
+        rr = r;
+        why = w;
+        cv.notify_all();
+        free_stages.close();  // (the window reader stops at its next stage)
+        if (on_end) on_end(rr);
+    }
+    void fail(std::exception_ptr e) {
+        std::lock_guard<std::mutex> g(m);
+        if (!err) err = e;
+        RawResumeInfo r;  // (the caller rethrows; the host reader must not wait forever, nor read)
+        r.done = true;
+        end_locked(r, "error");
+    }
+
+    // The window reader: exact pair-aligned windows, dealt round-robin; runs until the input is
+    // consumed, a window cannot be cut, or the stream stopped.
+    void read_windows(int target, int max_batch, Pool& pool) {
+        try {
+            uint64_t pos[2] = {0, 0};
+            double bpr[2] = {0, 0};  // bytes per record so far
+            const uint64_t piece = (uint64_t)1 << 20;
+            const char* w0_env = std::getenv("FQ_RAW_WINDOW0");  // first window's bytes (tests: tiny windows)
+            const uint64_t w0 = w0_env ? std::max<uint64_t>(4096, std::strtoull(w0_env, nullptr, 10)) : (uint64_t)4 << 20;
+            std::vector<uint32_t> cnt[2];
+            for (uint64_t id = 0;; ++id) {
+                {
+                    std::lock_guard<std::mutex> g(m);
+                    if (stopped) break;
+                }
+                Win w;
+                w.id = id;
+                bool left = false;
+                for (int k = 0; k < mates; ++k) left = left || pos[k] < size[k];
+                if (!left) {
+                    w.end = true;
+                    for (int k = 0; k < mates; ++k) w.start[k] = pos[k];
+                    wq[(size_t)(id % (uint64_t)G)]->push(w);
+                    break;
+                }
+                const auto s0 = std::chrono::steady_clock::now();
+                if (!free_stages.pop(w.stage)) break;
+                stage_wait_s += since(s0);
+                RawStage& st = *stages[(size_t)w.stage];
+                uint64_t want[2] = {0, 0};
+                for (int k = 0; k < mates; ++k)
+                    want[k] = bpr[k] > 0 ? (uint64_t)(target * bpr[k] * 1.02) + 4096 : w0;
+                int64_t P = 0;
+                for (;;) {  // read, count records; grow the window when it holds no whole pair
+                    const auto r0 = std::chrono::steady_clock::now();
+                    uint64_t n[2] = {0, 0};
+                    int pieces[2] = {0, 0};
+                    for (int k = 0; k < mates; ++k) {
+                        n[k] = std::min(std::min(want[k], wcap), size[k] - pos[k]);
+                        st.buf[k].resize_uninit((size_t)std::max<uint64_t>(n[k], 1));
+                        pieces[k] = (int)((n[k] + piece - 1) / piece);
+                        cnt[k].assign((size_t)pieces[k], 0);
+                    }
+                    std::atomic<bool> short_read{false};
+                    pool.run(pieces[0] + pieces[1], [&](int q) {
+                        const int k = q < pieces[0] ? 0 : 1;
+                        const int pi = k ? q - pieces[0] : q;
+                        const uint64_t o = (uint64_t)pi * piece, len = std::min(piece, n[k] - o);
+                        char* dst = st.buf[k].data() + o;
+                        uint64_t got = 0;
+                        while (got < len) {
+                            const ssize_t r = pread(fd[k], dst + got, (size_t)(len - got), (off_t)(pos[k] + o + got));
+                            if (r <= 0) {
+                                short_read = true;
+                                return;
+                            }
+                            got += (uint64_t)r;
+                        }
+                        cnt[k][(size_t)pi] = count_lf(dst, (size_t)len);
+                    });
+                    if (short_read) throw std::runtime_error("input file changed while reading");
+                    read_s += since(r0);
+                    P = max_batch;
+                    for (int k = 0; k < mates; ++k) {
+                        uint64_t lf = 0;
+                        for (uint32_t c : cnt[k]) lf += c;
+                        P = std::min<int64_t>(P, (int64_t)(lf / 4));
+                    }
+                    bool can_grow = false;
+                    for (int k = 0; k < mates; ++k) can_grow = can_grow || (n[k] < wcap && pos[k] + n[k] < size[k]);
+                    if (P > 0 || !can_grow) {
+                        for (int k = 0; k < mates; ++k) w.n[k] = n[k];
+                        break;
+                    }
+                    for (int k = 0; k < mates; ++k) want[k] = std::min(wcap, std::max<uint64_t>(2 * n[k], 4096));
+                }
+                if (P <= 0) {  // no whole pair fits: the host reader takes it from here
+                    free_stages.push(w.stage);
+                    w.stage = -1;
+                    w.end = true;
+                    for (int k = 0; k < mates; ++k) {
+                        w.start[k] = pos[k];
+                        w.n[k] = 0;
+                    }
+                    wq[(size_t)(id % (uint64_t)G)]->push(w);
+                    break;
+                }
+                for (int k = 0; k < mates; ++k) {  // each mate's window ends after its P-th record
+                    const uint64_t target_lf = 4 * (uint64_t)P;
+                    uint64_t seen = 0;
+                    size_t pi = 0;
+                    while (seen + cnt[k][pi] < target_lf) seen += cnt[k][pi++];
+                    const uint64_t at = nth_lf(st.buf[k].data() + pi * piece, (size_t)std::min(piece, w.n[k] - pi * piece),
+                                               (size_t)(target_lf - seen));
+                    w.start[k] = pos[k];
+                    w.n[k] = pi * piece + at + 1;
+                    pos[k] += w.n[k];
+                    bpr[k] = bpr[k] > 0 ? 0.5 * bpr[k] + 0.5 * (double)w.n[k] / (double)P : (double)w.n[k] / (double)P;
+                }
+                w.pairs = P;
+                if (!wq[(size_t)(id % (uint64_t)G)]->push(w)) {
+                    free_stages.push(w.stage);
+                    break;
+                }
+            }
+        } catch (...) {
+            fail(std::current_exception());
+        }
+        for (auto& q : wq) q->close();
+    }
+    static uint32_t count_lf(const char* p, size_t n) {
+        uint32_t c = 0;
+        size_t i = 0;
+        const __m128i nl = _mm_set1_epi8('\n');
+        for (; i + 16 <= n; i += 16)
+            c += (uint32_t)__builtin_popcount(
+                (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i)), nl)));
+        for (; i < n; ++i) c += p[i] == '\n';
+        return c;
+    }
+    // offset of the k-th (1-based) line feed in [p, p + n)
+    static uint64_t nth_lf(const char* p, size_t n, size_t k) {
+        for (size_t i = 0; i < n; ++i)
+            if (p[i] == '\n' && --k == 0) return i;
+        throw std::runtime_error("raw window: line feed count mismatch");
+    }
+};
 
 // One engine per entry of --devices (several may share a GPU), each fed by its own dispatcher
 // thread: pack k goes to engine k mod G.  A pack with longer reads (or more of them) re-creates
@@ -836,7 +1043,7 @@ struct Lane {
         if (rc != 1) throw std::runtime_error(std::string("fq_engine_poll: ") + fq_engine_last_error(e));
         if (seq != pk->seq_no) throw std::runtime_error("engine completed packs out of order");
         if (pk->raw) {  // its input window was copied: recycle the staging; the output sizes are in
-            if (pk->stage >= 0) free_stages.push(pk->stage);
+            if (pk->stage >= 0) (multi ? multi->free_stages : free_stages).push(pk->stage);
             pk->stage = -1;
             pk->tout = pk->rout.text;
         }
@@ -885,6 +1092,8 @@ struct Lane {
     };
     std::vector<std::unique_ptr<Stage>> stages;
     Queue<int> free_stages{64};
+    RawMulti* multi = nullptr;  // several engines: the shared window source (run_raw_multi)
+    bool merge = false;         // -m (PE): raw packs' mate-0 output is the merged stream
     uint64_t raw_pairs = 0, raw_packs = 0;  // what the raw stream took
     double raw_read_s = 0, raw_stage_wait_s = 0, raw_ready_wait_s = 0;  // window reader: preads, waits
     double raw_pack_wait_s = 0, raw_enqueue_s = 0;  // dispatcher: waiting for a spare pack, enqueue calls
@@ -1111,7 +1320,9 @@ struct Lane {
                         cin[1] = carry[1];
                     }
                     for (int m = 0; m < 2; ++m) {  // (output text, then the adapter entries)
-                        const size_t cap = m < mates ? (size_t)(cin[m] + w.n[m] + 4 * (uint64_t)target + 64) : 0;
+                        size_t cap = m < mates ? (size_t)(cin[m] + w.n[m] + 4 * (uint64_t)target + 64) : 0;
+                        if (merge && m == 0)  // (-m: the merged stream of both mates' text)
+                            cap = (size_t)(cin[0] + w.n[0] + cin[1] + w.n[1] + 28 * (uint64_t)target + 64);
                         pk->out_text[m].resize_uninit(cap);
                         pk->rout.text.text[m] = m < mates ? pk->out_text[m].data() : nullptr;
                     }
@@ -1197,13 +1408,141 @@ struct Lane {
         return rr;
     }
 
+    // This engine's part of a raw stream on several engines (RawMulti): its windows in id order,
+    // enqueued up to raw_ahead ahead, each launched in its turn (the previous window launched and
+    // took all its pairs).
+    void run_raw_multi(RawMulti& R, int g, int target, Queue<std::unique_ptr<Pack>>& spare) {
+        multi = &R;
+        const int raw_depth = 4;
+        const size_t raw_ahead = 3;
+        std::deque<RawMulti::Win> enq;  // enqueued on this engine (or the end marker), not launched
+        bool input_done = false;
+        bool engine_raw = false;
+        auto drop_all = [&] {  // windows not launched: their copies finish, then the stages return
+            (void)fq_engine_sync(e);
+            if (engine_raw) (void)fq_engine_raw_end(e);
+            engine_raw = false;
+            for (const RawMulti::Win& w : enq)
+                if (w.stage >= 0) R.free_stages.push(w.stage);
+            enq.clear();
+            RawMulti::Win w;
+            while (R.wq[(size_t)g]->pop(w))
+                if (w.stage >= 0) R.free_stages.push(w.stage);
+        };
+        try {
+            if (fq_engine_raw_begin(e, R.wcap, (uint64_t)16 << 20) != FQ_OK)
+                throw std::runtime_error(std::string("fq_engine_raw_begin: ") + fq_engine_last_error(e));
+            engine_raw = true;
+            for (;;) {
+                while (enq.size() < raw_ahead && !input_done) {
+                    RawMulti::Win w;
+                    if (!R.wq[(size_t)g]->pop(w)) {
+                        input_done = true;
+                        break;
+                    }
+                    if (!w.end) {
+                        fq_raw_window rw{};
+                        for (int m = 0; m < R.mates; ++m) {
+                            rw.bytes[m] = R.stages[(size_t)w.stage]->buf[m].data();
+                            rw.n[m] = w.n[m];
+                        }
+                        const auto q0 = std::chrono::steady_clock::now();
+                        const int qrc = fq_engine_raw_enqueue(e, &rw);
+                        raw_enqueue_s += since(q0);
+                        if (qrc != FQ_OK) {
+                            R.free_stages.push(w.stage);
+                            throw std::runtime_error(std::string("fq_engine_raw_enqueue: ") + fq_engine_last_error(e));
+                        }
+                    } else {
+                        input_done = true;
+                    }
+                    enq.push_back(w);
+                }
+                if (enq.empty()) break;
+                const RawMulti::Win w = enq.front();
+                {
+                    std::unique_lock<std::mutex> lk(R.m);
+                    R.cv.wait(lk, [&] { return R.stopped || R.next_launch == w.id; });
+                    if (R.stopped) break;
+                    if (w.end) {  // the input ends (or no whole pair fits): the host reader goes on
+                        RawResumeInfo rr;
+                        rr.done = true;
+                        for (int m = 0; m < R.mates; ++m) {
+                            rr.off[m] = w.start[m];
+                            rr.done = rr.done && w.start[m] == R.size[m];
+                        }
+                        rr.next_seq = w.id;
+                        R.end_locked(rr, rr.done ? "end of input" : "no whole pair fits a window");
+                        enq.pop_front();
+                        break;
+                    }
+                }
+                enq.pop_front();
+                std::unique_ptr<Pack> pk;
+                const auto p0 = std::chrono::steady_clock::now();
+                if (!spare.pop(pk)) throw Stopped();
+                raw_pack_wait_s += since(p0);
+                pk->clear();
+                pk->raw = true;
+                pk->text_mode = true;
+                pk->paired = R.mates == 2;
+                pk->seq_no = w.id;
+                pk->stage = w.stage;
+                for (int m = 0; m < 2; ++m) {  // (output text, then the adapter entries)
+                    size_t cap = m < R.mates ? (size_t)(w.n[m] + 4 * (uint64_t)target + 64) : 0;
+                    if (merge && m == 0)  // (-m: the merged stream of both mates' text)
+                        cap = (size_t)(w.n[0] + w.n[1] + 28 * (uint64_t)target + 64);
+                    pk->out_text[m].resize_uninit(cap);
+                    pk->rout.text.text[m] = m < R.mates ? pk->out_text[m].data() : nullptr;
+                }
+                fq_raw_result r{};
+                const auto e0 = std::chrono::steady_clock::now();
+                if (fq_engine_raw_launch(e, &r, &pk->rout, w.id) != FQ_OK) {
+                    R.free_stages.push(w.stage);
+                    throw std::runtime_error(std::string("fq_engine_raw_launch: ") + fq_engine_last_error(e));
+                }
+                submit_s += since(e0);
+                if (first_submit < 0) first_submit = since(t_start);
+                pk->n = r.pairs;
+                pk->max_cycles = max_cycles;
+                R.pairs += (uint64_t)r.pairs;
+                ++R.packs;
+                {
+                    std::lock_guard<std::mutex> lk(R.m);
+                    if (r.pairs != w.pairs || r.stop) {  // the GPU path stops inside this window
+                        RawResumeInfo rr;
+                        for (int m = 0; m < R.mates; ++m) rr.off[m] = w.start[m] + w.n[m] - r.carry[m];
+                        rr.next_seq = w.id + 1;
+                        R.end_locked(rr, std::string(r.stop ? "irregular record" : "short window") + " in window " +
+                                             std::to_string(w.id) + " (" + std::to_string(r.pairs) + " of " +
+                                             std::to_string(w.pairs) + " pairs)");
+                    }
+                    R.next_launch = w.id + 1;
+                    R.cv.notify_all();
+                }
+                while (!inflight.empty() && complete_oldest(false)) {
+                }
+                if ((int)inflight.size() >= raw_depth) complete_oldest();
+                inflight.push_back(std::move(pk));
+            }
+            while (!inflight.empty()) complete_oldest();
+            drop_all();
+        } catch (...) {
+            R.fail(std::current_exception());
+            inflight.clear();
+            drop_all();
+            throw;
+        }
+        multi = nullptr;
+    }
+
     // the dispatcher: planes (or the text index) of each pack, submit, completions in order
     void run(const Options& o, bool text_mode, Pool& pool, HostAcc& acc, std::mutex& acc_m) {
         try {
             std::unique_ptr<Pack> pk;
             while (in.pop(pk)) {
                 const auto p0 = std::chrono::steady_clock::now();
-                const bool as_text = text_mode && pack_text(*pk, &pool);
+                const bool as_text = text_mode && pack_text(*pk, &pool, o.merge);
                 if (!as_text) {
                     pack_tiles(*pk, &pool);
                     prepare_pack(o, *pk, &pool);
@@ -1350,10 +1689,12 @@ int run_tool(int argc, char** argv) {
     // uses --adapter_of_read{1,2} only (src/peprocessor.cpp:319, src/filterresult.cpp:315), so
     // the detection runs concurrently with the pipeline and is joined before the reports.  The
     // pack reader's messages wait for its messages (set_reader_stderr_gate).
+    // It starts once the engines exist (FQ_DETECT_EARLY=1: before them), so its k-mer device work
+    // does not compete with HIP start-up and the engines' allocations.
     std::promise<void> det_done;
     std::future<Detection> det;
-    if (o.detect_pe_adapter && !o.in2.empty()) {
-        set_reader_stderr_gate(det_done.get_future().share());
+    const bool det_on = o.detect_pe_adapter && !o.in2.empty();
+    auto start_detection = [&] {
         det = std::async(std::launch::async, [&o, &det_done] {
             Detection d;
             try {
@@ -1364,6 +1705,11 @@ int run_tool(int argc, char** argv) {
             det_done.set_value();
             return d;
         });
+    };
+    const bool det_early = std::getenv("FQ_DETECT_EARLY") != nullptr;  // (profiling)
+    if (det_on) {
+        set_reader_stderr_gate(det_done.get_future().share());
+        if (det_early) start_detection();
     }
     // FQ_TIMING=1: the time the pipeline's teardown (pinned packs, engines, pool, mappings) takes
     // after the summary line, on stderr once everything is destroyed
@@ -1397,17 +1743,22 @@ int run_tool(int argc, char** argv) {
         // GPU-side ingest and egress (fq_engine_submit_text): the engine builds the planes from
         // the FASTQ text and writes the output text, for the plain out1 (+ out2) case
         const char* tm_env = std::getenv("FQ_TEXT_MODE");
-        const bool text_mode = !(tm_env && std::string(tm_env) == "0") && !o.merge && !o.correction && !o.umi &&
+        // (-m: every pair's output goes to the merged stream, which the engine writes as well)
+        const bool text_mode = !(tm_env && std::string(tm_env) == "0") && !o.correction && !o.umi &&
                                !o.index_filter && !o.split() && !o.phred64 && o.failed_out.empty() &&
-                               o.unpaired1.empty() && o.unpaired2.empty() && !o.out1.empty() &&
-                               (!paired || !o.out2.empty());
+                               o.unpaired1.empty() && o.unpaired2.empty() &&
+                               (o.merge ? paired && !o.merge_out.empty()
+                                        : !o.out1.empty() && (!paired || !o.out2.empty()));
         std::vector<std::unique_ptr<Lane>> lanes;
         const int cyc0 = std::max(16, round16(o.merge ? 2 * est : est)), stride0 = round16(std::max(est, 16));
         for (int g = 0; g < G; ++g) {
             lanes.emplace_back(new Lane(devices[(size_t)g], depth));
             lanes.back()->t_start = t0;
+            lanes.back()->merge = o.merge && paired;
             lanes.back()->make(o, cyc0, (int)pack_n, stride0);
         }
+        const double engines_ready_s = since(t0);
+        if (det_on && !det_early) start_detection();
         std::exception_ptr reader_err, format_err;
         double parse_s = 0, spare_wait_s = 0;
         HostAcc acc(o.insert_size_max);
@@ -1425,10 +1776,67 @@ int run_tool(int argc, char** argv) {
         // GPU-side record indexing (fq_engine_raw_*) for plain files on one engine: the engine's
         // dispatcher drives the raw stream first; the host reader takes over only where it stops
         const char* raw_env = std::getenv("FQ_RAW_MODE");
-        const bool raw_mode = text_mode && G == 1 && !o.interleaved && !(raw_env && std::string(raw_env) == "0") &&
-                              pr.mapped() && !ends_with_gz(o.in1) && (!paired || !ends_with_gz(o.in2));
+        const bool raw_mode = text_mode && !o.interleaved && !(raw_env && std::string(raw_env) == "0") &&
+                              !ends_with_gz(o.in1) && (!paired || !ends_with_gz(o.in2)) && pr.mapped();
         std::promise<Lane::RawResume> raw_p;
         std::shared_future<Lane::RawResume> raw_f = raw_p.get_future().share();
+        // several engines: one window source cutting whole pairs, dealt round-robin (RawMulti)
+        std::unique_ptr<RawMulti> rm;
+        std::thread rm_reader, rm_warmer;
+        if (raw_mode && G > 1) {
+            rm.reset(new RawMulti);
+            RawMulti& R = *rm;
+            R.G = G;
+            R.mates = paired ? 2 : 1;
+            const std::string files[2] = {o.in1, o.in2};
+            bool ok = true;
+            for (int m = 0; m < R.mates; ++m) {
+                R.fd[m] = ::open(files[m].c_str(), O_RDONLY);
+                struct stat st;
+                ok = ok && R.fd[m] >= 0 && fstat(R.fd[m], &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0;
+                if (ok) {
+                    R.size[m] = (uint64_t)st.st_size;
+                    (void)posix_fadvise(R.fd[m], 0, 0, POSIX_FADV_SEQUENTIAL);
+                }
+            }
+            for (int g = 0; g < G; ++g) R.wq.emplace_back(new Queue<RawMulti::Win>(4));
+            std::promise<Lane::RawResume>* pp = &raw_p;
+            R.on_end = [pp](const RawResumeInfo& ri) {
+                Lane::RawResume r;
+                r.done = ri.done;
+                r.off[0] = ri.off[0];
+                r.off[1] = ri.off[1];
+                r.next_seq = ri.next_seq;
+                pp->set_value(r);
+            };
+            if (!ok) {  // (the host reader takes the whole input)
+                for (auto& q : R.wq) q->close();
+                std::lock_guard<std::mutex> g(R.m);
+                RawResumeInfo ri;
+                R.end_locked(ri, "inputs are not regular files");
+            } else {
+                // staging: packs in flight + enqueued per engine, and a few for the reader to run ahead;
+                // the first is handed out at once, the others page-locked on a helper thread
+                const int kStages = G * 8 + 4;
+                for (int i = 0; i < kStages; ++i) R.stages.emplace_back(new RawStage);
+                R.free_stages.push(0);
+                rm_warmer = std::thread([&R, kStages] {
+                    int i = 1;
+                    try {
+                        for (; i < kStages; ++i) {
+                            for (int m = 0; m < R.mates; ++m) R.stages[(size_t)i]->buf[m].reserve((size_t)R.wcap);
+                            if (!R.free_stages.push(i)) return;
+                        }
+                    } catch (...) {  // (no memory to reserve ahead: the rest grow when first used)
+                        for (; i < kStages; ++i)
+                            if (!R.free_stages.push(i)) return;
+                    }
+                });
+                rm_reader = std::thread([&R, &lanes, &pool, pack_n] {
+                    R.read_windows((int)pack_n, lanes[0]->max_batch, pool);
+                });
+            }
+        }
         std::thread reader([&] {
             try {
                 if (raw_mode) {  // wait for the raw stream's end; resume where it stopped
@@ -1454,11 +1862,13 @@ int run_tool(int argc, char** argv) {
             }
             for (auto& l : lanes) l->in.close();
         });
-        for (auto& lp : lanes) {
-            Lane* l = lp.get();
-            l->t = std::thread([&, l] {
+        for (size_t gi = 0; gi < lanes.size(); ++gi) {
+            Lane* l = lanes[gi].get();
+            l->t = std::thread([&, l, gi] {
                 try {
-                    if (raw_mode) {
+                    if (raw_mode && rm) {
+                        l->run_raw_multi(*rm, (int)gi, (int)pack_n, spare);
+                    } else if (raw_mode) {
                         Lane::RawResume rr;
                         rr.done = true;
                         try {
@@ -1520,6 +1930,18 @@ int run_tool(int argc, char** argv) {
         for (auto& l : lanes) l->t.join();
         formatter.join();
         reader.join();
+        if (rm) {
+            {
+                std::lock_guard<std::mutex> g(rm->m);
+                RawResumeInfo ri;
+                ri.done = true;
+                rm->end_locked(ri, "pipeline stopped");  // (no-op once ended; frees a waiting reader)
+            }
+            for (auto& q : rm->wq) q->close();
+            if (rm_reader.joinable()) rm_reader.join();
+            if (rm_warmer.joinable()) rm_warmer.join();
+            if (rm->err) std::rethrow_exception(rm->err);
+        }
         const double pipeline_done_s = since(t0);
         double tiles_s = 0, submit_s = 0, wait_s = 0;
         std::exception_ptr lane_err;
@@ -1567,7 +1989,11 @@ int run_tool(int argc, char** argv) {
         }
         teardown.logged = std::chrono::steady_clock::now();
         log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s)" +
-            (raw_mode ? " (raw stream: GPU record indexing, ingest/egress: " + std::to_string(lanes[0]->raw_pairs) + " pairs in " +
+            (raw_mode && rm ? " (raw stream on " + std::to_string(G) + " engines: host-cut pair windows, GPU record indexing, "
+                              "ingest/egress: " + std::to_string(rm->pairs.load()) + " pairs in " + std::to_string(rm->packs.load()) +
+                              " packs, ended: " + rm->why + "; window reads " + std::to_string(rm->read_s) +
+                              " s, reader waiting for a stage " + std::to_string(rm->stage_wait_s) + " s)"
+             : raw_mode ? " (raw stream: GPU record indexing, ingest/egress: " + std::to_string(lanes[0]->raw_pairs) + " pairs in " +
                             std::to_string(lanes[0]->raw_packs) + " packs, ended: " + lanes[0]->raw_end + "; window reads " +
                             std::to_string(lanes[0]->raw_read_s) + " s, reader waiting for a stage " +
                             std::to_string(lanes[0]->raw_stage_wait_s) + " s, dispatcher waiting for windows " +
@@ -1577,11 +2003,13 @@ int run_tool(int argc, char** argv) {
             std::to_string(since(t0)) + " s, engine submit " + std::to_string(submit_s) + " s, wait " + std::to_string(wait_s) + " s; pre-pass " +
             std::to_string(prepass_s) + " s, adapter detection (concurrent) " + std::to_string(detect_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +
             " s, tiles " + std::to_string(tiles_s) + " s, reader waiting " + std::to_string(spare_wait_s) +
-            " s, first pack submitted at " + std::to_string(lanes[0]->first_submit) + " s, pipeline done at " +
+            " s, engines ready at " + std::to_string(engines_ready_s) + " s, first pack submitted at " +
+            std::to_string(lanes[0]->first_submit) + " s, pipeline done at " +
             std::to_string(pipeline_done_s) +
             " s; JSON report " + o.json_file + ", HTML report " + o.html_file);
     } catch (const std::exception& e) {
         if (det.valid()) det.wait();  // the pre-pass's messages come first, as in the reference
+        else if (det_on) det_done.set_value();  // (it never started: release the reader's gate)
         std::cerr << "ERROR: " << e.what() << std::endl;
         return 255;
     }

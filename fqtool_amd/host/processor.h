@@ -37,6 +37,8 @@ class OutputSet {
     // out1 / out2 text as is (waits until both writers have taken it)
     // queue engine-assembled output text of both mates; `done` runs once both are written
     void write_text(const char* t1, size_t n1, const char* t2, size_t n2, std::function<void()> done);
+    // -m: a text pack's merged stream (the merged output; out1 / out2 get nothing)
+    void write_merged_text(const char* t, size_t n, std::function<void()> done);
     void close();  // flushes and closes every file
 
    private:
@@ -71,6 +73,7 @@ class Sink {
     std::unique_ptr<OutputSet> outs_;
     std::unique_ptr<SplitSink> split_;
     uint64_t pairs_ = 0;  // pairs (reads) consumed so far: the next pack's first global index
+    bool merge_ = false;  // -m (PE): text packs carry the merged stream
 };
 
 // Before the engine call: per-pair index-filter flags (Filter::filterByIndex) when enabled.

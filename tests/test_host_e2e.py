@@ -169,8 +169,9 @@ def test_split_with_several_workers(case, host, oracle, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("devices", ["0", "0,0,0"])
 @pytest.mark.parametrize("case", E.ok_cases())
-def test_fqtool_raw_stream_small_windows_matches_reference(case, tmp_path):
+def test_fqtool_raw_stream_small_windows_matches_reference(case, devices, tmp_path):
     """GPU record indexing (fq_engine_raw_*) under stress: gzip inputs are decompressed to plain
     files so every case with plain outputs takes the raw stream, the first window is 4 KiB and packs
     hold 7 pairs, so records straddle windows (the device carry), the mates' windows are sized
@@ -191,12 +192,16 @@ def test_fqtool_raw_stream_small_windows_matches_reference(case, tmp_path):
                 shutil.copyfileobj(f, g)
             argv[k] = str(plain)
     argv += ["--pack_pairs", "7"]
+    if devices != "0" and not E.is_split(case):  # (-d tables merge across engines; split keeps -w)
+        argv += ["--devices", devices]
     env = dict(os.environ, FQ_RAW_WINDOW0="4096")
     p = subprocess.run(argv, capture_output=True, cwd=outd, timeout=300, env=env)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     if case in ("td_pe_qag", "td_pe_plain", "td_pe_detect", "synth_pe_c3", "synth_pe_c5", "synth_se_c2", "polygr_pe",
-                "edge_pe_dup", "td_se_q"):
+                "edge_pe_dup", "td_se_q", "td_pe_merge", "td_pe_merge_discard", "synth_pe_c4", "edge_pe_merge"):
         assert "raw stream" in p.stderr.decode(), p.stderr.decode()[-1000:]
+        if devices != "0":
+            assert "raw stream on 3 engines" in p.stderr.decode(), p.stderr.decode()[-1000:]
     E.check_outputs(case, str(outd))
 
 
