@@ -70,7 +70,7 @@ def e2e_path(tool_log):
         mid = "host parse -> text packs -> device planes -> kernels -> GPU output text"
     else:
         mid = "host parse -> pinned tile packs -> kernels -> records -> host formatting"
-    return f"fqtool binary: FASTQ (page cache) -> {mid} -> /dev/null + JSON, C3 options"
+    return f"fqtool binary: FASTQ (page cache) -> {mid} -> /dev/null + JSON"
 
 
 def sq_profile(cfg, pairs):
@@ -243,9 +243,10 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
         torch.cuda.empty_cache()
         log(f"FASTQ written in {time.perf_counter() - t0:.1f}s ({cpu_pairs} + {e2e_pairs} pairs)")
         opts = ["-q", "-a", "--detect_pe_adapter", "-g"]
-        if big:
+
+        def e2e(extra):
             tool = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
-            cmd = [tool, "-i", big[0], "-I", big[1], "-o", "/dev/null", "-O", "/dev/null", *opts, "-w", str(workers),
+            cmd = [tool, "-i", big[0], "-I", big[1], "-o", "/dev/null", "-O", "/dev/null", *extra, "-w", str(workers),
                    "-J", os.path.join(tmp, "amd.json"), "-H", os.path.join(tmp, "amd.html")]
             runs = []  # three runs (the copy pipeline's run-to-run spread is wide): the median is reported
             for _ in range(3):
@@ -257,11 +258,16 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
                 runs.append((dt, [l for l in p.stderr.splitlines() if "fqtool-amd:" in l]))
             dt, tool_log = sorted(runs, key=lambda r: r[0])[1]
             gb = (os.path.getsize(big[0]) + os.path.getsize(big[1])) / 1e9
-            out["e2e"] = {"value": round(2 * e2e_pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": e2e_pairs,
-                          "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
-                          "runs_wall_s": [round(r[0], 3) for r in runs],
-                          "path": e2e_path(tool_log),
-                          "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
+            return {"value": round(2 * e2e_pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": e2e_pairs,
+                    "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
+                    "runs_wall_s": [round(r[0], 3) for r in runs], "options": " ".join(extra),
+                    "path": e2e_path(tool_log),
+                    "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
+
+        if big:
+            out["e2e"] = e2e(opts)
+            # BASELINE config 4 (-m): every pair's output is the merged stream (to /dev/null)
+            out["e2e_c4"] = e2e(["-q", "-a", "-g", "--enable_cut_right", "-m", "--merge_output", "/dev/null"])
         ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
         if os.path.exists(ref):
             w = min(16, workers)
@@ -458,7 +464,7 @@ class HipRunner:
     def paths_leg(self, pairs):
         """Off the BASELINE configs: C3's options with explicit adapter sequences (C3b, trimBySequence),
         with UMI (8 + 8), with -c, C4's with -c, and with 1 % of the
-        pairs holding a lowercase base (handed to the general kernel one by one), on the first
+        pairs holding a lowercase base, then an IUPAC code (handed to the general kernel), on the first
         `pairs` pairs of the resident shard; kernel ms per launch from HIP events on the launch
         stream (median of 3 after a warm-up).  Runs after every check: -c rewrites corrected
         bases in place and the lowercase bases are written into the shard."""
@@ -508,6 +514,9 @@ class HipRunner:
         i = torch.arange(0, n, 100, device=self.dev, dtype=torch.int64)
         self.planes[0][(i // abi.TILE_READS) * abi.TILE_READS * STRIDE + (i % abi.TILE_READS) * 16 + 5] = ord("a")
         timed(config_params(abi, "C3"), "c3_lowercase_1pct")
+        # the same pairs with an IUPAC code instead (R: neither ACGTN nor lowercase)
+        self.planes[0][(i // abi.TILE_READS) * abi.TILE_READS * STRIDE + (i % abi.TILE_READS) * 16 + 5] = ord("R")
+        timed(config_params(abi, "C3"), "c3_iupac_1pct")
         return out
 
     def host_legs(self, cpu_pairs, e2e_pairs, workers):
@@ -709,6 +718,7 @@ def run_rank(args):
         "engine": engine,
         "paths": paths,
         "e2e": None,
+        "e2e_c4": None,
         "acc_sha256": acc_digest,
         "parity_sample": sample,
     }
@@ -717,7 +727,9 @@ def run_rank(args):
         legs = runner.host_legs(args.cpu_pairs, args.e2e_pairs, min(16, os.cpu_count() or 1))
         out["cpu_baseline"] = legs["cpu_baseline"]
         out["e2e"] = legs["e2e"]
+        out["e2e_c4"] = legs.get("e2e_c4")
         log(f"e2e {legs['e2e']}")
+        log(f"e2e_c4 {legs.get('e2e_c4')}")
     runner.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

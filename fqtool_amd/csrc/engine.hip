@@ -359,13 +359,37 @@ static int retire_slot(fq_engine* e, int k) {
 
 // a text pack's output is at most its input plus the final line terminator an input may lack
 static const size_t kTextSlack = 16;
+// -m: mate 0's output is the merged stream, at most both mates' input plus a merged name's tag
+// ("_merged_<m1>_<m2>", < 24 bytes) per pair
+static size_t merged_cap(uint64_t text1, uint64_t text2, size_t pairs) {
+    return (size_t)text1 + (size_t)text2 + 24 * pairs + kTextSlack;
+}
+
+// the output text of a text / raw pack: out1 (+ out2), or (-m) the merged stream into mate 0's buffer
+static int launch_text_out(fq_engine* e, Slot& s, int n) {
+    const bool pe = e->p.paired;
+    if (pe && e->p.merge_enabled) {
+        HIP_TRY(e, fq_launch_merge_out(s.d_text[0], s.d_text[1], s.d_trec[0], s.d_trec[1], s.d_res, n, e->p.discard_unmerged,
+                                       s.d_tsize[0], s.d_toff[0], s.d_scan, s.scan_bytes, s.d_out[0], s.d_total, e->stream));
+        HIP_TRY(e, hipMemsetAsync(s.d_total + 1, 0, sizeof(unsigned long long), e->stream));
+        return FQ_OK;
+    }
+    for (int m = 0; m < (pe ? 2 : 1); ++m)
+        HIP_TRY(e, fq_launch_text_out(s.d_text[m], s.d_trec[m], s.d_res, n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
+                                      s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, e->stream));
+    if (!pe) HIP_TRY(e, hipMemsetAsync(s.d_total + 1, 0, sizeof(unsigned long long), e->stream));
+    return FQ_OK;
+}
 
 // device buffers of a text pack (grown on demand; growing frees the old ones, which waits for the
 // device, so steady-state packs of similar size reuse them)
 static int ensure_text(fq_engine* e, Slot& s, const fq_text_batch* tb) {
     const bool pe = e->p.paired;
+    const bool mrg = pe && e->p.merge_enabled;
     for (int m = 0; m < (pe ? 2 : 1); ++m) {
-        const size_t need = tb->text_bytes[m] + kTextSlack;
+        size_t need = tb->text_bytes[m] + kTextSlack;
+        // (-m: mate 0's output buffer takes the merged stream; the sizes go together)
+        if (mrg && m == 0) need = merged_cap(tb->text_bytes[0], tb->text_bytes[1], (size_t)tb->n);
         if (need > s.text_cap[m]) {
             s.raw_ready = false;  // (the raw-window buffers are re-made by ensure_raw)
             if (s.d_text[m]) (void)hipFree(s.d_text[m]);
@@ -487,11 +511,12 @@ int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*
     const bool pe = e->p.paired;
     if (tb->n < 0 || tb->n > e->max_batch || tb->stride <= 0 || tb->stride > e->max_stride || (tb->stride & 15))
         return fail(e, FQ_E_INVALID, "text pack exceeds the engine's max_batch/max_stride (or stride % 16 != 0)");
-    if (e->p.merge_enabled || e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0)
-        return fail(e, FQ_E_INVALID, "text packs take no -m, -c or UMI options");
+    if (e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0)
+        return fail(e, FQ_E_INVALID, "text packs take no -c or UMI options");
     for (int m = 0; m < (pe ? 2 : 1); ++m)
         if (tb->n > 0 && (!tb->text[m] || !tb->rec[m] || !out->text[m]))
             return fail(e, FQ_E_INVALID, "missing text pack arrays");
+    const bool mrg = pe && e->p.merge_enabled;
     out->bytes[0] = out->bytes[1] = 0;
     if (tb->n == 0) {
         e->pending.push_back(Pending{seq_no, -1, true, 0});
@@ -534,10 +559,7 @@ int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*
                                         e->stream));
     HIP_TRY(e, hipMemsetAsync(s.d_err, 0, sizeof(int), e->stream));
     if ((rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false, seq_no, s.d_err)) != FQ_OK) return rc;
-    for (int m = 0; m < (pe ? 2 : 1); ++m)
-        HIP_TRY(e, fq_launch_text_out(s.d_text[m], s.d_trec[m], s.d_res, tb->n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
-                                      s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, e->stream));
-    if (!pe) HIP_TRY(e, hipMemsetAsync(s.d_total + 1, 0, sizeof(unsigned long long), e->stream));
+    if ((rc = launch_text_out(e, s, tb->n)) != FQ_OK) return rc;
     HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
     // D2H: records, output sizes and text (the text up to its input span: an upper bound of the
     // output, no device-to-host round trip for the exact size), the error word
@@ -545,8 +567,10 @@ int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*
     const size_t nres = (size_t)tb->n * (pe ? 2 : 1);
     HIP_TRY(e, hipMemcpyAsync(results, s.d_res, nres * sizeof(fq_read_result), hipMemcpyDeviceToHost, e->s_out));
     HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
-    for (int m = 0; m < (pe ? 2 : 1); ++m)
-        HIP_TRY(e, hipMemcpyAsync(out->text[m], s.d_out[m], tb->text_bytes[m] + kTextSlack, hipMemcpyDeviceToHost, e->s_out));
+    for (int m = 0; m < (mrg ? 1 : pe ? 2 : 1); ++m) {
+        const size_t back = mrg ? merged_cap(tb->text_bytes[0], tb->text_bytes[1], (size_t)tb->n) : tb->text_bytes[m] + kTextSlack;
+        HIP_TRY(e, hipMemcpyAsync(out->text[m], s.d_out[m], back, hipMemcpyDeviceToHost, e->s_out));
+    }
     HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
     HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
     s.busy = true;
@@ -582,7 +606,9 @@ static int ensure_raw(fq_engine* e, Slot& s) {
         s.d_ad[m] = nullptr;
         if (m == 1 && !pe) continue;
         HIP_TRY(e, hipMalloc(&s.d_text[m], text));
-        HIP_TRY(e, hipMalloc(&s.d_out[m], text + 4 * recs + 64));  // (+ the adapter entries' slack)
+        // (+ the adapter entries' slack; -m: mate 0's takes the merged stream of both mates' text)
+        const size_t out = pe && m == 0 && e->p.merge_enabled ? merged_cap(text, text, recs) + 3 * recs + 64 : text + 4 * recs + 64;
+        HIP_TRY(e, hipMalloc(&s.d_out[m], out));
         HIP_TRY(e, hipMalloc(&s.d_trec[m], recs * sizeof(fq_text_rec)));
         HIP_TRY(e, hipMalloc(&s.d_tsize[m], recs * sizeof(uint32_t)));
         HIP_TRY(e, hipMalloc(&s.d_toff[m], recs * sizeof(uint32_t)));
@@ -608,8 +634,8 @@ static int ensure_raw(fq_engine* e, Slot& s) {
 int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap) {
     if (!e) return FQ_E_INVALID;
     if (!e->pending.empty() || !e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_begin with packs in flight");
-    if (e->p.merge_enabled || e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0)
-        return fail(e, FQ_E_INVALID, "raw streams take no -m, -c or UMI options");
+    if (e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0)
+        return fail(e, FQ_E_INVALID, "raw streams take no -c or UMI options");
     carry_cap = (carry_cap + 4095) / 4096 * 4096;
     if (!window_cap || carry_cap + window_cap + 4096 >= (1ull << 31) || e->max_batch <= 0)
         return fail(e, FQ_E_INVALID, "raw window / carry capacity out of range");
@@ -725,11 +751,13 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     HIP_TRY(e, hipMemsetAsync(s.d_total, 0, 4 * sizeof(unsigned long long), e->stream));
     // each mate's copy back: its output text (<= the input it spans) and the adapter entries after
     // it (per record, output + entry <= input + 3 bytes)
+    // (-m: mate 0's output is the merged stream, mate 1's is empty: only its adapter entries)
+    const bool mrg = pe && e->p.merge_enabled;
     size_t back[2] = {0, 0};
     for (int m = 0; m < mates; ++m) back[m] = (size_t)r->text_bytes[m] + kTextSlack + 3 * (size_t)n;
+    if (mrg) back[0] = merged_cap(r->text_bytes[0], r->text_bytes[1], (size_t)n) + 3 * (size_t)n;
+    if ((rc = launch_text_out(e, s, n)) != FQ_OK) return rc;
     for (int m = 0; m < mates; ++m) {
-        HIP_TRY(e, fq_launch_text_out(s.d_text[m], s.d_trec[m], s.d_res, n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
-                                      s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, e->stream));
         if (e->p.adapter_trimming)
             HIP_TRY(e, fq_launch_raw_adapters(s.d_text[m], s.d_trec[m], s.d_res, n, pe ? 1 : 0, m, s.d_tsize[m], s.d_toff[m],
                                               s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, back[m], s.d_total + 2 + m,

@@ -42,6 +42,11 @@ size_t fq_text_scan_temp_bytes(int n);
 hipError_t fq_launch_text_out(const char* d_text, const fq_text_rec* d_rec, const fq_read_result* d_res, int n, int paired,
                               int m, uint32_t* d_size, uint32_t* d_off, void* d_temp, size_t temp_bytes, char* d_out,
                               unsigned long long* d_total, hipStream_t s);
+// -m: the merged output stream of a PE text pack (text.hip), into d_out (mate 0's output)
+hipError_t fq_launch_merge_out(const char* d_text1, const char* d_text2, const fq_text_rec* d_rec1,
+                               const fq_text_rec* d_rec2, const fq_read_result* d_res, int n, int discard,
+                               uint32_t* d_size, uint32_t* d_off, void* d_temp, size_t temp_bytes, char* d_out,
+                               unsigned long long* d_total, hipStream_t s);
 // Raw FASTQ streams (raw.hip): per (window, mate) device state of the record indexing
 struct fq_raw_state {
     uint32_t text_start;  // buffer offset of the window's text (the carried bytes first)
