@@ -511,8 +511,9 @@ int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*
     const bool pe = e->p.paired;
     if (tb->n < 0 || tb->n > e->max_batch || tb->stride <= 0 || tb->stride > e->max_stride || (tb->stride & 15))
         return fail(e, FQ_E_INVALID, "text pack exceeds the engine's max_batch/max_stride (or stride % 16 != 0)");
-    if (e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0)
-        return fail(e, FQ_E_INVALID, "text packs take no -c or UMI options");
+    if (e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0 ||
+        (e->p.merge_enabled && e->p.discard_unmerged))
+        return fail(e, FQ_E_INVALID, "text packs take no -c, UMI or --discard_unmerged options");
     for (int m = 0; m < (pe ? 2 : 1); ++m)
         if (tb->n > 0 && (!tb->text[m] || !tb->rec[m] || !out->text[m]))
             return fail(e, FQ_E_INVALID, "missing text pack arrays");
@@ -634,8 +635,9 @@ static int ensure_raw(fq_engine* e, Slot& s) {
 int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap) {
     if (!e) return FQ_E_INVALID;
     if (!e->pending.empty() || !e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_begin with packs in flight");
-    if (e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0)
-        return fail(e, FQ_E_INVALID, "raw streams take no -c or UMI options");
+    if (e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0 ||
+        (e->p.merge_enabled && e->p.discard_unmerged))
+        return fail(e, FQ_E_INVALID, "raw streams take no -c, UMI or --discard_unmerged options");
     carry_cap = (carry_cap + 4095) / 4096 * 4096;
     if (!window_cap || carry_cap + window_cap + 4096 >= (1ull << 31) || e->max_batch <= 0)
         return fail(e, FQ_E_INVALID, "raw window / carry capacity out of range");

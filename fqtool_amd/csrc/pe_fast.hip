@@ -142,12 +142,16 @@ constexpr int kSlots = 6;
 constexpr int kDummySlot = 5;
 constexpr int kHistW = kChunks * kSlots * 32;
 __host__ __device__ constexpr int cell(int c, int slot) { return ((c >> 4) * kSlots + slot) * 32 + 2 * (c & 15); }
-// Removed-mode Stats rows: [cycle / 16][13 slots][cycle % 16] u64 cells per mate, slot =
-// 4 * kept + code for A C T G (codes 0-3), 8 + 4 * kept for N (the G slot + 5, so an N is one
-// nibble add away from the G that its code 3 reads as), 10 for positions beyond the read.
+// Removed-mode Stats rows: [cycle / 16][13 slots][mate][cycle % 16] u64 cells, slot = 4 * kept +
+// code for A C T G (codes 0-3), 8 + 4 * kept for N (the G slot + 5, so an N is one nibble add away
+// from the G that its code 3 reads as), 10 for positions beyond the read.  The mates' rows
+// interleave, so a cell's byte address is base | slot << 8 | mate << 7 | (cycle % 16) << 3 plus the
+// chunk's (wave-uniform) offset: the slot nibble goes in with one bit operation (statRead below).
 constexpr int kRSlots = 13;
 constexpr int kRNSlot = 8;   // removed N; kept N = kRNSlot + 4
-__host__ __device__ constexpr int rcell(int c, int slot) { return ((c >> 4) * kRSlots + slot) * 32 + 2 * (c & 15); }
+__host__ __device__ constexpr int rcell(int c, int slot) { return ((c >> 4) * kRSlots + slot) * 64 + 2 * (c & 15); }
+// read 2's merged parts (Layout::kMrgW): [cycle / 16][8 slot rows, A C T G N dummy + 2 unused][cycle % 16]
+__host__ __device__ constexpr int mcell(int c, int slot) { return ((c >> 4) * 8 + slot) * 32 + 2 * (c & 15); }
 constexpr int kRemW = 2 * kRSlots * 32 * kChunks;  // both mates' removed-mode rows
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int kSmallU64 = FQ_ACC_INSERT;                 // FilterResult / adapter / polyX / merged counters
@@ -186,10 +190,13 @@ struct Layout {
     // [pre1, pre2, post1 (x2 with MERGE), post2] (+ MERGE: read 2's merged parts, cycles 0..319,
     // in removed mode, which uses blocks 0-3 as the kept/removed rows of the two mates)
     static constexpr int kHists = MERGE ? 6 : 4;
-    static constexpr int kXtraW = MERGE ? kSlots * 32 : 0;  // one more cycle row: dummy positions up to 335
+    // read 2's merged parts (removed mode): cycle rows of 8 slot rows (mcell), cycles < 2 kMaxLen + 16
+    // (the last row: dummy positions past the part); 1 KiB-aligned, so a cell's byte address is
+    // row base | slot << 7 | (cycle % 16) << 3
+    static constexpr int kMrgW = MERGE ? (2 * kChunks + 1) * 8 * 32 : 0;
     // removed mode: both mates' kept/removed rows first, then (MERGE) read 2's merged parts
-    static constexpr int kMrgOff = cmax(4 * kHistW, kRemW);
-    static constexpr int kHistRegW = cmax(kHists * kHistW, MERGE ? kMrgOff + 2 * kHistW : kRemW) + kXtraW;
+    static constexpr int kMrgOff = (cmax(4 * kHistW, kRemW) + 255) & ~255;
+    static constexpr int kHistRegW = cmax(kHists * kHistW, MERGE ? kMrgOff + kMrgW : kRemW);
     static constexpr int kColsW = kWaves * kWaveW;
     static constexpr int kScalCopies = MERGE ? 8 : 16;
     static constexpr int kScalW = 2 * kScalStride * kScalCopies;
@@ -300,8 +307,10 @@ struct CodeSeq {  // forward base byte i rebuilt from the codes (alphabet A C G 
         uint32_t code = (col[(kFC + w) * 64 + c] >> sh) & 3u;
         const uint32_t nx = col[(kFN + w) * 64 + c] >> sh;  // bit 0: N, bit 1: lowercase
         code ^= rc ? 2u : 0u;
-        // "ACTG", lowercase with the flag (its code is its uppercase letter's, never N)
-        return (nx & 1u) ? (uint8_t)'N' : (uint8_t)(((0x47544341u >> (8 * code)) & 0xFFu) | ((nx & 2u) << 4));
+        // "ACTG", lowercase with the flag (its code is its uppercase letter's, never N); an exotic
+        // byte (N bit and flag) as 0x01, which equals no letter and no 'N' (lower_flags)
+        if (nx & 1u) return (nx & 2u) ? (uint8_t)1 : (uint8_t)'N';
+        return (uint8_t)(((0x47544341u >> (8 * code)) & 0xFFu) | ((nx & 2u) << 4));
     }
 };
 
@@ -349,6 +358,14 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
     return D < limit || ol > 50;
 }
 
+// (acc << 1) | (t >> 31): a flag bit shifted in from the sign of t, one v_alignbit.  Bit-flag words
+// built this way need no per-bit constant (a cmp / cndmask / or chain keeps every 1 << r in a VGPR).
+__device__ __forceinline__ uint32_t shift_in_sign(uint32_t acc, uint32_t t) {
+    uint32_t r;
+    asm("v_alignbit_b32 %0, %1, %2, 31" : "=v"(r) : "v"(acc), "v"(t));
+    return r;
+}
+
 // Scan one phase: offsets k = k0 .. cnt-1 move a 16-position window of column `cm` starting at
 // code position mpos0 + k against the fixed 16-position word `fixed`; returns the first offset
 // whose code-level lower bound is < K (or -1).  ol(k) = min(olA - k, olB).  With FIXED_MASK the
@@ -383,9 +400,9 @@ __device__ inline int ov_scan(const uint32_t* col, int cm, int mpos0, int k0, in
 #pragma unroll
         for (int r = 1; r < 16; r += 2) mn = min(mn, min(lb[r], r + 1 < 16 ? lb[r + 1] : lb[r]));
         if (mn < K) {
-            uint32_t bits = 0;
+            uint32_t bits = (uint32_t)(lb[15] - K) >> 31;  // bit r: lb[r] < K
 #pragma unroll
-            for (int r = 0; r < 16; ++r) bits |= (uint32_t)(lb[r] < K) << r;
+            for (int r = 14; r >= 0; --r) bits = shift_in_sign(bits, (uint32_t)(lb[r] - K));
             // keep offsets within [k, cnt)
             const int first_r = P & 15;
             bits &= ~((1u << first_r) - 1u);
@@ -738,12 +755,12 @@ __device__ inline bool cut_right_w4(const fq_params& p, const uint8_t* Q, int nc
             const uint4 q1 = *reinterpret_cast<const uint4*>(Q + cst * c);
             const uint4 q2 = c + 1 < nchunks ? *reinterpret_cast<const uint4*>(Q + cst * (c + 1)) : z;
             const uint32_t d[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-            uint32_t win = 0;  // bit j: the window starting at 16c - 3 + j is low
+            uint32_t win = 0;  // bit j: the window starting at 16c - 3 + j is low (sum < TW)
 #pragma unroll
-            for (int j = 0; j < 19; ++j) {
+            for (int j = 18; j >= 0; --j) {
                 const int o = 13 + j;  // its byte offset in d
                 const uint32_t W = (o & 3) ? __builtin_amdgcn_alignbyte(d[(o >> 2) + 1], d[o >> 2], o & 3) : d[o >> 2];
-                win |= (__builtin_amdgcn_sad_u8(W & wm, 0u, 0u) < TW ? 1u : 0u) << j;
+                win = shift_in_sign(win, __builtin_amdgcn_sad_u8(W & wm, 0u, 0u) - TW);
             }
             const int lo = a - (16 * c - 3), hi = bnd - (16 * c - 3);  // 0 <= lo < hi <= 19
             win &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
@@ -767,20 +784,30 @@ __device__ inline bool cut_right_w4(const fq_params& p, const uint8_t* Q, int nc
     return true;
 }
 
-// (rare) the lowercase flags of one lane's read: re-reads its row chunks, ORs a flag at the odd bit
-// of the N word for each lowercase a c g t (the uppercase letter | 0x20, whose 3-bit key and code
-// are the uppercase letter's) and returns true when the read holds any other byte outside ACGTN.
-// xp: the lane's column word of row chunk 0 (read 2: its reverse complement, stepped by wstep).
+// (rare) the flags of one lane's read that holds a byte outside ACGTN: re-reads its row chunks and
+// marks, in the column,
+//   * a lowercase a c g t (the uppercase letter | 0x20, whose 3-bit key and code are the uppercase
+//     letter's): a flag at the odd bit of the N word;
+//   * any other byte ("exotic": IUPAC codes, 'n', ...): code 3 with the N bit and the odd bit, so
+//     the comparing passes see a byte that equals nothing in read 1 and reads as 'N' in read 2's
+//     reverse complement (src/seq.h:24-48), and Stats counts it as N until its fix-up moves it to
+//     its class byte & 7 (src/stats.cpp:249).  passFilter counts only 'N' (src/filter.cpp:18):
+//     staging counted an exotic byte with key bit 2 as one, so it is taken off the prefix words (pfx:
+//     the lane's first prefix word, or null; step: chunks per word) and, by the caller, off nbf.
+// Returns bit 0 (hand the pair over: exotic bytes where they are not taken, allow_exotic false),
+// bit 1 (the read holds exotic bytes) and, from bit 2 on, the count staging took for 'N's.  xp: the lane's column word of row chunk 0 (read 2: its
+// reverse complement, stepped by wstep).
 template <bool PAIRED>
-__device__ __attribute__((noinline)) bool lower_flags(const uint8_t* S, uint32_t* xp, int wstep, int nch, int L, bool rc,
-                                                     uint32_t rsel) {
+__device__ __attribute__((noinline)) int lower_flags(const uint8_t* S, uint32_t* xp, int wstep, int nch, int L, bool rc,
+                                                    uint32_t rsel, uint32_t* pfx, int step, bool allow_exotic) {
     constexpr int cst = FQ_TILE_READS * FQ_CHUNK;
-    bool hard = false;
+    bool exotic = false;
+    int ntot = 0;
     for (int k = 0; k < nch; ++k, xp += wstep) {
         const uint4 s4 = *reinterpret_cast<const uint4*>(S + cst * k);
         const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
         const int Lk = L - 16 * k;
-        uint32_t x4 = 0;
+        uint32_t x4 = 0, e4 = 0, ncnt = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t sr = PAIRED ? __builtin_amdgcn_perm(sw[3 - j], sw[j], rsel) : sw[j];
@@ -792,13 +819,23 @@ __device__ __attribute__((noinline)) bool lower_flags(const uint8_t* S, uint32_t
             const uint32_t low = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & ~((kk & 0x04040404u) << 5) &
                                  0x80808080u;  // d == 0x20 and not 'n' (whose key is N's)
             const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
-            hard |= (nz & ~low) != 0u;
+            const uint32_t ex = nz & ~low;
+            ncnt += __popc(ex & ((kk & 0x04040404u) << 5));  // (staging's N flag: key bit 2)
             x4 |= (low >> 7) << (2 * j);
+            e4 |= (ex >> 7) << (2 * j);
         }
         const uint32_t vm = rc ? 0x55555555u & ~posmask(16 - Lk) : posmask(Lk);
-        xp[kFN * 64] |= (tr4x4(x4) & vm) << 1;
+        const uint32_t ef = tr4x4(e4) & vm;
+        xp[kFN * 64] |= ((tr4x4(x4) & vm) << 1) | ef | (ef << 1);
+        if (ef) {
+            exotic = true;
+            xp[kFC * 64] |= ef | (ef << 1);  // code 3
+            ntot += (int)ncnt;
+            if (pfx)
+                for (int j = k / step; (j + 1) * step <= nch; ++j) pfx[j * 64] -= ncnt << 24;
+        }
     }
-    return hard;
+    return (exotic && !allow_exotic ? 1 : 0) | (exotic ? 2 : 0) | ntot << 2;
 }
 
 __device__ __forceinline__ void sadd(unsigned long long* p, unsigned long long v) { atomicAdd(p, v); }
@@ -1111,7 +1148,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                          (MERGE && L + xor32(L) > p.max_cycles);
         uint32_t exo = 0, qhi = 0, q20 = 0, q30 = 0, lowf = 0, tqf = 0, nbf = 0;  // whole-read sums
         const uint32_t k80 = vk(0x80808080u), limq_v = vk(limq);  // (VGPR operands: full-rate VALU)
-        uint32_t lowr = 0;  // FULL with cut_right: bit k = chunk k holds a quality below its threshold
+        // FULL with cut_right: bit k = chunk k holds a quality below its threshold (shifted in from
+        // the top chunk by chunk, reversed after staging)
+        uint32_t lowr = 0;
         // column word of chunk k: k for read 1, 9-k for read 2 (stepped, not precomputed, so the
         // ten addresses are not kept live across tiles)
         uint32_t* wp = col + lane_x + (rc ? (kChunks - 1) * 64 : 0);
@@ -1209,7 +1248,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 #pragma unroll
                     for (int j = 0; j < 4; ++j) dword(j, std::false_type{});
                 }
-                if (!LEAN) lowr |= (lr != 0 ? 1u : 0u) << k;
+                if (!LEAN) lowr = shift_in_sign(lowr, lr | (0u - lr));  // (sign set iff lr != 0)
                 // N flags are kept only for positions inside the read (later passes rely on it);
                 // read 2's chunk is reversed: its positions inside the read are the high ones
                 const uint32_t vmask = full ? 0x55555555u : rc ? 0x55555555u & ~posmask(16 - Lk) : posmask(Lk);
@@ -1241,10 +1280,25 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
         // uppercase letter's (src/stats.cpp:249) and passFilter counts only 'N' (src/filter.cpp:18),
         // so those passes need nothing.  Any other byte outside ACGTN hands the pair over.  Rare: only
         // lanes holding such a byte re-read their row (from L2) here.
-        bool hard = false, xl = false;
+        if (!LEAN) lowr = nch > 0 ? __builtin_bitreverse32(lowr) >> (32 - nch) : 0u;  // chunk k to bit k
+        bool hard = false, xl = false, xe = false;
         if (__any(exo != 0)) {
             if (exo != 0) {
-                hard = lower_flags<PAIRED>(S, col + lane_x + (rc ? (kChunks - 1) * 64 : 0), wstep, nch, L, rc, rsel);
+                // exotic bytes stay here unless the passes that compare them as bytes need more
+                // than "equals nothing": the low-complexity filter (two exotic bytes may be equal),
+                // the merged read (read 2's exotic bytes become N inside it), -c, or an adapter
+                // sequence holding such a byte
+                bool ad_ok = true;
+                for (int i = 0; i < my_alen; ++i) {
+                    const uint32_t a = my_ad[i] & 0xDFu;
+                    ad_ok = ad_ok && (a == 'A' || a == 'C' || a == 'G' || a == 'T' || my_ad[i] == 'N');
+                }
+                const bool allow = !MERGE && !p.complexity_enabled && ad_ok;
+                const int lf = lower_flags<PAIRED>(S, col + lane_x + (rc ? (kChunks - 1) * 64 : 0), wstep, nch, L, rc, rsel,
+                                                   LY::kPfx ? col + kCodeW + lane_x : nullptr, LY::kPfxStep, allow);
+                hard = (lf & 1) != 0;
+                xe = (lf & 2) != 0;
+                nbf -= (uint32_t)(lf >> 2);
                 // (-c rewrites bases across the pair: its pairs with lowercase go over)
                 if (XTRA && p.correction_enabled) hard = true;
                 xl = !hard;
@@ -1493,7 +1547,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     corr = correct_pair_fast(p, col, lds, b, roff, mate, lane_x, mlane, mate ? st_o : st, mate ? st : st_o, n2,
                                       ov, Q, rr, q20, q30, lowf, tqf, nbf, limq,
                                       scal + kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate + 1,
-                                      removed_mode ? LY::kColsW + mate * (kRSlots * 32 * kChunks) : LY::kColsW + mate * kHistW,
+                                      removed_mode ? LY::kColsW + mate * 32 : LY::kColsW + mate * kHistW,
                                       removed_mode, acc);
                 }
             }
@@ -1585,8 +1639,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     cl += __popc(~(qm + limq_v) & m80);
                 }
                 // N bits of the chunk's first nbytes positions (read 2's column is reversed)
+                // (an exotic byte's N bit comes with its flag: not an 'N')
                 const uint32_t nw = col[(kFN + (rc ? kChunks - 1 - F : F)) * 64 + lane_x];
-                const uint32_t cn = __popc(nw & (rc ? 0x55555555u & ~posmask(16 - nbytes) : posmask(nbytes)));
+                const uint32_t cn = __popc(nw & ~(nw >> 1) & (rc ? 0x55555555u & ~posmask(16 - nbytes) : posmask(nbytes)));
                 return c20 | c30 << 8 | cl << 16 | cn << 24;
             };
             // counts of forward positions [0, x): the prefix word through chunk (c / step) * step - 1,
@@ -1697,7 +1752,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     const int s0 = rc ? kMaxLen - a1 : a0, s1 = rc ? kMaxLen - a0 : a1;
                     for (int c = s0 >> 4; c < ((s1 + 15) >> 4); ++c) {
                         const uint32_t w = col[(kFN + c) * 64 + lane_x];
-                        nb -= __popc(w & posmask(s1 - 16 * c) & ~posmask(s0 - 16 * c));
+                        nb -= __popc(w & ~(w >> 1) & posmask(s1 - 16 * c) & ~posmask(s0 - 16 * c));
                     }
                 }
                 if (direct) {
@@ -1785,6 +1840,41 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 
         FQ_STAMP(5)
         if (tile_x) {  // (rare) the lowercase flags have served: the Stats passes read spaced N masks
+            if (!MERGE && xe && valid && !(abl & 4)) {
+                // exotic bytes: the passes below count them as N (class 6, code 3 + N bit); move each
+                // to its class byte & 7 (src/stats.cpp:249) in the pre block and, inside the post
+                // window, the post block, straight in the global accumulator (rare).  The row's
+                // address is re-derived here (S itself is not kept live this far).
+                const size_t sb = acc_stats_offset(p.insert_size_max, p.max_cycles, 0);
+                const size_t sw = acc_stats_words(p.max_cycles);
+                constexpr int cst = FQ_TILE_READS * FQ_CHUNK;
+                int ix = idx;
+                asm volatile("" : "+v"(ix));
+                const uint8_t* Sx = (mate ? b.seq2 : b.seq1) + (size_t)(ix / FQ_TILE_READS) * FQ_TILE_READS * b.stride +
+                                    (ix % FQ_TILE_READS) * FQ_CHUNK;
+                for (int c = 0; c < kChunks; ++c) {
+                    const uint32_t w = col[(kFN + c) * 64 + lane_x];
+                    uint32_t ex = w & (w >> 1) & 0x55555555u;
+                    while (ex) {
+                        const int t = (__ffs(ex) - 1) >> 1;
+                        ex &= ex - 1u;
+                        const int q = 16 * c + t, P = rc ? kMaxLen - 1 - q : q;
+                        const int off = cst * (P >> 4) + (P & 15);
+                        const int cls = Sx[off] & 7;
+                        if (cls == 6) continue;
+                        const unsigned long long qv = (unsigned long long)(Q[off] - 33);
+                        auto move = [&](int k, int cyc) {
+                            unsigned long long* dst = acc + sb + (size_t)k * sw + FQ_ST_CYCLES + (size_t)cyc * FQ_ST_PER_CYCLE;
+                            atomicAdd(&dst[6], ~0ull);
+                            atomicAdd(&dst[8 + 6], 0ull - qv);
+                            atomicAdd(&dst[cls], 1ull);
+                            atomicAdd(&dst[8 + cls], qv);
+                        };
+                        move(mate, P);
+                        if (post_on && P >= ws && P < ws + wn) move(2 + mate, P - ws);
+                    }
+                }
+            }
             if (xl)
                 for (int c = 0; c < kChunks; ++c) col[(kFN + c) * 64 + lane_x] &= 0x55555555u;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1792,6 +1882,19 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         // ---------------- Stats::statRead, pre and post (src/peprocessor.cpp:276-277,400-401) ----
+        if (valid && !(abl & 4)) {
+            // per-read Stats scalars: (reads, length_sum) packed as count << 32 | sum, plus
+            // q20 << 32 | q30, into one of 16 LDS copies (lanes l, l + 16 share one); first, so
+            // that none of these values stays live through the passes below
+            unsigned long long* sc = scal + kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate;
+            sadd(&sc[0], (1ull << 32) | (unsigned long long)L);
+            sadd(&sc[1], ((unsigned long long)q20 << 32) | q30);
+            const bool post_here = (MERGE && merged) ? (post_on && mate == 0) : post_on;
+            if (post_here) {
+                sadd(&sc[8], (1ull << 32) | (unsigned long long)((MERGE && merged) ? mlen : n));
+                sadd(&sc[9], ((unsigned long long)w20 << 32) | w30);
+            }
+        }
         if (valid && !(abl & 4) && removed_mode) {
             // Every kept window is a prefix [0, wlen): each base goes to exactly one cell, kept or
             // removed (pre = kept + removed at the flush), one LDS atomic per base.  Per chunk the
@@ -1802,14 +1905,17 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             const int wlen = post_on && !(MERGE && merged && mate) ? wn : 0;
             const int dsel = r >> 2, rr4 = 4 * (r & 7);
             const bool rswap = r >= 8;
-            // LDS byte address of rotated position t's cell in slot 0 of chunk 0 (this mate's rows)
+            // LDS byte address of rotated position t's cell in slot 0 of chunk 0 (this mate's rows):
+            // bits 8-11 are clear, the slot nibble is or-ed in (rcell)
+            static_assert((LY::kColsW * 4) % 4096 == 0, "removed-mode rows: 4 KiB aligned");
             uint32_t rwb[16];
-            const uint32_t blk0 = (uint32_t)(LY::kColsW + mate * (kRSlots * 32 * kChunks)) * 4u;
+            const uint32_t blk0 = (uint32_t)(LY::kColsW + mate * 32) * 4u;
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 rwb[t] = blk0 + 8u * (uint32_t)((t + r) & 15);
                 asm volatile("" : "+v"(rwb[t]));  // kept whole (not re-split into base + offset per use)
             }
+            const uint32_t slot_m = vk(0xF00u);
             // quality chunks rotate through kSA + 1 registers (requested kSA chunks ahead)
             constexpr int kSA = FQ_STATS_AHEAD;
             uint4 qb[kSA + 1];
@@ -1852,9 +1958,13 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     // N bases: their slot kRNSlot + 4 * kept is the G slot + 5, one nibble add (staging
                     // kept N flags only inside the read)
                     if (__any(f.n != 0)) {
+                        // (n0 nibbles are 0 or 1: n0 | n0 << 2 is 5 n0, one v_lshl_or)
                         const uint32_t n0 = spread2to4(f.n), n1 = spread2to4(f.n >> 16);
-                        lo += n0 + (n0 << 2);
-                        hi += n1 + (n1 << 2);
+                        uint32_t n05, n15;
+                        asm("v_lshl_or_b32 %0, %1, 2, %1" : "=v"(n05) : "v"(n0));
+                        asm("v_lshl_or_b32 %0, %1, 2, %1" : "=v"(n15) : "v"(n1));
+                        lo += n05;
+                        hi += n15;
                     }
 #endif
                     if (__any(vl < 16)) {  // positions beyond the read (kept is 0 there) -> dummy slot 10
@@ -1874,11 +1984,11 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                             nv &= nv - 1;
                             const int kept = 16 * F + t < wlen ? 1 : 0;
                             const unsigned long long v = kCount1 | (unsigned long long)__builtin_amdgcn_ubfe(qs[t >> 2], 8 * (t & 3), 8);
-                            const uint32_t a = (uint32_t)(LY::kColsW + mate * (kRSlots * 32 * kChunks)) * 4u +
-                                               (uint32_t)(F * kRSlots * 32 * 4) + 8u * (uint32_t)t;
-                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(kRNSlot + 4 * kept) * 128u)), v,
+                            const uint32_t a = (uint32_t)(LY::kColsW + mate * 32) * 4u +
+                                               (uint32_t)(F * kRSlots * 64 * 4) + 8u * (uint32_t)t;
+                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(kRNSlot + 4 * kept) * 256u)), v,
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(4 * kept + 3) * 128u)), 0ull - v,
+                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + (uint32_t)(4 * kept + 3) * 256u)), 0ull - v,
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     }
@@ -1893,13 +2003,22 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     // quality bytes (< 128 here): the low word of a cell increment
                     const uint32_t qr[4] = {__builtin_amdgcn_alignbyte(a1, a0, r & 3), __builtin_amdgcn_alignbyte(a2, a1, r & 3),
                                             __builtin_amdgcn_alignbyte(a3, a2, r & 3), __builtin_amdgcn_alignbyte(a0, a3, r & 3)};
+                    // slot nibble t % 8 at bits 8-11: a right shift of the word (nibbles 2-7) or of the
+                    // word shifted left by 8 (nibbles 0-1; one 64-bit shift gives both words' copies,
+                    // the high one with klo's top byte in its low bits, masked off)
+                    const unsigned long long k8 = ((unsigned long long)khi << 32 | klo) << 8;
+                    const uint32_t klo8 = (uint32_t)k8, khi8 = (uint32_t)(k8 >> 32);
 #pragma unroll
                     for (int t = 0; t < 16; ++t) {
-                        const uint32_t ks = __builtin_amdgcn_ubfe(t < 8 ? klo : khi, 4 * (t & 7), 4);
-                        const uint32_t qv = __builtin_amdgcn_ubfe(qr[t >> 2], 8 * (t & 3), 8);
-                        uint32_t a;  // (ks << 7) + rwb[t] in one instruction
-                        asm("v_lshl_add_u32 %0, %1, 7, %2" : "=v"(a) : "v"(ks), "v"(rwb[t]));
-                        a += (uint32_t)(F * kRSlots * 32 * 4);  // (folds into the ds offset)
+                        const int u = t & 7;
+                        const uint32_t kw = u < 2 ? (t < 8 ? klo8 : khi8) : (t < 8 ? klo : khi);
+                        const uint32_t ksh = u < 2 ? kw >> (4 * u) : kw >> (4 * (u - 2));
+                        // (byte 0 and 3 by one full-rate op, 1 and 2 by a bit-field extract)
+                        const uint32_t qw = qr[t >> 2];
+                        const uint32_t qv = (t & 3) == 0 ? qw & 0xFFu : (t & 3) == 3 ? qw >> 24 : __builtin_amdgcn_ubfe(qw, 8 * (t & 3), 8);
+                        uint32_t a;  // rwb[t] | (ksh & 0xF00): one v_bitop3
+                        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xEA" : "=v"(a) : "v"(ksh), "v"(slot_m), "v"(rwb[t]));
+                        a += (uint32_t)(F * kRSlots * 64 * 4);  // (folds into the ds offset)
                         __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)a), kCount1 | (unsigned long long)qv,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
@@ -1921,12 +2040,16 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             const int c2 = lane_x | 32;  // read 2's column
             const int pos_hi = ws2 + m2 - 1;
             const int ci0 = kMaxLen - 1 - pos_hi;
+            // byte address of merged cycle m1 + 16 J + t's slot-0 cell (mcell), for this lane's next J
+            static_assert((LY::kColsW + LY::kMrgOff) % 256 == 0, "merged-part rows: 1 KiB aligned");
             uint32_t rb[16];
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
-                const int c = m1 + t;
-                rb[t] = xb + (uint32_t)((((c >> 4) * kSlots) * 32 + 2 * (c & 15)) * 4);
+                const int c = m1 + t + 16 * mate;
+                rb[t] = xb + (uint32_t)((c >> 4) << 10 | (c & 15) << 3);
+                asm volatile("" : "+v"(rb[t]));
             }
+            const uint32_t mslot_m = vk(0x380u);
             // quality dwords of forward positions [hi - 15, hi], hi = pos_hi - 16J: words
             // wl0 - 4J .. wl0 - 4J + 4; the lane's next group (J + 2) is requested one group ahead
             const int wl0 = (pos_hi - 15) >> 2, sh = (pos_hi - 15) & 3;  // (negative only for dummies)
@@ -1946,12 +2069,15 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 uint32_t qn[5];
 #pragma unroll
                 for (int i = 0; i < 5; ++i) qn[i] = qword(wl0 - 4 * (J + 2) + i);
-                // qualities ascending in qa[0..3], then reversed: qrev[k] byte b = merged t = 4k + b
-                uint32_t qa[4], qrev[4];
+                // qualities ascending in qa[0..3]: merged t is byte 3 - t % 4 of qa[3 - t / 4]
+                uint32_t qa[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) qa[i] = __builtin_amdgcn_alignbyte(qw5[i + 1], qw5[i], sh);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) qrev[i] = __builtin_amdgcn_perm(0u, qa[3 - i], 0x00010203u);
+                auto qbyte = [&](int t) -> uint32_t {  // (bytes 0 and 3 by one full-rate op)
+                    const uint32_t qw = qa[3 - (t >> 2)];
+                    const int bs = 3 - (t & 3);
+                    return bs == 0 ? qw & 0xFFu : bs == 3 ? qw >> 24 : __builtin_amdgcn_ubfe(qw, 8 * bs, 8);
+                };
                 // slot nibbles: code, or the dummy slot beyond the part
                 const int rem = m2 - 16 * J;
                 const unsigned long long dm = ~0ull << min(4 * max(rem, 0), 63);
@@ -1959,13 +2085,17 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 const uint32_t dlo = (uint32_t)dm, dhi = rem >= 16 ? 0u : (uint32_t)(dm >> 32);
                 nlo = (nlo & ~dlo) | (dlo & 0x55555555u);  // 5 = kDummySlot
                 nhi = (nhi & ~dhi) | (dhi & 0x55555555u);
-                const uint32_t jb = (uint32_t)J * (uint32_t)(kSlots * 32 * 4);
+                // slot nibble t % 8 to bits 7-9 by one right shift (of the words shifted left by 8
+                // for nibbles 0-1, as in the removed-mode pass above), or-ed into the cell address
+                const unsigned long long k8 = ((unsigned long long)nhi << 32 | nlo) << 8;
+                const uint32_t nlo8 = (uint32_t)k8, nhi8 = (uint32_t)(k8 >> 32);
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
-                    const uint32_t ks = __builtin_amdgcn_ubfe(t < 8 ? nlo : nhi, 4 * (t & 7), 4);
-                    const uint32_t qv = __builtin_amdgcn_ubfe(qrev[t >> 2], 8 * (t & 3), 8);
-                    const uint32_t a = rb[t] + jb + (ks << 7);
-                    __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)a), kCount1 | (unsigned long long)qv,
+                    const int u = t & 7;
+                    const uint32_t ksh = u < 2 ? (t < 8 ? nlo8 : nhi8) >> (4 * u + 1) : (t < 8 ? nlo : nhi) >> (4 * u - 7);
+                    uint32_t a;
+                    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xEA" : "=v"(a) : "v"(ksh), "v"(mslot_m), "v"(rb[t]));
+                    __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)a), kCount1 | (unsigned long long)qbyte(t),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 uint32_t nv = nw & posmask(rem);
@@ -1973,8 +2103,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     const int t = (__ffs(nv) - 1) >> 1;
                     nv &= nv - 1;
                     const unsigned long long v =
-                        kCount1 | (unsigned long long)__builtin_amdgcn_ubfe(qrev[t >> 2], 8 * (t & 3), 8);
-                    const uint32_t a = rb[t] + jb;
+                        kCount1 | (unsigned long long)__builtin_amdgcn_ubfe(qa[3 - (t >> 2)], 8 * (3 - (t & 3)), 8);
+                    const int c = m1 + 16 * J + t;  // (rb[t] recomputed: t is not a constant)
+                    const uint32_t a = xb + (uint32_t)((c >> 4) << 10 | (c & 15) << 3);
                     __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + 4u * 128u)), v, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + 3u * 128u)), 0ull - v,
@@ -1982,6 +2113,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 }
 #pragma unroll
                 for (int i = 0; i < 5; ++i) qw5[i] = qn[i];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) rb[t] += 2048u;  // (J + 2: two cycle rows on)
             }
         }
         if (valid && !(abl & 4) && !removed_mode) {
@@ -2035,18 +2168,6 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                         }
                     }
                 }
-            }
-        }
-        if (valid && !(abl & 4)) {
-            // per-read Stats scalars: (reads, length_sum) packed as count << 32 | sum, plus
-            // q20 << 32 | q30, into one of 16 LDS copies (lanes l, l + 16 share one)
-            unsigned long long* sc = scal + kScalStride * (lane_x & (LY::kScalCopies - 1)) + 4 * mate;
-            sadd(&sc[0], (1ull << 32) | (unsigned long long)L);
-            sadd(&sc[1], ((unsigned long long)q20 << 32) | q30);
-            const bool post_here = (MERGE && merged) ? (post_on && mate == 0) : post_on;
-            if (post_here) {
-                sadd(&sc[8], (1ull << 32) | (unsigned long long)((MERGE && merged) ? mlen : n));
-                sadd(&sc[9], ((unsigned long long)w20 << 32) | w30);
             }
         }
         FQ_STAMP(6)
@@ -2112,7 +2233,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
         for (int i = threadIdx.x; i < 2 * ncyc * 5; i += kThreads) {
             const int k = i / (ncyc * 5), j = i - k * ncyc * 5;
             const int c = j / 5, slot = j - c * 5;  // slots A C T G N
-            const uint32_t* hk = hist + k * (kRSlots * 32 * kChunks);
+            const uint32_t* hk = hist + k * 32;
             const unsigned long long kept = *reinterpret_cast<const unsigned long long*>(hk + rcell(c, slot < 4 ? 4 + slot : kRNSlot + 4));
             const unsigned long long rem = *reinterpret_cast<const unsigned long long*>(hk + rcell(c, slot < 4 ? slot : kRNSlot));
             const int cls = slot_class(slot);
@@ -2133,7 +2254,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
         const uint32_t* hx = hist + LY::kMrgOff;
         for (int i = threadIdx.x; i < ncyc * 5; i += kThreads) {
             const int c = i / 5, slot = i - c * 5;
-            const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hx + cell(c, slot));
+            const unsigned long long v = *reinterpret_cast<const unsigned long long*>(hx + mcell(c, slot));
             const long long cnt = (long long)(v >> 40);
             const long long qs = (long long)(v & kQMask) - 33ll * cnt;
             if (cnt == 0 && qs == 0) continue;

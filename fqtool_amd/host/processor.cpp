@@ -1743,11 +1743,12 @@ int run_tool(int argc, char** argv) {
         // GPU-side ingest and egress (fq_engine_submit_text): the engine builds the planes from
         // the FASTQ text and writes the output text, for the plain out1 (+ out2) case
         const char* tm_env = std::getenv("FQ_TEXT_MODE");
-        // (-m: every pair's output goes to the merged stream, which the engine writes as well)
+        // (-m: every pair's output goes to the merged stream, which the engine writes as well;
+        // with --discard_unmerged the unmerged pairs go to out1 / out2 instead: host packs)
         const bool text_mode = !(tm_env && std::string(tm_env) == "0") && !o.correction && !o.umi &&
                                !o.index_filter && !o.split() && !o.phred64 && o.failed_out.empty() &&
                                o.unpaired1.empty() && o.unpaired2.empty() &&
-                               (o.merge ? paired && !o.merge_out.empty()
+                               (o.merge ? paired && !o.merge_out.empty() && !o.discard_unmerged
                                         : !o.out1.empty() && (!paired || !o.out2.empty()));
         std::vector<std::unique_ptr<Lane>> lanes;
         const int cyc0 = std::max(16, round16(o.merge ? 2 * est : est)), stride0 = round16(std::max(est, 16));

@@ -355,9 +355,13 @@ int fq_engine_pending(const fq_engine* e); /* packs submitted and not yet report
  * the tiled batch planes from the text, runs the pack's kernels, and writes the output FASTQ text
  * of the records that pass (both mates of a pair for PE, to out1 / out2, in input order, each
  * record "name\nseq[start, start+len)\nstrand\nqual[start, start+len)\n" as the reference writes
- * it) into `out`.  Only for options whose outputs are out1 (+ out2): no -m, -c, UMI, index filter,
- * phred64, split, failed or unpaired outputs; the host routes everything else through
- * fq_engine_submit.  Records and text must stay valid until fq_engine_poll reports the pack; then
+ * it) into `out`.  With -m (merge_enabled, PE, no --discard_unmerged) every pair's output is the
+ * merged stream (src/peprocessor.cpp:351-385: the merged read, name "_merged_<m1>_<m2>" spliced in
+ * before the first space, when it merged and passes; otherwise each read that passes), written to
+ * out->text[0] (which must then hold text_bytes[0] + text_bytes[1] + 24 * n + 16 bytes), and
+ * out->bytes[1] is 0.  Only for options whose outputs are out1 (+ out2) or that merged stream: no
+ * -c, UMI, index filter, phred64, split, failed or unpaired outputs, no --discard_unmerged; the
+ * host routes everything else through fq_engine_submit.  Records and text must stay valid until fq_engine_poll reports the pack; then
  * `results` holds the records as from fq_engine_submit and out->bytes[m] the bytes of out->text[m].
  * out->text[m] must hold at least the mate's text_bytes + 16 (a record's output is never longer
  * than its input text, except by the final line terminator that the input may lack). */
@@ -403,7 +407,9 @@ int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*
  * (optional), fq_engine_raw_launch (window k: waits for its index), poll as for other packs.  At
  * most three windows are enqueued and not launched, and eight windows are in the engine (enqueued,
  * launched or not yet polled: a ninth enqueue waits for the oldest pack's copies); a window's
- * host bytes must stay valid until its pack is reported by fq_engine_poll.  Options as for text packs (no -m, -c, UMI, index filter).
+ * host bytes must stay valid until its pack is reported by fq_engine_poll.  Options as for text
+ * packs (-m writes the merged stream into out->text.text[0], which must then hold both mates' window
+ * and carry bytes + 28 * max_batch + 64; no -c, UMI, index filter, --discard_unmerged).
  * The trimmed-adapter strings (FilterResult::addAdapterTrimmed, src/filterresult.cpp:138-157) come
  * back after the output text, at out->text.text[m] + out->text.bytes[m], adapter_bytes[m] bytes of
  * entries "u16 ad_len (little endian), u8 neg, then ad_len bytes of the read (neg 0) or u16

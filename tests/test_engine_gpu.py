@@ -225,6 +225,42 @@ def test_lowercase_bases(eng_lib, oracle, name, stride):
     assert_same(p, res_o, acc_o, res_e, acc_e)
 
 
+@pytest.mark.parametrize("stride", [160, 336])
+@pytest.mark.parametrize("name", ["C3", "C3b", "C4", "C5", "PE_all", "C2", "SE_all"])
+def test_iupac_bases(eng_lib, oracle, name, stride):
+    """IUPAC codes and other bytes outside ACGTN (R Y K M S W B D H V, 'n', 'X', '.') stay on the fast
+    kernels (code 3 with the N bit and the flag bit beside the codes): anywhere in either mate,
+    several per read, inside polyG tails and the overlap of truly overlapping pairs, next to
+    lowercase bases.  Byte semantics as the reference: the reverse complement makes them 'N'
+    (src/seq.h:24-48), Stats buckets byte & 7 (src/stats.cpp:249, classes 0, 2 and 5 included),
+    passFilter counts only 'N' (src/filter.cpp:18), overlap / polyG / polyX / adapters compare
+    bytes.  The merge variant and the low-complexity filter hand such pairs over."""
+    p = config(name, max_cycles=512)
+    paired = bool(p.paired)
+    n = 6007
+    pk = synth_pack(oracle, n, paired, first=777, stride=stride)
+    rng = np.random.default_rng(53)
+    mates = [(pk.seq1, pk.len1)] + ([(pk.seq2, pk.len2)] if paired else [])
+    codes = np.frombuffer(b"RYKMSWBDHVnX.", np.uint8)
+    for m, (s, ln) in enumerate(mates):
+        for i in range(n):
+            L = int(ln[i])
+            u = rng.random()
+            if u < 0.08:  # a few exotic bytes anywhere
+                for _ in range(int(rng.integers(1, 4))):
+                    s[i, int(rng.integers(0, L))] = codes[int(rng.integers(0, len(codes)))]
+            elif u < 0.10:  # in the tail (polyG / polyX / adapter region)
+                s[i, L - int(rng.integers(1, 20))] = codes[int(rng.integers(0, len(codes)))]
+            elif u < 0.11:  # next to lowercase bases
+                a = int(rng.integers(0, max(1, L - 20)))
+                row = s[i, a:a + 20]
+                row[np.isin(row, np.frombuffer(b"ACGT", np.uint8))] |= 0x20
+                s[i, a + 10] = ord("R")
+    res_o, acc_o = run_oracle(oracle, p, pk)
+    res_e, acc_e = run_engine(eng_lib, p, pk)
+    assert_same(p, res_o, acc_o, res_e, acc_e)
+
+
 @pytest.mark.parametrize("name", ["C3", "C2", "PE_correct", "PE_umi", "C4"])
 def test_index_filtered_pairs(eng_lib, oracle, name, mode):
     """fq_batch.flags: pairs the host's index filter dropped count only in the pre-filter stats

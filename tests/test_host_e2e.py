@@ -198,7 +198,7 @@ def test_fqtool_raw_stream_small_windows_matches_reference(case, devices, tmp_pa
     p = subprocess.run(argv, capture_output=True, cwd=outd, timeout=300, env=env)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     if case in ("td_pe_qag", "td_pe_plain", "td_pe_detect", "synth_pe_c3", "synth_pe_c5", "synth_se_c2", "polygr_pe",
-                "edge_pe_dup", "td_se_q", "td_pe_merge", "td_pe_merge_discard", "synth_pe_c4", "edge_pe_merge"):
+                "edge_pe_dup", "td_se_q", "td_pe_merge", "synth_pe_c4", "edge_pe_merge"):
         assert "raw stream" in p.stderr.decode(), p.stderr.decode()[-1000:]
         if devices != "0":
             assert "raw stream on 3 engines" in p.stderr.decode(), p.stderr.decode()[-1000:]
