@@ -13,6 +13,13 @@
 #include <sys/mman.h>
 #include <string>
 
+// profiling only (FQ_PROF_NO_EGRESS=1): raw packs copy no output text back and report none, to
+// time the pipeline without its device-to-host leg (the outputs are empty)
+static bool prof_no_egress() {
+    static const bool on = std::getenv("FQ_PROF_NO_EGRESS") != nullptr;
+    return on;
+}
+
 #include "engine_internal.h"
 
 // Tile list the fast kernel hands to the general kernel (one per concurrently running launch).
@@ -82,6 +89,7 @@ struct fq_engine {
     hipStream_t stream = nullptr;
     unsigned long long* acc = nullptr;      // accumulator in use
     unsigned long long* own_acc = nullptr;  // the engine's own buffer
+    unsigned long long* xfix = nullptr;     // the fast kernels' exotic-byte Stats moves (fq_xfix_words)
     size_t acc_words = 0;
     int* err = nullptr;
     // host-memory path: pipeline slots and their streams
@@ -243,6 +251,9 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     e->acc = e->own_acc;
     if ((he = hipMalloc(&e->err, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc err"));
     if ((he = hipMemset(e->acc, 0, e->acc_words * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
+    const size_t xw = fq_xfix_words(params->max_cycles);
+    if ((he = hipMalloc(&e->xfix, xw * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc xfix"));
+    if ((he = hipMemset(e->xfix, 0, xw * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
     if ((he = hipMemset(e->err, 0, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
     // the first pipeline slot up front, so an engine that cannot hold one pack fails here
     if (max_batch > 0 && max_stride > 0 && alloc_slot(e, e->slots[0]) != FQ_OK) return bail(FQ_E_HIP);
@@ -265,6 +276,7 @@ int fq_engine_destroy(fq_engine* e) {
     (void)hipSetDevice(e->device);
     (void)hipDeviceSynchronize();
     if (e->own_acc) (void)hipFree(e->own_acc);
+    if (e->xfix) (void)hipFree(e->xfix);
     if (e->err) (void)hipFree(e->err);
     for (Slot& s : e->slots) free_slot(s);
     free_scratch(e->scratch);
@@ -304,7 +316,9 @@ static int launch(fq_engine* e, const fq_batch& db, fq_read_result* dres, hipStr
         if (rc != FQ_OK) return rc;
         HIP_TRY(e, hipMemsetAsync(sc.slow_count, 0, sizeof(int), s));
         if (timed) HIP_TRY(e, hipEventRecord(e->ev0, s));
-        HIP_TRY(e, fq_launch_pe_fast(e->p, db, dres, e->acc, sc.slow_tiles, sc.slow_count, e->cus, s));
+        HIP_TRY(e, fq_launch_pe_fast(e->p, db, dres, e->acc, sc.slow_tiles, sc.slow_count, e->xfix, e->cus, s));
+        HIP_TRY(e, fq_launch_xfix_fold(e->acc + fq_acc_stats_offset(e->p.insert_size_max, e->p.max_cycles, 0), e->xfix,
+                                       e->p.max_cycles, s));
         // (the hand-off list's length is known on the device only: as many workgroups as the
         // batch could need, at the occupancy the kernel's LDS allows; empty ones exit at once)
         HIP_TRY(e, fq_launch_pack_kernel(e->p, db, dres, e->acc, derr, grid_for(e, db.n), s, sc.slow_tiles,
@@ -352,6 +366,7 @@ static int retire_slot(fq_engine* e, int k) {
         for (int m = 0; m < 2; ++m) {
             o->adapter_bytes[m] = s.h_total[2 + m];
             if (o->adapter_bytes[m] == ~0ull) return fail(e, FQ_E_INVALID, "raw pack: adapter entries exceed the output copy");
+            if (prof_no_egress()) o->adapter_bytes[m] = o->text.bytes[m] = 0;
         }
     }
     return FQ_OK;
@@ -768,7 +783,7 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
     HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
     HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
-    for (int m = 0; m < mates; ++m)
+    for (int m = 0; m < mates && !prof_no_egress(); ++m)
         HIP_TRY(e, hipMemcpyAsync(out->text.text[m], s.d_out[m], back[m], hipMemcpyDeviceToHost, e->s_out));
     HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
     HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));

@@ -23,12 +23,16 @@ hipError_t fq_launch_pack_kernel(const fq_params& p, const fq_batch& b, fq_read_
 bool fq_pe_fast_supported(const fq_params& p);
 hipError_t fq_pe_fast_prepare();
 hipError_t fq_launch_pe_fast(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
-                             int* slow_tiles, int* slow_count, int grid, hipStream_t stream);
+                             int* slow_tiles, int* slow_count, unsigned long long* xfix, int grid, hipStream_t stream);
+// the fast kernels' exotic-byte Stats moves: a zeroed buffer of fq_xfix_words(max_cycles) words per
+// engine, folded into the accumulator's Stats blocks (acc_stats: their first word) after each launch
+size_t fq_xfix_words(int32_t max_cycles);
+hipError_t fq_launch_xfix_fold(unsigned long long* acc_stats, unsigned long long* xfix, int32_t max_cycles, hipStream_t s);
 // the same kernels built for rows of up to 320 bytes (pe_fast_long.hip; fq_launch_pe_fast
 // forwards batches with stride > 160 to it, except -m)
 hipError_t fq_pe_fast_long_prepare();
 hipError_t fq_launch_pe_fast_long(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
-                                  int* slow_tiles, int* slow_count, int grid, hipStream_t stream);
+                                  int* slow_tiles, int* slow_count, unsigned long long* xfix, int grid, hipStream_t stream);
 hipError_t fq_launch_synth(const fq_batch& b, uint64_t seed, uint64_t first_index, int read_len, hipStream_t stream);
 // Duplication analysis of one pack into a table (dup.hip); order_base orders the pack's reads
 // against other packs (the pack's sequence number).

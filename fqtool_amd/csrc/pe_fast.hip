@@ -208,6 +208,7 @@ struct Layout {
 };
 
 constexpr unsigned long long kCount1 = 1ull << 40;
+constexpr int kXfixCopies = 64;  // copies of the Stats blocks for the exotic-byte moves (see the Stats fix-up)
 constexpr unsigned long long kQMask = kCount1 - 1;
 
 // x of lane l ^ 32 (the other mate of the pair): one v_permlane32_swap, no LDS round trip
@@ -1013,7 +1014,7 @@ __device__ inline bool correct_pair_fast(const fq_params& p, uint32_t* col, uint
 template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA = false, bool FIX = false>
 __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __attribute__((amdgpu_waves_per_eu(Layout<LEAN, MERGE, PAIRED>::kWavesPerEU))) pe_fast_kernel(fq_params p, fq_batch b, fq_read_result* __restrict__ res,
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
-                                                         int* __restrict__ slow_count) {
+                                                         int* __restrict__ slow_count, unsigned long long* __restrict__ xfix) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     using LY = Layout<LEAN, MERGE, PAIRED>;
@@ -1843,10 +1844,14 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             if (!MERGE && xe && valid && !(abl & 4)) {
                 // exotic bytes: the passes below count them as N (class 6, code 3 + N bit); move each
                 // to its class byte & 7 (src/stats.cpp:249) in the pre block and, inside the post
-                // window, the post block, straight in the global accumulator (rare).  The row's
-                // address is re-derived here (S itself is not kept live this far).
-                const size_t sb = acc_stats_offset(p.insert_size_max, p.max_cycles, 0);
+                // window, the post block (rare).  The moves go to one of kXfixCopies copies of the
+                // four Stats blocks in global memory (by workgroup, so a column of IUPAC codes does
+                // not funnel every workgroup's atomics into one address), summed into the
+                // accumulator after the launch (fq_launch_xfix_fold).  The row's address is
+                // re-derived here (S itself is not kept live this far).
                 const size_t sw = acc_stats_words(p.max_cycles);
+                unsigned long long* xf = xfix + (size_t)(blockIdx.x & (kXfixCopies - 1)) * 4 * sw;
+                xfix[kXfixCopies * 4 * sw] = 1ull;  // (the fold's flag)
                 constexpr int cst = FQ_TILE_READS * FQ_CHUNK;
                 int ix = idx;
                 asm volatile("" : "+v"(ix));
@@ -1864,7 +1869,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                         if (cls == 6) continue;
                         const unsigned long long qv = (unsigned long long)(Q[off] - 33);
                         auto move = [&](int k, int cyc) {
-                            unsigned long long* dst = acc + sb + (size_t)k * sw + FQ_ST_CYCLES + (size_t)cyc * FQ_ST_PER_CYCLE;
+                            unsigned long long* dst = xf + (size_t)k * sw + FQ_ST_CYCLES + (size_t)cyc * FQ_ST_PER_CYCLE;
                             atomicAdd(&dst[6], ~0ull);
                             atomicAdd(&dst[8 + 6], 0ull - qv);
                             atomicAdd(&dst[cls], 1ull);
@@ -2345,24 +2350,25 @@ hipError_t FQ_PREPARE() {
 
 template <bool LEAN, bool PAIRED, bool MERGE, bool XTRA>
 static void launch_variant(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
-                           int* slow_tiles, int* slow_count, int grid, int extra_lds, hipStream_t stream) {
+                           int* slow_tiles, int* slow_count, unsigned long long* xfix, int grid, int extra_lds,
+                           hipStream_t stream) {
     using LY = Layout<LEAN, MERGE, PAIRED>;
     const dim3 g(grid * LY::kBlocksPerCU), t(LY::kThreads);
     const size_t lds = LY::kLdsW * 4 + extra_lds;
     if (b.stride == 16 * kChunks)
         hipLaunchKernelGGL((pe_fast_kernel<LEAN, PAIRED, MERGE, XTRA, true>), g, t, lds, stream, p, b, res, acc, slow_tiles,
-                           slow_count);
+                           slow_count, xfix);
     else
         hipLaunchKernelGGL((pe_fast_kernel<LEAN, PAIRED, MERGE, XTRA, false>), g, t, lds, stream, p, b, res, acc, slow_tiles,
-                           slow_count);
+                           slow_count, xfix);
 }
 
 hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res, unsigned long long* acc,
-                     int* slow_tiles, int* slow_count, int grid, hipStream_t stream) {
+                     int* slow_tiles, int* slow_count, unsigned long long* xfix, int grid, hipStream_t stream) {
 #if FQ_MAXLEN == 160
     // rows longer than 160 bytes: the 320-position build (reads beyond 320 bp are handed off per tile)
     if (b.stride > kMaxLen)
-        return fq_launch_pe_fast_long(p, b, res, acc, slow_tiles, slow_count, grid, stream);
+        return fq_launch_pe_fast_long(p, b, res, acc, slow_tiles, slow_count, xfix, grid, stream);
 #endif
     const bool lean = p.trim_front1 == 0 && p.trim_tail1 == 0 && p.trim_front2 == 0 && p.trim_tail2 == 0 &&
                       !(p.avg_qual_limit > 0) &&
@@ -2373,23 +2379,53 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
     const bool xtra = p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0 || p.avg_qual_limit > 0;
     const int pad = p.reserved[2] > 0 && p.reserved[2] <= 4096 ? p.reserved[2] : 0;  // profiling: extra LDS (LEAN)
     if (p.merge_enabled && (p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0))  // -c / UMI with -m
-        launch_variant<false, true, true, true>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
+        launch_variant<false, true, true, true>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, 0, stream);
     else if (p.merge_enabled)
-        launch_variant<false, true, true, false>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
+        launch_variant<false, true, true, false>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, 0, stream);
     else
     if (p.paired && lean)
-        launch_variant<true, true, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, pad, stream);
+        launch_variant<true, true, false, false>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, pad, stream);
     else if (p.paired && xtra)
-        launch_variant<false, true, false, true>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
+        launch_variant<false, true, false, true>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, 0, stream);
     else if (p.paired)
-        launch_variant<false, true, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
+        launch_variant<false, true, false, false>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, 0, stream);
     else if (lean)
-        launch_variant<true, false, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, pad, stream);
+        launch_variant<true, false, false, false>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, pad, stream);
     else if (xtra)
-        launch_variant<false, false, false, true>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
+        launch_variant<false, false, false, true>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, 0, stream);
     else
-        launch_variant<false, false, false, false>(p, b, res, acc, slow_tiles, slow_count, grid, 0, stream);
+        launch_variant<false, false, false, false>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, 0, stream);
     return hipGetLastError();
 }
 #undef FQ_PREPARE
 #undef FQ_LAUNCH
+
+#if FQ_MAXLEN == 160
+// The exotic-byte Stats moves (kXfixCopies copies of the four Stats blocks, see the fix-up in the
+// kernel) summed into the accumulator and cleared, when the flag after the copies is set.
+namespace {
+__global__ void xfix_fold_kernel(unsigned long long* __restrict__ acc, unsigned long long* __restrict__ xfix, size_t words) {
+    if (!xfix[kXfixCopies * words]) return;
+    for (size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (size_t)gridDim.x * blockDim.x) {
+        unsigned long long v = 0;
+        for (int c = 0; c < kXfixCopies; ++c) {
+            v += xfix[(size_t)c * words + w];
+            xfix[(size_t)c * words + w] = 0ull;
+        }
+        if (v) atomicAdd(&acc[w], v);
+    }
+}
+__global__ void xfix_flag_clear_kernel(unsigned long long* __restrict__ xfix, size_t words) {
+    xfix[kXfixCopies * words] = 0ull;
+}
+}  // namespace
+
+size_t fq_xfix_words(int32_t max_cycles) { return (size_t)kXfixCopies * 4 * fq_acc_stats_words(max_cycles) + 1; }
+
+hipError_t fq_launch_xfix_fold(unsigned long long* acc_stats, unsigned long long* xfix, int32_t max_cycles, hipStream_t s) {
+    const size_t words = 4 * fq_acc_stats_words(max_cycles);
+    hipLaunchKernelGGL(xfix_fold_kernel, dim3(64), dim3(256), 0, s, acc_stats, xfix, words);
+    hipLaunchKernelGGL(xfix_flag_clear_kernel, dim3(1), dim3(1), 0, s, xfix, words);
+    return hipGetLastError();
+}
+#endif

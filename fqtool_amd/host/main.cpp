@@ -2,4 +2,4 @@
 // per-pack hot path runs on MI355X through libfqengine.so.
 #include "processor.h"
 
-int main(int argc, char** argv) { return fqhost::run_tool(argc, argv); }
+int main(int argc, char** argv) { return fqhost::run_tool(argc, argv, true); }

@@ -89,6 +89,9 @@ std::string merged_name(const std::string& name, int len1, int len2);
 Options prepare_options(int argc, char** argv, bool detect_adapters = true);
 
 // The whole tool: returns the process exit code.
-int run_tool(int argc, char** argv);
+// exit_when_done: the command-line binary ends the process right after the outputs and reports
+// are written and the summary logged (_exit, no teardown of page-locked buffers, engines, pool);
+// in-process callers (fqh_run) get the return code as usual.
+int run_tool(int argc, char** argv, bool exit_when_done = false);
 
 }  // namespace fqhost

@@ -86,7 +86,9 @@ def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
            "-J", o["r.json"], "-H", o["r.html"], *extra]
     if cfg == "C4":
         cmd += ["--merge_output", o["m.fq"]]
-    env = dict(os.environ, FQ_TIMING="1")
+    env = dict(os.environ)
+    if os.environ.get("E2E_TEARDOWN_TIMING"):  # (FQ_TIMING keeps the teardown the binary otherwise skips)
+        env["FQ_TIMING"] = "1"
     for tok in [t for t in cmd if re.fullmatch(r"[A-Z_]+=\S*", t)]:  # KEY=VALUE extras: environment
         k, v = tok.split("=", 1)
         env[k] = v

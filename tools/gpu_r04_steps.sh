@@ -18,6 +18,8 @@ for st in ${STEPS:-}; do
     CONFIG=$c VARIANTS=full FQ_ENGINE_LIB=$PWD/build/alt/lib_stamps.so timeout -k 10 300 python -u tools/ablate.py > gpurun_out/stamps_$c.txt 2>&1 || exit 1 ;;
   e2e_gz) timeout -k 10 400 python -u tools/e2e_bench.py --pairs ${GZ_PAIRS:-4000000} --gz gzip --no-ref --null-out --repeat 2 > gpurun_out/e2e_gz.txt 2>&1 || exit 1 ;;
   e2e:*) d=${st#e2e:}; timeout -k 10 500 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 --devices $d ${E2E_ARGS:-} > gpurun_out/e2e_$d.txt 2>&1 || exit 1 ;;
+  e2e_noegress) FQ_PROF_NO_EGRESS=1 timeout -k 10 500 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 > gpurun_out/e2e_noegress.txt 2>&1 || exit 1 ;;
+  e2e_early) FQ_DETECT_EARLY=1 timeout -k 10 500 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 > gpurun_out/e2e_early.txt 2>&1 || exit 1 ;;
   e2e) timeout -k 10 500 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 ${E2E_ARGS:-} > gpurun_out/e2e.txt 2>&1 || exit 1 ;;
   bench) timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.log || exit 1 ;;
   round:*) c=${st#round:}; ROUND=r04 CONFIG=$c timeout -k 10 1000 bash tools/profile_round.sh > gpurun_out/profile_round_$c.log 2>&1 || exit 1 ;;
