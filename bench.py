@@ -241,6 +241,7 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
         big = write_fastq_fast(bufs, e2e_pairs, first, tmp, "e2e_") if e2e_pairs else None
         del bufs, lens
         torch.cuda.empty_cache()
+        os.sync()  # (the files' dirty pages written back now, not during the first timed run)
         log(f"FASTQ written in {time.perf_counter() - t0:.1f}s ({cpu_pairs} + {e2e_pairs} pairs)")
         opts = ["-q", "-a", "--detect_pe_adapter", "-g"]
 

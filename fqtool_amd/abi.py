@@ -119,7 +119,8 @@ class FqRawResult(ctypes.Structure):  # fq_raw_result
 
 
 class FqRawOut(ctypes.Structure):  # fq_raw_out
-    _fields_ = [("text", FqTextOut), ("adapter_bytes", ctypes.c_uint64 * 2)]
+    _fields_ = [("text", FqTextOut), ("adapter_bytes", ctypes.c_uint64 * 2),
+                ("results", ctypes.c_void_p), ("rec", ctypes.c_void_p * 2)]
 
 
 # Batch planes hold rows in chunk-interleaved tiles (include/fqengine.h): byte j of read i at

@@ -3,6 +3,7 @@
 // No CPU fallback: creation fails with FQ_E_NO_DEVICE unless a gfx950 device is present.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -220,10 +221,19 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     *out = nullptr;
     std::string why;
     if (validate_params(params, why) != FQ_OK) return fail(nullptr, FQ_E_INVALID, why);
+    // FQ_ENGINE_TIMING=1: the creation's steps on stderr (profiling: start-up of the tool)
+    static const bool timing = std::getenv("FQ_ENGINE_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto stamp = [&](const char* what) {
+        if (timing)
+            std::fprintf(stderr, "fq_engine_create: %s at %.4f s\n", what,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    };
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(nullptr, FQ_E_NO_DEVICE, "no HIP device visible (the engine has no CPU fallback)");
     if (device < 0 || device >= ndev) return fail(nullptr, FQ_E_NO_DEVICE, "device id out of range");
+    stamp("runtime up (hipGetDeviceCount)");
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess)
         return fail(nullptr, FQ_E_NO_DEVICE, "hipGetDeviceProperties failed");
@@ -255,8 +265,10 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     if ((he = hipMalloc(&e->xfix, xw * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMalloc xfix"));
     if ((he = hipMemset(e->xfix, 0, xw * 8)) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
     if ((he = hipMemset(e->err, 0, sizeof(int))) != hipSuccess) return bail(hip_fail(e, he, "hipMemset"));
+    stamp("streams and accumulators");
     // the first pipeline slot up front, so an engine that cannot hold one pack fails here
     if (max_batch > 0 && max_stride > 0 && alloc_slot(e, e->slots[0]) != FQ_OK) return bail(FQ_E_HIP);
+    stamp("first slot");
     if ((he = hipEventCreate(&e->ev0)) != hipSuccess) return bail(hip_fail(e, he, "hipEventCreate"));
     if ((he = hipEventCreate(&e->ev1)) != hipSuccess) return bail(hip_fail(e, he, "hipEventCreate"));
     if (fq_pack_kernel_lds_bytes(e->p) > 160 * 1024)
@@ -264,9 +276,11 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     if ((he = fq_pack_kernel_set_lds(e->p)) != hipSuccess) return bail(hip_fail(e, he, "hipFuncSetAttribute"));
     const char* force_general = std::getenv("FQ_ENGINE_GENERAL_ONLY");
     e->fast = fq_pe_fast_supported(e->p) && !(force_general && force_general[0] == '1');
+    stamp("general kernel attributes");
     if (e->fast) {
         if ((he = fq_pe_fast_prepare()) != hipSuccess) return bail(hip_fail(e, he, "hipFuncSetAttribute fast"));
     }
+    stamp("fast kernel attributes");
     *out = e;
     return FQ_OK;
 }
@@ -745,8 +759,9 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
         e->pending.push_back(Pending{seq_no, -1, true, 0});
         return FQ_OK;
     }
+    const bool recs_only = out->results != nullptr;  // (records-only egress: the caller formats)
     for (int m = 0; m < mates; ++m)
-        if (!out->text.text[m]) return fail(e, FQ_E_INVALID, "raw pack: missing output buffer");
+        if (recs_only ? !out->rec[m] : !out->text.text[m]) return fail(e, FQ_E_INVALID, "raw pack: missing output buffer");
     const size_t plane = fq_batch_bytes(e->max_batch, e->max_stride);
     fq_batch db{};
     db.n = n;
@@ -766,6 +781,22 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     int rc = launch(e, db, s.d_res, e->stream, s.scratch, false, false, seq_no, s.d_err);
     if (rc != FQ_OK) return rc;
     HIP_TRY(e, hipMemsetAsync(s.d_total, 0, 4 * sizeof(unsigned long long), e->stream));
+    if (recs_only) {  // the records and their line offsets back, no output text
+        HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
+        HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
+        HIP_TRY(e, hipMemcpyAsync(out->results, s.d_res, (size_t)n * mates * sizeof(fq_read_result), hipMemcpyDeviceToHost,
+                                  e->s_out));
+        for (int m = 0; m < mates; ++m)
+            HIP_TRY(e, hipMemcpyAsync(out->rec[m], s.d_trec[m], (size_t)n * sizeof(fq_text_rec), hipMemcpyDeviceToHost, e->s_out));
+        HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
+        HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
+        HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
+        s.busy = true;
+        s.text_out = &out->text;
+        s.raw_out = out;
+        e->pending.push_back(Pending{seq_no, k, false, 0});
+        return FQ_OK;
+    }
     // each mate's copy back: its output text (<= the input it spans) and the adapter entries after
     // it (per record, output + entry <= input + 3 bytes)
     // (-m: mate 0's output is the merged stream, mate 1's is empty: only its adapter entries)

@@ -1037,6 +1037,10 @@ void Pool::run(int n, const std::function<void(int)>& fn) {
 void Pack::clear() {
     n = 0;
     raw = false;
+    recs = false;
+    stage = -1;
+    rout.results = nullptr;
+    rout.rec[0] = rout.rec[1] = nullptr;
     stride = 0;
     base[0] = base[1] = nullptr;
     for (int m = 0; m < 2; ++m) {

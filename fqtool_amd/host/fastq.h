@@ -273,6 +273,13 @@ struct Pack {
     bool raw = false;
     fq_raw_out rout{};
     int stage = -1;  // the raw driver's staging window of the pack's input bytes
+    // records-only egress (fq_raw_out.results): the records and line offsets came back, the host
+    // formats from its staging window (rbuf[m]: [carry capacity - rcin | window bytes rwin] in the
+    // device buffer's layout; the carry is copied in front by the formatter from the previous pack)
+    bool recs = false;
+    char* rbuf[2] = {nullptr, nullptr};
+    uint64_t rwin[2] = {0, 0}, rcin[2] = {0, 0}, rccap = 0;
+    std::function<void(int)> stage_release;  // (records-only: the formatter returns stages through it)
 
     // -c: pairs whose bases the engine corrected read their seq/qual from a corrected copy
     // (fix[i] -> seq1 qual1 seq2 qual2 back to back; nullptr = the original text)

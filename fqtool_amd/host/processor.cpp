@@ -395,6 +395,15 @@ class Queue {  // bounded FIFO between pipeline threads; push/pop return at once
         not_full_.notify_one();
         return true;
     }
+    // 1: v taken; 0: empty (not closed); -1: closed and drained
+    int try_pop(T& v) {
+        std::lock_guard<std::mutex> l(m_);
+        if (q_.empty()) return closed_ ? -1 : 0;
+        v = std::move(q_.front());
+        q_.pop_front();
+        not_full_.notify_one();
+        return 1;
+    }
     void close() {
         std::lock_guard<std::mutex> l(m_);
         closed_ = true;
@@ -788,6 +797,129 @@ double since(std::chrono::steady_clock::time_point t) {
 
 struct Stopped {};  // another pipeline stage failed and closed the queues
 
+// Records-only raw packs (fq_raw_out.results): the output text and the trimmed-adapter entries built
+// on the host from its staging window, as text.hip's text_write_kernel and raw.hip's entries do on
+// the device (Read::toString of the passing records in input order, src/read.h:166-168,
+// src/peprocessor.cpp:457-491; FilterResult::addAdapterTrimmed's strings).  The window's carry (the
+// previous pack's unconsumed bytes) is copied in front of it first, from the previous pack's
+// window, which is then returned to the window reader.
+struct RawPrev {
+    char* buf[2] = {nullptr, nullptr};
+    uint64_t end[2] = {0, 0};
+    int stage = -1;
+    std::function<void(int)> release;
+};
+
+void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p, Pool& pool, AdapterCounts& ac) {
+    const int mates = pk.paired ? 2 : 1;
+    for (int m = 0; m < mates; ++m) {
+        char* base = pk.rbuf[m];
+        if (!base) {  // (the window that only drains the carry)
+            pk.text[m].resize_uninit((size_t)pk.rccap + 16);
+            base = pk.text[m].data();
+        }
+        if (pk.rcin[m]) {
+            if (!prev.buf[m] || prev.end[m] < pk.rcin[m]) throw std::runtime_error("raw pack: carry without its window");
+            std::memcpy(base + pk.rccap - pk.rcin[m], prev.buf[m] + prev.end[m] - pk.rcin[m], (size_t)pk.rcin[m]);
+        }
+        pk.base[m] = base;
+    }
+    if (prev.stage >= 0 && prev.release) prev.release(prev.stage);
+    prev.stage = pk.stage;
+    prev.release = pk.stage_release;
+    pk.stage = -1;
+    for (int m = 0; m < mates; ++m) {
+        prev.buf[m] = const_cast<char*>(pk.base[m]);
+        prev.end[m] = pk.rccap + pk.rwin[m];
+    }
+    const size_t n = (size_t)pk.n;
+    const fq_read_result* res = pk.res.data();
+    auto passes = [](const fq_read_result& r) {
+        return !(r.flags & (FQ_RF_NULL | FQ_RF_INDEX_FILTERED)) && r.code == FQ_PASS_FILTER;
+    };
+    auto out_ok = [&](size_t i) {
+        return pk.paired ? passes(res[2 * i]) && passes(res[2 * i + 1]) : passes(res[i]);
+    };
+    auto rr = [&](size_t i, int m) -> const fq_read_result& { return res[pk.paired ? 2 * i + m : i]; };
+    auto entry_bytes = [](const fq_read_result& r) -> size_t {
+        if (!(r.flags & (FQ_RF_AD_OVERLAP | FQ_RF_AD_SEQ)) || r.ad_len == 0) return 0;
+        return (r.flags & FQ_RF_AD_NEG) ? 5 : 3 + (size_t)r.ad_len;
+    };
+    const int parts = std::max(1, std::min(pool.size() * 2, (int)((n + 4095) / 4096)));
+    std::vector<size_t> osz((size_t)parts * 2, 0), esz((size_t)parts * 2, 0);
+    pool.run(parts, [&](int k) {
+        const size_t i0 = n * (size_t)k / (size_t)parts, i1 = n * (size_t)(k + 1) / (size_t)parts;
+        for (int m = 0; m < mates; ++m) {
+            const fq_text_rec* T = pk.trec[m].data();
+            size_t o = 0, e = 0;
+            for (size_t i = i0; i < i1; ++i) {
+                const fq_read_result& r = rr(i, m);
+                if (out_ok(i)) o += (size_t)T[i].name_len + T[i].strand_len + 2 * (size_t)r.len + 4;
+                if (adapters) e += entry_bytes(r);
+            }
+            osz[(size_t)(2 * k + m)] = o;
+            esz[(size_t)(2 * k + m)] = e;
+        }
+    });
+    size_t otot[2] = {0, 0}, etot[2] = {0, 0};
+    for (int k = 0; k < parts; ++k)
+        for (int m = 0; m < mates; ++m) {
+            const size_t a = osz[(size_t)(2 * k + m)], b = esz[(size_t)(2 * k + m)];
+            osz[(size_t)(2 * k + m)] = otot[m];
+            esz[(size_t)(2 * k + m)] = etot[m];
+            otot[m] += a;
+            etot[m] += b;
+        }
+    for (int m = 0; m < mates; ++m) {
+        pk.out_text[m].resize_uninit(otot[m] + etot[m] + 16);
+        pk.tout.text[m] = pk.out_text[m].data();
+        pk.tout.bytes[m] = otot[m];
+    }
+    pool.run(parts, [&](int k) {
+        const size_t i0 = n * (size_t)k / (size_t)parts, i1 = n * (size_t)(k + 1) / (size_t)parts;
+        for (int m = 0; m < mates; ++m) {
+            const fq_text_rec* T = pk.trec[m].data();
+            const char* t = pk.base[m];
+            char* d = pk.out_text[m].data() + osz[(size_t)(2 * k + m)];
+            char* ed = pk.out_text[m].data() + otot[m] + esz[(size_t)(2 * k + m)];
+            for (size_t i = i0; i < i1; ++i) {
+                const fq_text_rec& R = T[i];
+                const fq_read_result& r = rr(i, m);
+                if (out_ok(i)) {
+                    std::memcpy(d, t + R.name_off, R.name_len);
+                    d += R.name_len;
+                    *d++ = '\n';
+                    std::memcpy(d, t + R.seq_off + r.start, r.len);
+                    d += r.len;
+                    *d++ = '\n';
+                    std::memcpy(d, t + R.strand_off, R.strand_len);
+                    d += R.strand_len;
+                    *d++ = '\n';
+                    std::memcpy(d, t + R.qual_off + r.start, r.len);
+                    d += r.len;
+                    *d++ = '\n';
+                }
+                if (adapters && entry_bytes(r)) {
+                    ed[0] = (char)(r.ad_len & 0xFF);
+                    ed[1] = (char)(r.ad_len >> 8);
+                    if (r.flags & FQ_RF_AD_NEG) {
+                        ed[2] = 1;
+                        ed[3] = (char)(r.ad_pos & 0xFF);
+                        ed[4] = (char)(r.ad_pos >> 8);
+                        ed += 5;
+                    } else {
+                        ed[2] = 0;
+                        std::memcpy(ed + 3, t + R.seq_off + r.ad_pos, r.ad_len);
+                        ed += 3 + r.ad_len;
+                    }
+                }
+            }
+        }
+    });
+    if (adapters)
+        for (int m = 0; m < mates; ++m) ac.add_entries(m, pk.out_text[m].data() + otot[m], etot[m], p, &pool);
+}
+
 // Raw streams on several engines (--devices with more than one entry; fq_engine_raw_*).  The host cuts
 // the inputs into windows of whole pairs: it counts the line feeds of the bytes it preads and ends
 // every mate's window after the same number of four-line records (at most the engines' max_batch),
@@ -1043,8 +1175,9 @@ struct Lane {
         if (rc != 1) throw std::runtime_error(std::string("fq_engine_poll: ") + fq_engine_last_error(e));
         if (seq != pk->seq_no) throw std::runtime_error("engine completed packs out of order");
         if (pk->raw) {  // its input window was copied: recycle the staging; the output sizes are in
-            if (pk->stage >= 0) (multi ? multi->free_stages : free_stages).push(pk->stage);
-            pk->stage = -1;
+            // (records-only egress: the formatter still reads the window, and returns it)
+            if (pk->stage >= 0 && !pk->recs) (multi ? multi->free_stages : free_stages).push(pk->stage);
+            if (!pk->recs) pk->stage = -1;
             pk->tout = pk->rout.text;
         }
         if (!out.push(std::move(pk))) throw Stopped();
@@ -1123,6 +1256,12 @@ struct Lane {
         // windows of up to 64 MiB per mate (a pack of `target` 2x150 pairs is ~45 MiB), 16 MiB of
         // carry (partial records, the mates' imbalance); six windows in the engine at once
         const uint64_t wcap = (uint64_t)64 << 20, ccap = (uint64_t)16 << 20;
+        // records-only egress (FQ_RAW_EGRESS=host): the engine sends back records and line offsets,
+        // the formatter writes the output from the staging window, which then keeps the carry
+        // capacity free in front of the window bytes (the device buffer's layout)
+        const char* eg_env = std::getenv("FQ_RAW_EGRESS");
+        const bool recs = !merge && eg_env && std::string(eg_env) == "host";
+        const uint64_t off0 = recs ? ccap : 0;
         const int raw_depth = 4;  // packs launched and not yet polled
         const size_t raw_ahead = 3;  // windows enqueued ahead of their launch (the copy-in queue)
         if (fq_engine_raw_begin(e, wcap, ccap) != FQ_OK)
@@ -1145,10 +1284,10 @@ struct Lane {
             const int have = (int)stages.size();
             while ((int)stages.size() < kStages) stages.emplace_back(new Stage);
             free_stages.push(have);
-            warmer = std::thread([this, have, kStages, wcap, mates] {
+            warmer = std::thread([this, have, kStages, wcap, off0, mates] {
                 try {
                     for (int i = have + 1; i < kStages; ++i) {
-                        for (int m = 0; m < mates; ++m) stages[(size_t)i]->buf[m].reserve((size_t)wcap);
+                        for (int m = 0; m < mates; ++m) stages[(size_t)i]->buf[m].reserve((size_t)(off0 + wcap));
                         if (!free_stages.push(i)) break;
                     }
                 } catch (...) {  // (no page-locked memory left: the stages made so far suffice)
@@ -1228,7 +1367,7 @@ struct Lane {
                     const uint64_t piece = piece_bytes;
                     int pieces[2] = {0, 0};
                     for (int m = 0; m < mates; ++m) {
-                        st.buf[m].resize_uninit((size_t)std::max<uint64_t>(w.n[m], 1));
+                        st.buf[m].resize_uninit((size_t)(off0 + std::max<uint64_t>(w.n[m], 1)));
                         pieces[m] = (int)((w.n[m] + piece - 1) / piece);
                     }
                     std::atomic<bool> short_read{false};
@@ -1236,13 +1375,14 @@ struct Lane {
                         const int m = k < pieces[0] ? 0 : 1;
                         const uint64_t o = (uint64_t)(m ? k - pieces[0] : k) * piece;
                         const uint64_t len = std::min(piece, w.n[m] - o);
+                        char* dst = st.buf[m].data() + off0 + o;
                         if (mp[m]) {  // (FQ_RAW_COPY=mmap: copy from a read-only mapping)
-                            std::memcpy(st.buf[m].data() + o, mp[m] + w.start[m] + o, (size_t)len);
+                            std::memcpy(dst, mp[m] + w.start[m] + o, (size_t)len);
                             return;
                         }
                         uint64_t got = 0;
                         while (got < len) {
-                            const ssize_t r = pread(fd[m], st.buf[m].data() + o + got, (size_t)(len - got), (off_t)(w.start[m] + o + got));
+                            const ssize_t r = pread(fd[m], dst + got, (size_t)(len - got), (off_t)(w.start[m] + o + got));
                             if (r <= 0) {
                                 short_read = true;
                                 return;
@@ -1265,7 +1405,7 @@ struct Lane {
         auto enqueue_window = [&](const Win& w) {  // (stage -1: an empty window)
             fq_raw_window rw{};
             for (int m = 0; m < mates; ++m) {
-                rw.bytes[m] = w.stage >= 0 ? stages[(size_t)w.stage]->buf[m].data() : nullptr;
+                rw.bytes[m] = w.stage >= 0 ? stages[(size_t)w.stage]->buf[m].data() + off0 : nullptr;
                 rw.n[m] = w.n[m];
             }
             const auto q0 = std::chrono::steady_clock::now();
@@ -1319,12 +1459,28 @@ struct Lane {
                         cin[0] = carry[0];
                         cin[1] = carry[1];
                     }
-                    for (int m = 0; m < 2; ++m) {  // (output text, then the adapter entries)
-                        size_t cap = m < mates ? (size_t)(cin[m] + w.n[m] + 4 * (uint64_t)target + 64) : 0;
-                        if (merge && m == 0)  // (-m: the merged stream of both mates' text)
-                            cap = (size_t)(cin[0] + w.n[0] + cin[1] + w.n[1] + 28 * (uint64_t)target + 64);
-                        pk->out_text[m].resize_uninit(cap);
-                        pk->rout.text.text[m] = m < mates ? pk->out_text[m].data() : nullptr;
+                    if (recs) {  // records and line offsets back; the formatter writes the text
+                        pk->recs = true;
+                        pk->rccap = ccap;
+                        pk->stage_release = [this](int sidx) { free_stages.push(sidx); };
+                        pk->res.resize((size_t)target * mates);
+                        pk->rout.results = pk->res.data();
+                        for (int m = 0; m < 2; ++m) {
+                            pk->rbuf[m] = m < mates && w.stage >= 0 ? stages[(size_t)w.stage]->buf[m].data() : nullptr;
+                            pk->rwin[m] = m < mates ? w.n[m] : 0;
+                            pk->rcin[m] = m < mates ? cin[m] : 0;
+                            if (m < mates) pk->trec[m].resize((size_t)target);
+                            pk->rout.rec[m] = m < mates ? pk->trec[m].data() : nullptr;
+                            pk->rout.text.text[m] = nullptr;
+                        }
+                    } else {
+                        for (int m = 0; m < 2; ++m) {  // (output text, then the adapter entries)
+                            size_t cap = m < mates ? (size_t)(cin[m] + w.n[m] + 4 * (uint64_t)target + 64) : 0;
+                            if (merge && m == 0)  // (-m: the merged stream of both mates' text)
+                                cap = (size_t)(cin[0] + w.n[0] + cin[1] + w.n[1] + 28 * (uint64_t)target + 64);
+                            pk->out_text[m].resize_uninit(cap);
+                            pk->rout.text.text[m] = m < mates ? pk->out_text[m].data() : nullptr;
+                        }
                     }
                     fq_raw_result r{};
                     const auto e0 = std::chrono::steady_clock::now();
@@ -1435,8 +1591,11 @@ struct Lane {
             engine_raw = true;
             for (;;) {
                 while (enq.size() < raw_ahead && !input_done) {
+                    // (wait for a window only when none is enqueued: the front one may be due)
                     RawMulti::Win w;
-                    if (!R.wq[(size_t)g]->pop(w)) {
+                    const int got = enq.empty() ? (R.wq[(size_t)g]->pop(w) ? 1 : -1) : R.wq[(size_t)g]->try_pop(w);
+                    if (got == 0) break;
+                    if (got < 0) {
                         input_done = true;
                         break;
                     }
@@ -1659,17 +1818,20 @@ Options prepare_options(int argc, char** argv, bool detect_adapters) {
 }
 
 int run_tool(int argc, char** argv, bool exit_when_done) {
-    // Eight hardware queues instead of HIP's default four: the engine's copy-in, index, compute
-    // and copy-out streams plus the concurrent adapter detection's stream each get their own, so
-    // the DMA copies of one direction do not queue behind those of the other (unless the caller
-    // chose a value; read when HIP initialises, before any engine exists)
-    setenv("GPU_MAX_HW_QUEUES", "8", 0);
     Options o;
     const auto t0 = std::chrono::steady_clock::now();
     try {
         // (an interleaved input has no read2 file to detect on: the synchronous pre-pass fails
         // on it before anything is written, as in the reference)
         o = prepare_options(argc, argv, false);
+        // Hardware queues beyond HIP's default four: each engine's copy-in, index, compute and
+        // copy-out streams plus the concurrent adapter detection's stream get their own, so the
+        // DMA copies of one direction (or of one engine) do not queue behind the others' work
+        // (unless the caller chose a value; read when HIP initialises, before any engine exists)
+        {
+            const int per_gpu = std::max<int>(1, (int)o.device_list().size());
+            setenv("GPU_MAX_HW_QUEUES", std::to_string(std::min(4 * per_gpu + 4, 24)).c_str(), 0);
+        }
         if (o.detect_pe_adapter && o.in2.empty()) {
             Detection d = detect_pe_adapters(o);
             if (d.err) std::rethrow_exception(d.err);
@@ -1897,11 +2059,20 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
         double format_s = 0;
         std::thread formatter([&] {
             try {
+                RawPrev raw_prev;  // (records-only raw packs: the window the next carry comes from)
                 std::unique_ptr<Pack> pk;
                 for (uint64_t k = 0; lanes[(size_t)(k % (uint64_t)G)]->out.pop(pk); ++k) {
                     const auto f0 = std::chrono::steady_clock::now();
                     if (pk->seq_no != k) throw std::runtime_error("packs reached the formatter out of order");
                     const fq_params p = o.to_params(pk->max_cycles);
+                    if (pk->raw && pk->recs) {  // records-only egress: the text is formatted here
+                        format_raw_recs(*pk, raw_prev, o.adapter_trimming, p, pool, ac);
+                        format_s += since(f0);
+                        reads += (uint64_t)pk->n * (paired ? 2 : 1);
+                        Pack* raw = pk.release();
+                        outs.consume_text(*raw, [raw, &spare] { spare.push(std::unique_ptr<Pack>(raw)); });
+                        continue;
+                    }
                     if (pk->text_mode) {  // the engine wrote the output text
                         if (o.adapter_trimming) {
                             if (pk->raw)

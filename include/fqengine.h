@@ -431,6 +431,15 @@ typedef struct fq_raw_result {
 typedef struct fq_raw_out {
     fq_text_out text;          /* text[m]: >= carry capacity + window bytes + 4 * max_batch + 16 */
     uint64_t adapter_bytes[2]; /* set by fq_engine_poll: entries after the output text */
+    /* Records-only egress (all set, or all null): instead of the output text the pack's records
+     * come back -- results[2i + m] (PE) / results[i] as from fq_engine_submit, and rec[m][i] the
+     * record's line offsets in the window buffer [carry capacity - carry | window bytes] (the
+     * window's bytes at offset carry capacity, the previous pack's unconsumed bytes just before),
+     * so a caller that kept its page-locked window bytes (and the carry in front of them) formats
+     * the output itself; text.bytes and adapter_bytes are 0.  80 bytes per pair cross PCIe instead
+     * of the ~input-sized text. */
+    fq_read_result* results;   /* >= pairs * 2 (PE) / reads */
+    fq_text_rec* rec[2];       /* >= max_batch each (rec[1]: PE) */
 } fq_raw_out;
 int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap);
 int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w);

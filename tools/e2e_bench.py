@@ -100,7 +100,9 @@ def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
         raise SystemExit(f"{tag} failed rc={p.returncode}: {p.stderr[-2000:]}")
     m = re.search(r"fqtool-amd: (.*)", p.stderr)
     t = re.search(r"fqtool-amd timing: (.*)", p.stderr)
-    return wall, (m.group(1) if m else "(no fqtool-amd summary line)") + ((" | " + t.group(1)) if t else ""), o
+    ec = re.findall(r"fq_engine_create: (.*)", p.stderr)  # (FQ_ENGINE_TIMING=1)
+    return wall, (m.group(1) if m else "(no fqtool-amd summary line)") + ((" | " + t.group(1)) if t else "") + \
+        ((" | engine: " + "; ".join(ec)) if ec else ""), o
 
 
 def _bgzf_chunk(arg):
@@ -161,6 +163,7 @@ def main():
         t0 = time.perf_counter()
         r1, r2 = gen_fastq(args.pairs, tmp)
         gb = (os.path.getsize(r1) + os.path.getsize(r2)) / 1e9
+        os.sync()
         print(f"[e2e] wrote {args.pairs} pairs ({gb:.2f} GB FASTQ) in {time.perf_counter() - t0:.1f}s", flush=True)
         if args.gz:
             t0 = time.perf_counter()
