@@ -48,6 +48,9 @@ namespace long320 {  // (kernel names tell the two builds apart in profiles)
 namespace {
 #endif
 
+#ifndef FQ_MERGE_ROTATE  // merged-part Stats walk rotated per lane (conflict-free LDS banks; slower)
+#define FQ_MERGE_ROTATE 0
+#endif
 #ifndef FQ_ABLATE_STAGE
 #define FQ_ABLATE_STAGE 0
 #endif
@@ -2045,16 +2048,30 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             const int c2 = lane_x | 32;  // read 2's column
             const int pos_hi = ws2 + m2 - 1;
             const int ci0 = kMaxLen - 1 - pos_hi;
-            // byte address of merged cycle m1 + 16 J + t's slot-0 cell (mcell), for this lane's next J
+            // FQ_MERGE_ROTATE=1: each lane walks its groups rotated by rl = (lane - m1) % 16
+            // positions: at step t it takes part position 16 J + (t + rl) % 16, merged cycle c with
+            // c % 16 = (t + lane) % 16, so the 16 lanes of an LDS group hit 16 bank pairs whatever
+            // their m1.  Unrotated (the default), the cycles of a step depend on m1 and collide: 39 %
+            // of the C4 kernel's LDS cycles are bank conflicts, 4.6 % rotated -- but the rotation's
+            // VALU (+104 per tile) costs more than the conflicts (C4 +1-2 % per launch,
+            // profiles/r04_ab_merge_rotate.txt): the LDS waits overlap other waves' VALU.
+            // rb[t]: byte address of step t's slot-0 cell (mcell) for the lane's next J.
             static_assert((LY::kColsW + LY::kMrgOff) % 256 == 0, "merged-part rows: 1 KiB aligned");
+            constexpr bool kRot = FQ_MERGE_ROTATE != 0;
+            const int rl = kRot ? (lane_x - m1) & 15 : 0;
             uint32_t rb[16];
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
-                const int c = m1 + t + 16 * mate;
+                const int c = m1 + ((t + rl) & 15) + 16 * mate;
                 rb[t] = xb + (uint32_t)((c >> 4) << 10 | (c & 15) << 3);
                 asm volatile("" : "+v"(rb[t]));
             }
             const uint32_t mslot_m = vk(0x380u);
+            const bool mswap = rl >= 8;
+            const int rr4m = 4 * (rl & 7);
+            // qualities: qa is in reversed position order v = 15 - u (byte v % 4 of qa[v / 4]);
+            // rotated by rv = -rl bytes, step t's byte is at reversed index 15 - t
+            const int rv = (16 - rl) & 15, vsel = rv >> 2;
             // quality dwords of forward positions [hi - 15, hi], hi = pos_hi - 16J: words
             // wl0 - 4J .. wl0 - 4J + 4; the lane's next group (J + 2) is requested one group ahead
             const int wl0 = (pos_hi - 15) >> 2, sh = (pos_hi - 15) & 3;  // (negative only for dummies)
@@ -2074,13 +2091,23 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 uint32_t qn[5];
 #pragma unroll
                 for (int i = 0; i < 5; ++i) qn[i] = qword(wl0 - 4 * (J + 2) + i);
-                // qualities ascending in qa[0..3]: merged t is byte 3 - t % 4 of qa[3 - t / 4]
+                // qualities ascending in qa[0..3]: part position u is byte 3 - u % 4 of qa[3 - u / 4]
                 uint32_t qa[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) qa[i] = __builtin_amdgcn_alignbyte(qw5[i + 1], qw5[i], sh);
-                auto qbyte = [&](int t) -> uint32_t {  // (bytes 0 and 3 by one full-rate op)
-                    const uint32_t qw = qa[3 - (t >> 2)];
-                    const int bs = 3 - (t & 3);
+                // rotated: reversed index x = 4k + b is byte b of qv4[k], position u = (15 - x + rl) % 16
+                uint32_t qv4[4] = {qa[0], qa[1], qa[2], qa[3]};
+                if constexpr (kRot) {
+                const uint32_t t0 = (vsel & 1) ? qa[1] : qa[0], t1 = (vsel & 1) ? qa[2] : qa[1];
+                const uint32_t t2 = (vsel & 1) ? qa[3] : qa[2], t3 = (vsel & 1) ? qa[0] : qa[3];
+                const uint32_t a0 = (vsel & 2) ? t2 : t0, a1 = (vsel & 2) ? t3 : t1;
+                const uint32_t a2 = (vsel & 2) ? t0 : t2, a3 = (vsel & 2) ? t1 : t3;
+                qv4[0] = __builtin_amdgcn_alignbyte(a1, a0, rv & 3), qv4[1] = __builtin_amdgcn_alignbyte(a2, a1, rv & 3);
+                qv4[2] = __builtin_amdgcn_alignbyte(a3, a2, rv & 3), qv4[3] = __builtin_amdgcn_alignbyte(a0, a3, rv & 3);
+                }
+                auto qbyte = [&](int t) -> uint32_t {  // step t (bytes 0 and 3 by one full-rate op)
+                    const uint32_t qw = qv4[(15 - t) >> 2];
+                    const int bs = (15 - t) & 3;
                     return bs == 0 ? qw & 0xFFu : bs == 3 ? qw >> 24 : __builtin_amdgcn_ubfe(qw, 8 * bs, 8);
                 };
                 // slot nibbles: code, or the dummy slot beyond the part
@@ -2090,14 +2117,20 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 const uint32_t dlo = (uint32_t)dm, dhi = rem >= 16 ? 0u : (uint32_t)(dm >> 32);
                 nlo = (nlo & ~dlo) | (dlo & 0x55555555u);  // 5 = kDummySlot
                 nhi = (nhi & ~dhi) | (dhi & 0x55555555u);
+                // rotated by rl nibbles: nibble t of {khi:klo} is part position (t + rl) % 16
+                uint32_t klo = nlo, khi = nhi;
+                if constexpr (kRot) {
+                    const uint32_t xa = mswap ? nhi : nlo, xb2 = mswap ? nlo : nhi;
+                    klo = __builtin_amdgcn_alignbit(xb2, xa, rr4m), khi = __builtin_amdgcn_alignbit(xa, xb2, rr4m);
+                }
                 // slot nibble t % 8 to bits 7-9 by one right shift (of the words shifted left by 8
                 // for nibbles 0-1, as in the removed-mode pass above), or-ed into the cell address
-                const unsigned long long k8 = ((unsigned long long)nhi << 32 | nlo) << 8;
+                const unsigned long long k8 = ((unsigned long long)khi << 32 | klo) << 8;
                 const uint32_t nlo8 = (uint32_t)k8, nhi8 = (uint32_t)(k8 >> 32);
 #pragma unroll
                 for (int t = 0; t < 16; ++t) {
                     const int u = t & 7;
-                    const uint32_t ksh = u < 2 ? (t < 8 ? nlo8 : nhi8) >> (4 * u + 1) : (t < 8 ? nlo : nhi) >> (4 * u - 7);
+                    const uint32_t ksh = u < 2 ? (t < 8 ? nlo8 : nhi8) >> (4 * u + 1) : (t < 8 ? klo : khi) >> (4 * u - 7);
                     uint32_t a;
                     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xEA" : "=v"(a) : "v"(ksh), "v"(mslot_m), "v"(rb[t]));
                     __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)a), kCount1 | (unsigned long long)qbyte(t),

@@ -18,9 +18,10 @@ import re
 import sys
 from collections import defaultdict
 
-SRC = "pe_fast.hip"
-SRC_PATH = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "..",
-                                        "fqtool_amd", "csrc", SRC)
+# (ISA_SRC: another copy of the source the assembly was built from, e.g. an older revision)
+SRC_PATH = __import__("os").environ.get("ISA_SRC") or __import__("os").path.join(
+    __import__("os").path.dirname(__import__("os").path.abspath(__file__)), "..", "fqtool_amd", "csrc", "pe_fast.hip")
+SRC = __import__("os").path.basename(SRC_PATH)
 # kernel-body sections: the "// ---------------- <name>" marker comments of pe_fast.hip
 MARKERS = [("staging", "staging"), ("trimAndCut", "trim"), ("polyG", "polyG"), ("overlap", "overlap"),
            ("polyX", "polyx_maxlen"), ("merge", "merge"), ("passFilter", "filter"), ("Stats::statRead", "stats"),
