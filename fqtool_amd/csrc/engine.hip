@@ -115,6 +115,22 @@ struct fq_engine {
 
 static std::string g_create_error;
 
+// Raw-window copies of the engines that share one GPU (and so one PCIe link) run one after another
+// in call order: each engine's host-to-device copies wait for the last one another engine enqueued
+// on the device (and likewise its device-to-host copies).  Left to share the link, the copies of a
+// window that is due would finish only with those of the windows enqueued behind it on the other
+// engines (the raw stream launches windows in order), so several engines on one GPU ran slower than
+// one.  Engines on different GPUs never wait for each other.
+struct LinkChain {
+    std::mutex m;
+    hipEvent_t in = nullptr, out = nullptr;  // the last copies enqueued on the device
+    const fq_engine *in_owner = nullptr, *out_owner = nullptr;
+};
+static LinkChain& link_chain(int device) {
+    static LinkChain chains[64];
+    return chains[device & 63];
+}
+
 static int fail(fq_engine* e, int code, const std::string& msg) {
     if (e) e->last_error = msg;
     else g_create_error = msg;
@@ -289,6 +305,12 @@ int fq_engine_destroy(fq_engine* e) {
     if (!e) return FQ_OK;
     (void)hipSetDevice(e->device);
     (void)hipDeviceSynchronize();
+    {
+        LinkChain& lc = link_chain(e->device);  // (its events are about to go)
+        std::lock_guard<std::mutex> g(lc.m);
+        if (lc.in_owner == e) lc.in = nullptr, lc.in_owner = nullptr;
+        if (lc.out_owner == e) lc.out = nullptr, lc.out_owner = nullptr;
+    }
     if (e->own_acc) (void)hipFree(e->own_acc);
     if (e->xfix) (void)hipFree(e->xfix);
     if (e->err) (void)hipFree(e->err);
@@ -699,10 +721,16 @@ int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w) {
     Slot& s = e->slots[k];
     if ((rc = alloc_slot(e, s)) != FQ_OK) return rc;
     if ((rc = ensure_raw(e, s)) != FQ_OK) return rc;
-    for (int m = 0; m < (pe ? 2 : 1); ++m)
-        if (w->n[m])
-            HIP_TRY(e, hipMemcpyAsync(s.d_text[m] + e->raw_ccap, w->bytes[m], w->n[m], hipMemcpyHostToDevice, e->s_in));
-    HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
+    {
+        LinkChain& lc = link_chain(e->device);
+        std::lock_guard<std::mutex> g(lc.m);
+        if (lc.in && lc.in_owner != e) HIP_TRY(e, hipStreamWaitEvent(e->s_in, lc.in, 0));
+        for (int m = 0; m < (pe ? 2 : 1); ++m)
+            if (w->n[m])
+                HIP_TRY(e, hipMemcpyAsync(s.d_text[m] + e->raw_ccap, w->bytes[m], w->n[m], hipMemcpyHostToDevice, e->s_in));
+        HIP_TRY(e, hipEventRecord(s.ev_in, e->s_in));
+        lc.in = s.ev_in, lc.in_owner = e;
+    }
     HIP_TRY(e, hipStreamWaitEvent(e->s_idx, s.ev_in, 0));
     s.raw_n[0] = w->n[0];
     s.raw_n[1] = pe ? w->n[1] : 0;
@@ -813,11 +841,17 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     }
     HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
     HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
-    HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
-    for (int m = 0; m < mates && !prof_no_egress(); ++m)
-        HIP_TRY(e, hipMemcpyAsync(out->text.text[m], s.d_out[m], back[m], hipMemcpyDeviceToHost, e->s_out));
-    HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
-    HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
+    {
+        LinkChain& lc = link_chain(e->device);
+        std::lock_guard<std::mutex> g(lc.m);
+        if (lc.out && lc.out_owner != e) HIP_TRY(e, hipStreamWaitEvent(e->s_out, lc.out, 0));
+        HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
+        for (int m = 0; m < mates && !prof_no_egress(); ++m)
+            HIP_TRY(e, hipMemcpyAsync(out->text.text[m], s.d_out[m], back[m], hipMemcpyDeviceToHost, e->s_out));
+        HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
+        HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
+        lc.out = s.ev_done, lc.out_owner = e;
+    }
     s.busy = true;
     s.text_out = &out->text;
     s.raw_out = out;

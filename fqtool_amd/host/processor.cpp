@@ -957,6 +957,8 @@ struct RawMulti {
     std::mutex m;
     std::condition_variable cv;
     uint64_t next_launch = 0;  // the id allowed to launch next
+    uint64_t next_enqueue = 0;  // the id allowed to enqueue next (its copies follow the previous
+                                // window's on a shared GPU: fq_engine_raw_enqueue)
     bool stopped = false;      // the stream has ended; rr says where
     RawResumeInfo rr;
     std::string why;
@@ -1572,6 +1574,8 @@ struct Lane {
         const int raw_depth = 4;
         const size_t raw_ahead = 3;
         std::deque<RawMulti::Win> enq;  // enqueued on this engine (or the end marker), not launched
+        RawMulti::Win held;             // popped, waiting for its turn to enqueue (windows enqueue in id order)
+        bool have_held = false;
         bool input_done = false;
         bool engine_raw = false;
         auto drop_all = [&] {  // windows not launched: their copies finish, then the stages return
@@ -1581,6 +1585,8 @@ struct Lane {
             for (const RawMulti::Win& w : enq)
                 if (w.stage >= 0) R.free_stages.push(w.stage);
             enq.clear();
+            if (have_held && held.stage >= 0) R.free_stages.push(held.stage);
+            have_held = false;
             RawMulti::Win w;
             while (R.wq[(size_t)g]->pop(w))
                 if (w.stage >= 0) R.free_stages.push(w.stage);
@@ -1590,15 +1596,29 @@ struct Lane {
                 throw std::runtime_error(std::string("fq_engine_raw_begin: ") + fq_engine_last_error(e));
             engine_raw = true;
             for (;;) {
+                bool stop_now = false;
                 while (enq.size() < raw_ahead && !input_done) {
                     // (wait for a window only when none is enqueued: the front one may be due)
-                    RawMulti::Win w;
-                    const int got = enq.empty() ? (R.wq[(size_t)g]->pop(w) ? 1 : -1) : R.wq[(size_t)g]->try_pop(w);
-                    if (got == 0) break;
-                    if (got < 0) {
-                        input_done = true;
-                        break;
+                    if (!have_held) {
+                        const int got = enq.empty() ? (R.wq[(size_t)g]->pop(held) ? 1 : -1) : R.wq[(size_t)g]->try_pop(held);
+                        if (got == 0) break;
+                        if (got < 0) {
+                            input_done = true;
+                            break;
+                        }
+                        have_held = true;
                     }
+                    if (!held.end) {  // its turn: the window before it has been enqueued (on any engine)
+                        std::unique_lock<std::mutex> lk(R.m);
+                        if (enq.empty()) R.cv.wait(lk, [&] { return R.stopped || R.next_enqueue == held.id; });
+                        if (R.stopped) {
+                            stop_now = true;
+                            break;
+                        }
+                        if (R.next_enqueue != held.id) break;  // (launch the front window first)
+                    }
+                    const RawMulti::Win w = held;
+                    have_held = false;
                     if (!w.end) {
                         fq_raw_window rw{};
                         for (int m = 0; m < R.mates; ++m) {
@@ -1612,12 +1632,15 @@ struct Lane {
                             R.free_stages.push(w.stage);
                             throw std::runtime_error(std::string("fq_engine_raw_enqueue: ") + fq_engine_last_error(e));
                         }
+                        std::lock_guard<std::mutex> lk(R.m);
+                        R.next_enqueue = w.id + 1;
+                        R.cv.notify_all();
                     } else {
                         input_done = true;
                     }
                     enq.push_back(w);
                 }
-                if (enq.empty()) break;
+                if (stop_now || enq.empty()) break;
                 const RawMulti::Win w = enq.front();
                 {
                     std::unique_lock<std::mutex> lk(R.m);
