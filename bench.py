@@ -249,6 +249,11 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             tool = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
             cmd = [tool, "-i", big[0], "-I", big[1], "-o", "/dev/null", "-O", "/dev/null", *extra, "-w", str(workers),
                    "-J", os.path.join(tmp, "amd.json"), "-H", os.path.join(tmp, "amd.html")]
+            # one untimed run first, on the small sample: the binary's first start on a box (its
+            # libraries and code objects read in, the GPU's first process setup) is not the pipeline
+            warm = [tool, "-i", small[0], "-I", small[1], "-o", "/dev/null", "-O", "/dev/null", *extra, "-w", str(workers),
+                    "-J", os.path.join(tmp, "warm.json"), "-H", os.path.join(tmp, "warm.html")]
+            subprocess.run(warm if small else cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
             runs = []  # three runs (the copy pipeline's run-to-run spread is wide): the median is reported
             for _ in range(3):
                 t0 = time.perf_counter()

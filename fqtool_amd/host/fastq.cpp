@@ -73,22 +73,39 @@ ByteBuf& ByteBuf::operator=(ByteBuf&& o) noexcept {
     return *this;
 }
 
+extern std::atomic<uint64_t> g_pinned_bytes;
+
 void ByteBuf::release() {
     if (!p_) return;
-    if (is_pinned_) fq_host_free(p_);
+    if (is_pinned_) {
+        fq_host_free(p_);
+        g_pinned_bytes -= cap_;
+    }
     else delete[] p_;
     p_ = nullptr;
     cap_ = size_ = 0;
     is_pinned_ = false;
 }
 
+std::atomic<uint64_t> g_pinned_regrows{0}, g_pinned_bytes{0};
+
 void ByteBuf::reserve(size_t n) {
     if (n <= cap_) return;
     char* q = nullptr;
     bool pinned = false;
     if (want_pinned_) {
+        // Page-locked buffers grow by at least 1/8 and to whole 2 MiB pages (fq_host_alloc maps
+        // those anyway): a regrowth frees the old buffer, and unregistering page-locked memory
+        // waits for the device to go idle, so a buffer that grows by a little for every slightly
+        // larger window would stall the pipeline each time.
+        if (is_pinned_) {
+            n = std::max(n, cap_ + cap_ / 8);
+            ++g_pinned_regrows;
+        }
+        n = (n + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
         void* v = nullptr;
         if (fq_host_alloc(n, &v) == FQ_OK) {
+            g_pinned_bytes += n;
             q = static_cast<char*>(v);
             pinned = true;
         } else {

@@ -950,7 +950,7 @@ struct RawMulti {
     int G = 1, mates = 1;
     int fd[2] = {-1, -1};
     uint64_t size[2] = {0, 0};
-    uint64_t wcap = (uint64_t)64 << 20;
+    uint64_t wcap = (uint64_t)48 << 20;
     std::vector<std::unique_ptr<RawStage>> stages;
     Queue<int> free_stages{1024};
     std::vector<std::unique_ptr<Queue<Win>>> wq;  // per engine, windows in id order
@@ -1255,9 +1255,11 @@ struct Lane {
             size[m] = (uint64_t)st.st_size;
             (void)posix_fadvise(fd[m], 0, 0, POSIX_FADV_SEQUENTIAL);
         }
-        // windows of up to 64 MiB per mate (a pack of `target` 2x150 pairs is ~45 MiB), 16 MiB of
+        // windows of up to 48 MiB per mate (a pack of `target` 2x150 pairs is ~45 MiB; longer reads
+        // make smaller packs: every page-locked byte costs ~40 ms/GiB again when the process exits,
+        // tools/micro/exit_cost), 16 MiB of
         // carry (partial records, the mates' imbalance); six windows in the engine at once
-        const uint64_t wcap = (uint64_t)64 << 20, ccap = (uint64_t)16 << 20;
+        const uint64_t wcap = (uint64_t)48 << 20, ccap = (uint64_t)16 << 20;
         // records-only egress (FQ_RAW_EGRESS=host): the engine sends back records and line offsets,
         // the formatter writes the output from the staging window, which then keeps the carry
         // capacity free in front of the window bytes (the device buffer's layout)
@@ -1907,7 +1909,7 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
     } teardown{t0, t0, std::getenv("FQ_TIMING") != nullptr};
     try {
         const bool paired = o.paired();
-        // (raw streams: packs of 128 Ki pairs keep six windows' copies queued in 64 MiB windows)
+        // (raw streams: packs of 128 Ki pairs keep six windows' copies queued in 48 MiB windows)
         const size_t pack_n = o.pack_pairs ? o.pack_pairs : std::max<size_t>(o.max_reads_in_pack, 131072);
         int est = std::max(o.est_seq_len1, paired ? o.est_seq_len2 : 0);
         const std::vector<int> devices = o.device_list();
@@ -2204,6 +2206,14 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
             std::to_string(lanes[0]->first_submit) + " s, pipeline done at " +
             std::to_string(pipeline_done_s) +
             " s; JSON report " + o.json_file + ", HTML report " + o.html_file);
+        if (std::getenv("FQ_TIMING_MONO")) {  // (profiling: steady-clock stamps, to time exec and exit from outside)
+            auto mono = [](std::chrono::steady_clock::time_point t) {
+                return std::to_string(std::chrono::duration<double>(t.time_since_epoch()).count());
+            };
+            extern std::atomic<uint64_t> g_pinned_regrows, g_pinned_bytes;
+            log("fqtool-amd mono: t0 " + mono(t0) + " end " + mono(std::chrono::steady_clock::now()) + " pinned " +
+                std::to_string(g_pinned_bytes.load() >> 20) + " MiB, regrown " + std::to_string(g_pinned_regrows.load()) + " times");
+        }
         // Everything is written.  The process ends here: the teardown (page-locked packs and
         // windows, engines, the pool's threads) only returns memory the exit returns anyway, and
         // took 0.15-0.2 s of the command's wall time (FQ_TIMING=1 keeps it, and times it).

@@ -93,14 +93,20 @@ def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
         k, v = tok.split("=", 1)
         env[k] = v
         cmd.remove(tok)
+    env["FQ_TIMING_MONO"] = "1"  # (the tool's steady-clock stamps: exec and exit time from outside)
     t0 = time.perf_counter()
+    m0 = time.monotonic()
     p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    m1 = time.monotonic()
     wall = time.perf_counter() - t0
     if p.returncode != 0:
         raise SystemExit(f"{tag} failed rc={p.returncode}: {p.stderr[-2000:]}")
     m = re.search(r"fqtool-amd: (.*)", p.stderr)
     t = re.search(r"fqtool-amd timing: (.*)", p.stderr)
     ec = re.findall(r"fq_engine_create: (.*)", p.stderr)  # (FQ_ENGINE_TIMING=1)
+    mm = re.search(r"fqtool-amd mono: t0 ([\d.]+) end ([\d.]+)(.*)", p.stderr)
+    if mm:  # before the tool's clock starts (exec, loading, static init) and after its last line (exit)
+        ec.append(f"exec {float(mm.group(1)) - m0:.3f} s, exit {m1 - float(mm.group(2)):.3f} s;{mm.group(3)}")
     return wall, (m.group(1) if m else "(no fqtool-amd summary line)") + ((" | " + t.group(1)) if t else "") + \
         ((" | engine: " + "; ".join(ec)) if ec else ""), o
 
