@@ -415,7 +415,12 @@ int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*
  * entries "u16 ad_len (little endian), u8 neg, then ad_len bytes of the read (neg 0) or u16
  * ad_pos (neg 1: the string is adapter[ad_pos, ad_pos + ad_len) of the mate's adapter parameter)";
  * one copy back per mate, of the pack's text_bytes[m] + 3 * pairs + 16 bytes (a record's output
- * plus its entry is at most its input + 3 bytes). */
+ * plus its entry is at most its input + 3 bytes).
+ * Several engines on one GPU (one PCIe link): a window's host-to-device copies wait for the last
+ * ones any other engine of the process enqueued on that device, and a pack's copies back likewise,
+ * so copies run one after another in call order at the link's full rate; a caller dealing one
+ * stream's windows over such engines enqueues (and launches) them in stream order.  Engines on
+ * different GPUs never wait for each other. */
 typedef struct fq_raw_window {
     const char* bytes[2]; /* mate m's next input bytes (bytes[1]: PE only) */
     uint64_t n[2];        /* their count, <= the window capacity given to fq_engine_raw_begin */
