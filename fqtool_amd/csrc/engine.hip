@@ -115,6 +115,13 @@ struct fq_engine {
 
 static std::string g_create_error;
 
+// FQ_ENGINE_TIMING=1: creation steps and the raw stream's one-time set-up on stderr (profiling)
+static bool engine_timing() {
+    static const bool on = std::getenv("FQ_ENGINE_TIMING") != nullptr;
+    return on;
+}
+static double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
 // Raw-window copies of the engines that share one GPU (and so one PCIe link) run one after another
 // in call order: each engine's host-to-device copies wait for the last one another engine enqueued
 // on the device (and likewise its device-to-host copies).  Left to share the link, the copies of a
@@ -238,7 +245,7 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     std::string why;
     if (validate_params(params, why) != FQ_OK) return fail(nullptr, FQ_E_INVALID, why);
     // FQ_ENGINE_TIMING=1: the creation's steps on stderr (profiling: start-up of the tool)
-    static const bool timing = std::getenv("FQ_ENGINE_TIMING") != nullptr;
+    const bool timing = engine_timing();
     const auto t0 = std::chrono::steady_clock::now();
     auto stamp = [&](const char* what) {
         if (timing)
@@ -689,6 +696,13 @@ int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap) {
     if (e->p.correction_enabled || e->p.umi_front1 > 0 || e->p.umi_front2 > 0 ||
         (e->p.merge_enabled && e->p.discard_unmerged))
         return fail(e, FQ_E_INVALID, "raw streams take no -c, UMI or --discard_unmerged options");
+    const double tb = engine_timing() ? now_s() : 0;
+    struct Stamp {
+        double t;
+        ~Stamp() {
+            if (t > 0) std::fprintf(stderr, "fq_engine_raw_begin: %.2f ms\n", 1e3 * (now_s() - t));
+        }
+    } stamp{tb};
     carry_cap = (carry_cap + 4095) / 4096 * 4096;
     if (!window_cap || carry_cap + window_cap + 4096 >= (1ull << 31) || e->max_batch <= 0)
         return fail(e, FQ_E_INVALID, "raw window / carry capacity out of range");
@@ -719,8 +733,11 @@ int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w) {
     int rc = retire_slot(e, k);
     if (rc != FQ_OK) return rc;
     Slot& s = e->slots[k];
+    const bool fresh = !s.raw_ready;
+    const double ts = fresh && engine_timing() ? now_s() : 0;
     if ((rc = alloc_slot(e, s)) != FQ_OK) return rc;
     if ((rc = ensure_raw(e, s)) != FQ_OK) return rc;
+    if (ts > 0) std::fprintf(stderr, "fq_engine_raw_enqueue: slot %d set up in %.2f ms\n", k, 1e3 * (now_s() - ts));
     {
         LinkChain& lc = link_chain(e->device);
         std::lock_guard<std::mutex> g(lc.m);

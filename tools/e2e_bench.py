@@ -104,6 +104,10 @@ def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
     m = re.search(r"fqtool-amd: (.*)", p.stderr)
     t = re.search(r"fqtool-amd timing: (.*)", p.stderr)
     ec = re.findall(r"fq_engine_create: (.*)", p.stderr)  # (FQ_ENGINE_TIMING=1)
+    rb = re.findall(r"fq_engine_raw_begin: ([\d.]+) ms", p.stderr)
+    rs = [float(x) for x in re.findall(r"fq_engine_raw_enqueue: slot \d+ set up in ([\d.]+) ms", p.stderr)]
+    if rb or rs:
+        ec.append(f"raw_begin {'+'.join(rb)} ms, {len(rs)} raw slots set up in {sum(rs):.1f} ms (max {max(rs or [0]):.1f})")
     mm = re.search(r"fqtool-amd mono: t0 ([\d.]+) end ([\d.]+)(.*)", p.stderr)
     if mm:  # before the tool's clock starts (exec, loading, static init) and after its last line (exit)
         ec.append(f"exec {float(mm.group(1)) - m0:.3f} s, exit {m1 - float(mm.group(2)):.3f} s;{mm.group(3)}")
