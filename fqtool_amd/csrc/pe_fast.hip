@@ -111,6 +111,12 @@ namespace {
 #ifndef FQ_EXO3
 #define FQ_EXO3 1  // staging: exotic bytes OR-accumulated with one v_bitop3 (full rate) instead of v_sad_u8
 #endif
+#ifndef FQ_PG4
+#define FQ_PG4 1  // polyG: the all-G groups at the scan's start (a G tail) passed over by a light loop
+#endif
+#ifndef FQ_PG3
+#define FQ_PG3 1  // polyG: the scan loop loads group g+1's column words before deciding group g
+#endif
 #ifndef FQ_PG2
 #define FQ_PG2 1  // polyG: group 0 decided without the loop when the break is the second non-G base
 #endif
@@ -644,12 +650,13 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, in
             if (!rc) x = __builtin_bitreverse32(x) >> 1;  // forward window -> scan order
             return x;
         };
+        uint32_t xg = nong(0);  // group g's non-G mask (group 0 first; later groups loaded one ahead)
 #if FQ_PG2
         // Group 0 decides almost every read: while the allowance is 1 (scan indices < 2 per - 1) the
         // scan breaks at the second non-G base; the loop below runs only for the reads it leaves open
         // (a polyG tail, or per < 8).
         if (maxMM >= 1) {
-            const uint32_t valid = posmask(n), x = nong(0) & valid, x2 = x & (x - 1u);
+            const uint32_t valid = posmask(n), x = xg & valid, x2 = x & (x - 1u);
             const int s2 = (__ffs(x2) - 1) >> 1;
             if (x2 && (maxMM == 1 || s2 + 1 < 2 * per)) {
                 iend = s2;
@@ -658,9 +665,26 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, in
             }
         }
 #endif
-        for (int g = 0; 16 * g < n && iend == n; ++g) {
+        int g = 0;
+#if FQ_PG4
+        // A polyG tail (the reads the shortcut above leaves open): its all-G groups change nothing
+        // but firstGpos, so they are passed over at ~16 VALU a group (the loop below spends ~45)
+        if (iend == n) {
+            while (16 * (g + 1) < n && (xg & posmask(n - 16 * g)) == 0u) xg = nong(++g);
+            if (g > 0) lastG = 16 * g - 1;  // (scan indices below 16 g are all G)
+        }
+#endif
+        for (; 16 * g < n && iend == n; ++g) {
             const uint32_t valid = posmask(n - 16 * g);
-            uint32_t x = nong(g) & valid;
+#if FQ_PG3
+            uint32_t x = xg & valid;
+            // the next group's column words are requested before this group is decided (a G tail
+            // spans several groups, and each LDS round trip otherwise stalls the few lanes that
+            // scan -- and with them their wave); past the window they are masked off by `valid`
+            xg = nong(g + 1);
+#else
+            uint32_t x = (g ? nong(g) : xg) & valid;
+#endif
             uint32_t gm = ~x & valid;  // G bases of the group
             const int a0 = allowed(16 * g + 1);  // allowance at the group start
             if (cum + __popc(x) > a0) {

@@ -88,6 +88,9 @@ void ByteBuf::release() {
 }
 
 std::atomic<uint64_t> g_pinned_regrows{0}, g_pinned_bytes{0};
+static std::mutex g_retired_m;
+static std::vector<void*> g_retired;  // page-locked blocks outgrown mid-run (freed by the exit)
+static size_t g_retired_bytes = 0;
 
 void ByteBuf::reserve(size_t n) {
     if (n <= cap_) return;
@@ -102,6 +105,7 @@ void ByteBuf::reserve(size_t n) {
             n = std::max(n, cap_ + cap_ / 8);
             ++g_pinned_regrows;
         }
+        retire_pinned_ = is_pinned_;  // (the old block is kept, see below)
         n = (n + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
         void* v = nullptr;
         if (fq_host_alloc(n, &v) == FQ_OK) {
@@ -115,6 +119,20 @@ void ByteBuf::reserve(size_t n) {
     if (!q) q = new char[n];
     if (size_) std::memcpy(q, p_, size_);
     const size_t keep = size_;
+    if (retire_pinned_ && is_pinned_) {
+        // Unregistering page-locked memory waits for the device to go idle: a buffer that grows
+        // mid-run (a pack's output, a staging window) leaves its old block registered until the
+        // process ends instead of draining the pipeline here (up to 256 MiB of such blocks)
+        std::lock_guard<std::mutex> g(g_retired_m);
+        if (g_retired_bytes + cap_ <= ((size_t)256 << 20)) {
+            g_retired.push_back(p_);
+            g_retired_bytes += cap_;
+            p_ = nullptr;
+            cap_ = size_ = 0;
+            is_pinned_ = false;
+        }
+    }
+    retire_pinned_ = false;
     release();
     p_ = q;
     size_ = keep;

@@ -70,7 +70,7 @@ class ByteBuf {
     void release();
     char* p_ = nullptr;
     size_t size_ = 0, cap_ = 0;
-    bool want_pinned_ = false, is_pinned_ = false;
+    bool want_pinned_ = false, is_pinned_ = false, retire_pinned_ = false;
 };
 
 // Array of T over a ByteBuf (read lengths, result records): pinned like its buffer.

@@ -395,6 +395,17 @@ class Queue {  // bounded FIFO between pipeline threads; push/pop return at once
         not_full_.notify_one();
         return true;
     }
+    // pop of the most recently pushed element (a stack of recycled buffers: the warm ones go out
+    // again first, the cold ones stay untouched -- never page-locked -- unless demand needs them)
+    bool pop_recent(T& v) {
+        std::unique_lock<std::mutex> l(m_);
+        not_empty_.wait(l, [&] { return !q_.empty() || closed_; });
+        if (q_.empty()) return false;
+        v = std::move(q_.back());
+        q_.pop_back();
+        not_full_.notify_one();
+        return true;
+    }
     // 1: v taken; 0: empty (not closed); -1: closed and drained
     int try_pop(T& v) {
         std::lock_guard<std::mutex> l(m_);
@@ -1449,7 +1460,7 @@ struct Lane {
                     wins.pop_front();
                     std::unique_ptr<Pack> pk;
                     const auto p0 = std::chrono::steady_clock::now();
-                    if (!spare.pop(pk)) throw Stopped();
+                    if (!spare.pop_recent(pk)) throw Stopped();
                     raw_pack_wait_s += since(p0);
                     pk->clear();
                     pk->raw = true;
@@ -1664,7 +1675,7 @@ struct Lane {
                 enq.pop_front();
                 std::unique_ptr<Pack> pk;
                 const auto p0 = std::chrono::steady_clock::now();
-                if (!spare.pop(pk)) throw Stopped();
+                if (!spare.pop_recent(pk)) throw Stopped();
                 raw_pack_wait_s += since(p0);
                 pk->clear();
                 pk->raw = true;
@@ -2040,7 +2051,7 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
                 std::unique_ptr<Pack> pk;
                 for (;;) {
                     const auto w0 = std::chrono::steady_clock::now();
-                    if (!spare.pop(pk)) break;
+                    if (!spare.pop_recent(pk)) break;
                     spare_wait_s += since(w0);
                     if (!pr.next(*pk, pack_n, &pool)) break;
                     Lane& l = *lanes[(size_t)(pk->seq_no % (uint64_t)G)];

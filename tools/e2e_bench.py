@@ -166,6 +166,7 @@ def main():
     ap.add_argument("--variants", default=None, help="';'-separated list of --extra strings, each run in turn")
     ap.add_argument("--null-out", action="store_true", help="FASTQ outputs to /dev/null (as bench.py's e2e leg)")
     ap.add_argument("--workers-list", default=None, help="comma list of -w values to run (overrides --workers)")
+    ap.add_argument("--pause", type=float, default=0.0, help="seconds between fqtool-amd runs")
     ap.add_argument("--gz", default=None, choices=["bgzf", "gzip"], help="compressed inputs: BGZF or one gzip stream")
     args = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="fqe2e_")
@@ -185,6 +186,8 @@ def main():
         variants = args.variants.split(";") if args.variants else [args.extra]
         wl = [int(x) for x in args.workers_list.split(",")] if args.workers_list else [args.workers]
         for _, w, v in [(r, w, v) for v in variants for w in wl for r in range(args.repeat)]:
+            if args.pause:
+                time.sleep(args.pause)
             extra = (["--devices", args.devices] if args.devices else []) + v.split()
             wall, inner, o_ours = run(ours, r1, r2, tmp, "amd", args.config, w, extra, args.null_out)
             line = {"tool": "fqtool-amd", "config": args.config, "pairs": args.pairs, "fastq_GB": round(gb, 3),
