@@ -210,6 +210,9 @@ def port_baseline(abi, pairs, first, threads):
                       f"(no -w cap), in-memory packs, wall {dt:.2f}s"}
 
 
+E2E_PAUSE_S = 2.0  # between e2e runs (host_legs)
+
+
 def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
     """Rank 0 at N=1, after the timed region: both host-side legs on FASTQ files of the same
     synthetic workload (fixed-width records, page cache):
@@ -256,6 +259,11 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             subprocess.run(warm if small else cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
             runs = []  # three runs (the copy pipeline's run-to-run spread is wide): the median is reported
             for _ in range(3):
+                # each run starts as a separate invocation would: the kernel's GPU driver releases a finished
+                # process's GPU memory and page-locked pages after its exit, and a process started
+                # while that is still going finds HIP's start-up 0.1-0.15 s slower
+                # (profiles/r04_e2e_pause_50M.txt)
+                time.sleep(E2E_PAUSE_S)
                 t0 = time.perf_counter()
                 p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
                 dt = time.perf_counter() - t0
@@ -266,7 +274,8 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             gb = (os.path.getsize(big[0]) + os.path.getsize(big[1])) / 1e9
             return {"value": round(2 * e2e_pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": e2e_pairs,
                     "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
-                    "runs_wall_s": [round(r[0], 3) for r in runs], "options": " ".join(extra),
+                    "runs_wall_s": [round(r[0], 3) for r in runs], "pause_between_runs_s": E2E_PAUSE_S,
+                    "options": " ".join(extra),
                     "path": e2e_path(tool_log),
                     "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
 

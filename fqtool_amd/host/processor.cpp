@@ -1493,6 +1493,9 @@ struct Lane {
                             size_t cap = m < mates ? (size_t)(cin[m] + w.n[m] + 4 * (uint64_t)target + 64) : 0;
                             if (merge && m == 0)  // (-m: the merged stream of both mates' text)
                                 cap = (size_t)(cin[0] + w.n[0] + cin[1] + w.n[1] + 28 * (uint64_t)target + 64);
+                            // (1/8 headroom when the page-locked buffer is first made or outgrown:
+                            // windows vary by a few percent, and a regrowth registers anew)
+                            pk->out_text[m].reserve(cap + cap / 8);
                             pk->out_text[m].resize_uninit(cap);
                             pk->rout.text.text[m] = m < mates ? pk->out_text[m].data() : nullptr;
                         }
@@ -1687,6 +1690,7 @@ struct Lane {
                     size_t cap = m < R.mates ? (size_t)(w.n[m] + 4 * (uint64_t)target + 64) : 0;
                     if (merge && m == 0)  // (-m: the merged stream of both mates' text)
                         cap = (size_t)(w.n[0] + w.n[1] + 28 * (uint64_t)target + 64);
+                    pk->out_text[m].reserve(cap + cap / 8);  // (headroom: see run_raw)
                     pk->out_text[m].resize_uninit(cap);
                     pk->rout.text.text[m] = m < R.mates ? pk->out_text[m].data() : nullptr;
                 }
