@@ -128,8 +128,11 @@ def test_text_pack_last_record_without_terminator(lib, oracle):
     assert got == exp
 
 
-def test_text_pack_refuses_merge(lib, oracle):
+def test_text_pack_refuses_discard_unmerged(lib, oracle):
+    # -m runs on text packs (the merged stream, tests/test_host_e2e.py); with --discard_unmerged the
+    # unmerged pairs go to out1 / out2 instead, which only the host packs write
     p = config("C4", max_cycles=512)
+    p.discard_unmerged = 1
     pk = synth_pack(oracle, 64, True)
     rng = random.Random(1)
     texts = [fastq_text(pk, m, rng) for m in (1, 2)]
