@@ -2021,8 +2021,13 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
                 // staging: per engine the packs in flight (4), the windows enqueued (3) and queued
                 // for it (2), plus a few for the reader to run ahead (a stage comes back only when its
                 // pack completes: fewer starve the reader); the first is handed out at once, the
-                // others page-locked on a helper thread
-                const int kStages = G * 9 + 4;
+                // others page-locked on a helper thread.  Engines sharing a GPU share its link, so
+                // beyond the first engine of a GPU three more stages each (page-locked memory is
+                // paid again at the exit, ~40 ms per GiB)
+                std::vector<int> devs(devices.begin(), devices.end());
+                std::sort(devs.begin(), devs.end());
+                const int P = (int)(std::unique(devs.begin(), devs.end()) - devs.begin());
+                const int kStages = P * 9 + 4 + 3 * (G - P);
                 for (int i = 0; i < kStages; ++i) R.stages.emplace_back(new RawStage);
                 R.free_stages.push(0);
                 rm_warmer = std::thread([&R, kStages] {
