@@ -111,6 +111,9 @@ namespace {
 #ifndef FQ_EXO3
 #define FQ_EXO3 1  // staging: exotic bytes OR-accumulated with one v_bitop3 (full rate) instead of v_sad_u8
 #endif
+#ifndef FQ_STG2
+#define FQ_STG2 1  // staging: the chunk's code and N-flag words from two nibble-packed key words
+#endif
 #ifndef FQ_PG4
 #define FQ_PG4 1  // polyG: the all-G groups at the scan's start (a G tail) passed over by a light loop
 #endif
@@ -1225,6 +1228,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
                 const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
                 uint32_t cc = 0, nn4 = 0, lr = 0;
+                uint32_t kkj[4];  // (FQ_STG2) the four dwords' 3-bit keys
                 // bases of this chunk still in the read; opaque, or the masks of all ten chunks
                 // (functions of L alone) are computed up front and kept live across the loop
                 int Lk = L - 16 * k;
@@ -1266,8 +1270,12 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     // which runs on the XTRA instantiation (and the merge variant)
                     if (!LEAN && (XTRA || MERGE)) tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);
                     if (!LEAN) lr |= ~(qm + limr) & (0x80808080u & bm);         // q < cut_right threshold
+#if FQ_STG2
+                    kkj[j] = kk;
+#else
                     cc |= (kk & 0x03030303u) << (2 * j);
                     nn4 |= ((kk >> 2) & 0x01010101u) << (2 * j);
+#endif
                 };
                 if (full) {
 #pragma unroll
@@ -1276,6 +1284,19 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 #pragma unroll
                     for (int j = 0; j < 4; ++j) dword(j, std::false_type{});
                 }
+#if FQ_STG2
+                {
+                    // the keys of dwords 0 and 2 (1 and 3) share each byte in nibbles: code field j at
+                    // bits 2j of the byte and N flag j at bit 2j come out of two masked merges
+                    // (7 VALU for the chunk instead of ~18 in per-dword shifts)
+                    const uint32_t p02 = kkj[0] | (kkj[2] << 4), p13 = kkj[1] | (kkj[3] << 4);
+                    uint32_t c13;
+                    asm("v_lshlrev_b32 %0, 2, %1" : "=v"(c13) : "v"(p13));
+                    const uint32_t m33 = vk(0x33333333u);
+                    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xAC" : "=v"(cc) : "v"(m33), "v"(c13), "v"(p02));  // m33 ? p02 : c13
+                    nn4 = ((p02 >> 2) & 0x11111111u) | (p13 & 0x44444444u);
+                }
+#endif
                 if (!LEAN) lowr = shift_in_sign(lowr, lr | (0u - lr));  // (sign set iff lr != 0)
                 // N flags are kept only for positions inside the read (later passes rely on it);
                 // read 2's chunk is reversed: its positions inside the read are the high ones
