@@ -1281,10 +1281,12 @@ struct Lane {
         const size_t raw_ahead = 3;  // windows enqueued ahead of their launch (the copy-in queue)
         if (fq_engine_raw_begin(e, wcap, ccap) != FQ_OK)
             throw std::runtime_error(std::string("fq_engine_raw_begin: ") + fq_engine_last_error(e));
-        // in flight + enqueued + being filled, and four more so the window reader can run ahead
-        // of the packs (a stage comes back only when its pack completes)
+        // in flight + enqueued + being filled, and one more so the window reader can run ahead of
+        // the packs (a stage comes back only when its pack completes).  Ten stages ran the 50 M-pair
+        // pipeline as fast as thirteen (0.78-0.87 s vs 0.80-0.85 s) with ~0.3 GiB less page-locked
+        // memory to release at the exit (profiles/r04_e2e_stages_10_13.txt)
         const char* st_env = std::getenv("FQ_RAW_STAGES");  // (profiling)
-        const int kStages = std::max(raw_depth + (int)raw_ahead + 2, st_env ? std::atoi(st_env) : raw_depth + (int)raw_ahead + 6);
+        const int kStages = std::max(raw_depth + (int)raw_ahead + 2, st_env ? std::atoi(st_env) : raw_depth + (int)raw_ahead + 3);
         // The first new stage is handed out at once; the others are made page-locked (~0.06 s/GiB)
         // on a helper thread and handed out as they become ready, so their registration overlaps
         // the first windows instead of stalling the reader.

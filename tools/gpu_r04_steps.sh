@@ -21,6 +21,7 @@ for st in ${STEPS:-}; do
   e2e_multi) timeout -k 10 600 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 --variants "--devices 0;--devices 0,0;--devices 0,0,0" > gpurun_out/e2e_multi.txt 2>&1 || exit 1 ;;
   e2e_pause) timeout -k 10 500 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 --pause ${E2E_PAUSE:-2} > gpurun_out/e2e_pause.txt 2>&1 || exit 1 ;;
   e2e_numa) timeout -k 10 700 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-50000000} --no-ref --null-out --repeat 3 --pause 2 --variants "FQ_NUMA=0;FQ_NUMA=1" > gpurun_out/e2e_numa.txt 2>&1 || exit 1 ;;
+  e2e_var) timeout -k 10 900 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-50000000} --no-ref --null-out --repeat ${E2E_REPEAT:-3} --pause 2 --variants "${E2E_VARIANTS}" > gpurun_out/e2e_var.txt 2>&1 || exit 1 ;;
   e2e_noegress) FQ_PROF_NO_EGRESS=1 timeout -k 10 500 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 > gpurun_out/e2e_noegress.txt 2>&1 || exit 1 ;;
   e2e_hostegress) FQ_RAW_EGRESS=host timeout -k 10 500 python -u tools/e2e_bench.py --pairs ${E2E_PAIRS:-20000000} --no-ref --null-out --repeat 3 > gpurun_out/e2e_hostegress.txt 2>&1 || exit 1 ;;
   htests_hostegress) FQ_RAW_EGRESS=host timeout -k 10 900 python -u -m pytest tests/test_host_e2e.py -m gpu -k "${HTESTS:-raw_stream}" -x -q --timeout 300 --timeout-method thread > gpurun_out/pt_host_hostegress.log 2>&1 || exit 1 ;;
