@@ -129,6 +129,15 @@ namespace {
 #ifndef FQ_PLAUNDER
 #define FQ_PLAUNDER 1  // re-read fq_params / fq_batch from the kernarg segment every tile (SGPR pressure)
 #endif
+#ifndef FQ_ST_SH64
+#define FQ_ST_SH64 1  // removed-mode Stats: slot nibbles positioned two at a time by 64-bit shifts
+#endif
+#ifndef FQ_ST_KM2
+#define FQ_ST_KM2 1  // removed-mode Stats: kept mask by one med3 + one bitop3 per word, 64-bit spread
+#endif
+#ifndef FQ_ST_PF2
+#define FQ_ST_PF2 1  // removed-mode Stats: column words requested two chunks ahead (no wait on the atomics)
+#endif
 #ifndef FQ_PREFETCH
 #define FQ_PREFETCH 0  // profiling: after staging, pull the first FQ_PREFETCH chunks of the wave's next tile
                        // toward L2 with LDS-DMA loads (0: off; measured slower at 10)
@@ -1977,7 +1986,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             // this lane's column word of forward chunk F: cw0 + F * cstep (read 2's column is reversed)
             const uint32_t* cwp = col + lane_x + (rc ? (kChunks - 1) * 64 : 0);
             const int cstep = rc ? -64 : 64;
-            auto fwd_at = [&](const uint32_t* wp_) {
+            [[maybe_unused]] auto fwd_at = [&](const uint32_t* wp_) {
                 uint32_t cw = wp_[kFC * 64], nw = wp_[kFN * 64];
                 if (rc) {
                     cw = pairrev(cw);
@@ -1986,27 +1995,79 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 }
                 return Fwd{cw, nw};
             };
+#if FQ_ST_PF2
+            // raw column words of chunks F and F + 1 (requested two chunks ahead: the wait for
+            // chunk F's words then does not cover the atomics issued since)
+            uint32_t rw0c = cwp[kFC * 64], rw0n = cwp[kFN * 64];
+            uint32_t rw1c = cwp[cstep + kFC * 64], rw1n = cwp[cstep + kFN * 64];
+            cwp += cstep;
+#else
             Fwd fn = fwd_at(cwp);
+#endif
+#if FQ_ST_KM2
+            const uint32_t m0f = vk(0x0F0F0F0Fu), m33 = vk(0x33333333u), m44 = vk(0x44444444u);
+#endif
             // nibble prefix masks from one 64-bit shift: ~(~0 << 4 * clamp(len, 0, 16)), the
             // 64th bit never needed (nibble 15's top bit is 0 in 0x4444... and 0xAAAA... masks)
             const int w4 = 4 * wlen, l4 = 4 * L;
 #pragma unroll
             for (int F = 0; F < kChunks; ++F) {
                 if (F < nch) {  // wave-uniform; positions >= L are dummies
+#if FQ_ST_PF2
+                    uint32_t fc = rw0c, fnw = rw0n;
+                    if (rc) {
+                        fc = pairrev(fc);
+                        fnw = pairrev(fnw);
+                        fc ^= 0xAAAAAAAAu & ~(fnw << 1);  // complement back, N stays code 3
+                    }
+                    const Fwd f{fc, fnw};
+                    rw0c = rw1c;
+                    rw0n = rw1n;
+                    if (F + 2 < kChunks) {
+                        cwp += cstep;
+                        rw1c = cwp[kFC * 64];
+                        rw1n = cwp[kFN * 64];
+                    }
+#else
                     const Fwd f = fn;
+#endif
                     const uint32_t q0 = qb[F % (kSA + 1)].x, q1 = qb[F % (kSA + 1)].y, q2 = qb[F % (kSA + 1)].z,
                                    q3 = qb[F % (kSA + 1)].w;
                     if (F + kSA < kChunks) qb[(F + kSA) % (kSA + 1)] = qchunk(min(F + kSA, nchunks - 1));
                     // (chunks from nch on are zero-filled by staging: no clamp)
+#if !FQ_ST_PF2
                     if (F + 1 < kChunks) {
                         cwp += cstep;
                         fn = fwd_at(cwp);
                     }
+#endif
                     const int vl = L - 16 * F;
                     // slot 4 * kept + code; an N (code 3) reads as a G here
+#if FQ_ST_KM2
+                    // kept nibbles: ~(~0 << s), s = clamp(4 wlen - 64 F, 0, 63) (one v_med3); the
+                    // codes spread to nibbles for both halves at once by 64-bit shifts, masked by
+                    // one v_bitop3 per word, the kept bit or-ed in by another
+                    int sk;
+                    asm("v_med3_i32 %0, %1, 0, 63" : "=v"(sk) : "v"(w4 - 64 * F));
+                    const unsigned long long km = ~0ull << sk;
+                    uint32_t lo, hi;
+                    {
+                        const uint32_t x0 = __builtin_amdgcn_perm(f.c, f.c, 0x0c010c00u);  // code bytes 0, 1 to bytes 0, 2
+                        const uint32_t x1 = __builtin_amdgcn_perm(f.c, f.c, 0x0c030c02u);  // code bytes 2, 3
+                        unsigned long long X = (unsigned long long)x1 << 32 | x0, X4, X2;
+                        asm("v_lshlrev_b64 %0, 4, %1" : "=v"(X4) : "v"(X));
+                        const uint32_t y0 = (x0 | (uint32_t)X4) & m0f, y1 = (x1 | (uint32_t)(X4 >> 32)) & m0f;
+                        X = (unsigned long long)y1 << 32 | y0;
+                        asm("v_lshlrev_b64 %0, 2, %1" : "=v"(X2) : "v"(X));
+                        const uint32_t z0 = (y0 | (uint32_t)X2) & m33, z1 = (y1 | (uint32_t)(X2 >> 32)) & m33;
+                        lo = (~(uint32_t)km & m44) | z0;
+                        hi = (~(uint32_t)(km >> 32) & m44) | z1;
+                    }
+#else
                     const unsigned long long km = ~(~0ull << min(max(w4 - 64 * F, 0), 63));
                     uint32_t lo = spread2to4(f.c) + ((uint32_t)km & 0x44444444u);
                     uint32_t hi = spread2to4(f.c >> 16) + ((uint32_t)(km >> 32) & 0x44444444u);
+#endif
 #if FQ_NFOLD
                     // N bases: their slot kRNSlot + 4 * kept is the G slot + 5, one nibble add (staging
                     // kept N flags only inside the read)
@@ -2059,13 +2120,32 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     // slot nibble t % 8 at bits 8-11: a right shift of the word (nibbles 2-7) or of the
                     // word shifted left by 8 (nibbles 0-1; one 64-bit shift gives both words' copies,
                     // the high one with klo's top byte in its low bits, masked off)
+#if FQ_ST_SH64
+                    // nibble u of both words to bits 8-11 by one 64-bit shift of {khi, klo} (its low
+                    // word: klo's nibble u, its high word: khi's): steps t and t + 8 share it
+                    const unsigned long long K = (unsigned long long)khi << 32 | klo;
+                    // (one v_lshlrev_b64 / v_lshrrev_b64 each, full rate; left to itself the compiler
+                    // splits them into a v_alignbit and a shift)
+                    unsigned long long Ks[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (u == 2) Ks[u] = K;
+                        else if (u < 2) asm("v_lshlrev_b64 %0, %2, %1" : "=v"(Ks[u]) : "v"(K), "i"(8 - 4 * u));
+                        else asm("v_lshrrev_b64 %0, %2, %1" : "=v"(Ks[u]) : "v"(K), "i"(4 * (u - 2)));
+                    }
+#else
                     const unsigned long long k8 = ((unsigned long long)khi << 32 | klo) << 8;
                     const uint32_t klo8 = (uint32_t)k8, khi8 = (uint32_t)(k8 >> 32);
+#endif
 #pragma unroll
                     for (int t = 0; t < 16; ++t) {
                         const int u = t & 7;
+#if FQ_ST_SH64
+                        const uint32_t ksh = t < 8 ? (uint32_t)Ks[u] : (uint32_t)(Ks[u] >> 32);
+#else
                         const uint32_t kw = u < 2 ? (t < 8 ? klo8 : khi8) : (t < 8 ? klo : khi);
                         const uint32_t ksh = u < 2 ? kw >> (4 * u) : kw >> (4 * (u - 2));
+#endif
                         // (byte 0 and 3 by one full-rate op, 1 and 2 by a bit-field extract)
                         const uint32_t qw = qr[t >> 2];
                         const uint32_t qv = (t & 3) == 0 ? qw & 0xFFu : (t & 3) == 3 ? qw >> 24 : __builtin_amdgcn_ubfe(qw, 8 * (t & 3), 8);
