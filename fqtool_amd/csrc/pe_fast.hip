@@ -138,6 +138,9 @@ namespace {
 #ifndef FQ_ST_PF2
 #define FQ_ST_PF2 1  // removed-mode Stats: column words requested two chunks ahead (no wait on the atomics)
 #endif
+#ifndef FQ_OV_SH64
+#define FQ_OV_SH64 1  // overlap candidates: planes realigned by 64-bit shifts (one block per pass)
+#endif
 #ifndef FQ_PREFETCH
 #define FQ_PREFETCH 0  // profiling: after staging, pull the first FQ_PREFETCH chunks of the wave's next tile
                        // toward L2 with LDS-DMA loads (0: off; measured slower at 10)
@@ -508,9 +511,22 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
         if (bk < kOvBlocks - 1) planes(L1, H1);
         else L1 = H1 = 0u;
         // mismatch vector of compared position j over the block's 32 offsets
+#if FQ_OV_SH64
+        const unsigned long long HA = (unsigned long long)H1 << 32 | H0, LA = (unsigned long long)L1 << 32 | L0;
+        auto shr64 = [](unsigned long long v, int j) -> uint32_t {
+            unsigned long long r;
+            asm("v_lshrrev_b64 %0, %2, %1" : "=v"(r) : "v"(v), "i"(j));
+            return (uint32_t)r;
+        };
+#endif
         auto m = [&](int j) -> uint32_t {
+#if FQ_OV_SH64
+            const uint32_t hs = j ? shr64(HA, j) : H0;
+            const uint32_t ls = j ? shr64(LA, j) : L0;
+#else
             const uint32_t hs = j ? __builtin_amdgcn_alignbit(H1, H0, j) : H0;
             const uint32_t ls = j ? __builtin_amdgcn_alignbit(L1, L0, j) : L0;
+#endif
             const uint32_t fh = (uint32_t)__builtin_amdgcn_sbfe((int)fu, 16 + j, 1);
             const uint32_t fl = (uint32_t)__builtin_amdgcn_sbfe((int)fu, j, 1);
             return (hs ^ fh) | (ls ^ fl);
