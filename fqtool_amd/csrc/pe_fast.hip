@@ -2011,15 +2011,19 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 }
                 return Fwd{cw, nw};
             };
-#if FQ_ST_PF2
-            // raw column words of chunks F and F + 1 (requested two chunks ahead: the wait for
-            // chunk F's words then does not cover the atomics issued since)
-            uint32_t rw0c = cwp[kFC * 64], rw0n = cwp[kFN * 64];
-            uint32_t rw1c = cwp[cstep + kFC * 64], rw1n = cwp[cstep + kFN * 64];
-            cwp += cstep;
-#else
-            Fwd fn = fwd_at(cwp);
-#endif
+            // PF2: raw column words of chunks F and F + 1 (requested two chunks ahead: the wait for
+            // chunk F's words then does not cover the atomics issued since).  Two more live VGPRs:
+            // the FULL non-merge variants would spill, so they read one chunk ahead.
+            constexpr bool kPf2 = FQ_ST_PF2 && (LEAN || (MERGE && !XTRA));
+            uint32_t rw0c = 0, rw0n = 0, rw1c = 0, rw1n = 0;
+            Fwd fn{0u, 0u};
+            if constexpr (kPf2) {
+                rw0c = cwp[kFC * 64], rw0n = cwp[kFN * 64];
+                rw1c = cwp[cstep + kFC * 64], rw1n = cwp[cstep + kFN * 64];
+                cwp += cstep;
+            } else {
+                fn = fwd_at(cwp);
+            }
 #if FQ_ST_KM2
             const uint32_t m0f = vk(0x0F0F0F0Fu), m33 = vk(0x33333333u), m44 = vk(0x44444444u);
 #endif
@@ -2029,34 +2033,31 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 #pragma unroll
             for (int F = 0; F < kChunks; ++F) {
                 if (F < nch) {  // wave-uniform; positions >= L are dummies
-#if FQ_ST_PF2
-                    uint32_t fc = rw0c, fnw = rw0n;
-                    if (rc) {
-                        fc = pairrev(fc);
-                        fnw = pairrev(fnw);
-                        fc ^= 0xAAAAAAAAu & ~(fnw << 1);  // complement back, N stays code 3
+                    Fwd f = fn;
+                    if constexpr (kPf2) {
+                        uint32_t fc = rw0c, fnw = rw0n;
+                        if (rc) {
+                            fc = pairrev(fc);
+                            fnw = pairrev(fnw);
+                            fc ^= 0xAAAAAAAAu & ~(fnw << 1);  // complement back, N stays code 3
+                        }
+                        f = Fwd{fc, fnw};
+                        rw0c = rw1c;
+                        rw0n = rw1n;
+                        if (F + 2 < kChunks) {
+                            cwp += cstep;
+                            rw1c = cwp[kFC * 64];
+                            rw1n = cwp[kFN * 64];
+                        }
                     }
-                    const Fwd f{fc, fnw};
-                    rw0c = rw1c;
-                    rw0n = rw1n;
-                    if (F + 2 < kChunks) {
-                        cwp += cstep;
-                        rw1c = cwp[kFC * 64];
-                        rw1n = cwp[kFN * 64];
-                    }
-#else
-                    const Fwd f = fn;
-#endif
                     const uint32_t q0 = qb[F % (kSA + 1)].x, q1 = qb[F % (kSA + 1)].y, q2 = qb[F % (kSA + 1)].z,
                                    q3 = qb[F % (kSA + 1)].w;
                     if (F + kSA < kChunks) qb[(F + kSA) % (kSA + 1)] = qchunk(min(F + kSA, nchunks - 1));
                     // (chunks from nch on are zero-filled by staging: no clamp)
-#if !FQ_ST_PF2
-                    if (F + 1 < kChunks) {
+                    if (!kPf2 && F + 1 < kChunks) {
                         cwp += cstep;
                         fn = fwd_at(cwp);
                     }
-#endif
                     const int vl = L - 16 * F;
                     // slot 4 * kept + code; an N (code 3) reads as a G here
 #if FQ_ST_KM2
