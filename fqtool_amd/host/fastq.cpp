@@ -278,9 +278,16 @@ bool FqReader::read(std::string& name, std::string& seq, std::string& strand, st
 // members are inflated in parallel into one buffer at their prefix-summed offsets, each checked
 // against its CRC32 and ISIZE.  The byte stream is the one gzread would give; any other .gz goes
 // through zlib's stream reader as in the reference (src/fqreader.cpp:3-16).
+//
+// Corrupt data: the reference reads gzip through gzread calls of `call` bytes (1 MiB,
+// src/fqreader.cpp:28-35), and the call during which zlib meets the error returns -1, so the
+// stream it sees ends at the start of that call: every earlier call's bytes, including the bad
+// member's bytes that zlib had written out before its CRC / ISIZE check or its data error.  Here the
+// bytes of a batch are handed out only up to the last call boundary before the batch's end until
+// the next batch is known to be good, so the cut can fall anywhere before a bad member.
 class BgzfSource {
    public:
-    static std::unique_ptr<BgzfSource> open(const std::string& path) {
+    static std::unique_ptr<BgzfSource> open(const std::string& path, size_t call) {
         const int fd = ::open(path.c_str(), O_RDONLY);
         if (fd < 0) return nullptr;
         struct stat st;
@@ -291,29 +298,50 @@ class BgzfSource {
         void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
         ::close(fd);
         if (m == MAP_FAILED) return nullptr;
-        std::unique_ptr<BgzfSource> b(new BgzfSource(static_cast<const unsigned char*>(m), (size_t)st.st_size));
+        std::unique_ptr<BgzfSource> b(new BgzfSource(static_cast<const unsigned char*>(m), (size_t)st.st_size,
+                                                     std::max<size_t>(call, 1)));
         if (!b->walk()) return nullptr;
         madvise(m, (size_t)st.st_size, MADV_SEQUENTIAL);
         return b;
     }
-    // up to `want` more bytes of the decompressed stream into dst; false on corrupt data, after the
-    // bytes of every member before the first bad one (in stream order) have been handed out
+    // up to `want` more bytes of the decompressed stream into dst; false on corrupt data, once the
+    // bytes the reference's gzread calls would have returned before the failing one are handed out
     bool read(char* dst, size_t want, size_t& got) {
         got = 0;
+        if (!started_) {
+            started_ = true;
+            fetch();
+        }
         while (got < want) {
-            if (pos_ == buf_.size()) {
-                if (bad_) return false;
-                if (!next_batch()) bad_ = true;  // buf_ holds the good members' prefix of the batch
-                if (buf_.empty()) {
-                    if (bad_) return false;
-                    break;  // end of the stream
-                }
+            if (q_.empty()) break;
+            Batch& c = q_.front();
+            if (pos_ == c.data.size()) {
+                q_.pop_front();
+                pos_ = 0;
+                if (q_.empty() && !done_) fetch();
                 continue;
             }
-            const size_t n = std::min(want - got, buf_.size() - pos_);
-            std::memcpy(dst + got, buf_.data() + pos_, n);
+            const size_t at = c.base + pos_;
+            if (at >= limit_) {
+                if (done_) break;
+                fetch();
+                continue;
+            }
+            const size_t n = std::min(std::min(want - got, c.data.size() - pos_), limit_ - at);
+            std::memcpy(dst + got, c.data.data() + pos_, n);
             pos_ += n;
             got += n;
+        }
+        // corrupt data: reported once, by the call that reaches the cut
+        if (bad_ && !reported_) {
+            while (!q_.empty() && pos_ == q_.front().data.size()) {
+                q_.pop_front();
+                pos_ = 0;
+            }
+            if (q_.empty() || q_.front().base + pos_ >= limit_) {
+                reported_ = true;
+                return false;
+            }
         }
         return true;
     }
@@ -327,7 +355,14 @@ class BgzfSource {
         size_t data, clen;  // deflate payload offset and length
         uint32_t crc, isize;
     };
-    BgzfSource(const unsigned char* m, size_t n) : map_(m), size_(n) {}
+    struct Batch {
+        std::string data;  // inflated bytes of the batch's members (the bad one's as far as zlib got)
+        size_t base = 0;   // stream offset of data[0]
+        bool ok = true;
+        size_t keep = 0;   // (!ok) stream offset where the reference's stream ends
+        bool last = true;  // no member after the batch
+    };
+    BgzfSource(const unsigned char* m, size_t n, size_t call) : map_(m), size_(n), call_(call) {}
     static uint32_t le16(const unsigned char* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
     static uint32_t le32(const unsigned char* p) { return le16(p) | le16(p + 2) << 16; }
     // the member chain from the headers (RFC 1952 header, BGZF 'BC' extra subfield)
@@ -357,43 +392,60 @@ class BgzfSource {
         }
         return !members_.empty();
     }
-    // the current batch is used up: take the one inflated ahead (or inflate one now), and start
-    // inflating the following batch while this one is read
-    bool next_batch() {
-        pos_ = 0;
-        bool ok = true;
-        if (ahead_.valid()) {
-            ok = ahead_.get();
-            buf_.swap(ahead_buf_);
+    // the next batch (inflated now, or the one inflating ahead), queued behind the ones being read;
+    // starts inflating the one after it.  Bytes go out up to the last call boundary before the end of
+    // what is known to be good: a call is the reference's gzread, which fails as a whole.
+    void fetch() {
+        Batch b;
+        if (ahead_.valid()) b = ahead_.get();
+        else inflate_batch(b);
+        if (!b.ok) {
+            limit_ = b.keep;
+            done_ = bad_ = true;
+        } else if (b.last) {
+            limit_ = b.base + b.data.size();
+            done_ = true;
         } else {
-            ok = inflate_batch(buf_, next_);
+            limit_ = (b.base + b.data.size()) / call_ * call_;
+            ahead_ = std::async(std::launch::async, [this] {
+                Batch n;
+                inflate_batch(n);
+                return n;
+            });
         }
-        if (!ok) next_ = members_.size();  // nothing after a bad member
-        if (ok && next_ < members_.size())
-            ahead_ = std::async(std::launch::async, [this] { return inflate_batch(ahead_buf_, next_); });
-        return ok;
+        q_.push_back(std::move(b));
     }
-    // the members from `first` (~64 MB of output) inflated into `out` on up to kThreads threads;
-    // advances `first` past them.  A member that fails its inflate, CRC32 or ISIZE check ends the
-    // stream: `out` keeps the members before the first such one and the call returns false.
-    bool inflate_batch(std::string& out, size_t& first_io) {
+    // the members from next_member_ (~64 MB of output) inflated into b.data on up to kThreads
+    // threads.  A member that fails its inflate, CRC32 or ISIZE check ends the stream: b.keep is
+    // the start of the reference's gzread call that meets the failure (the bytes before it, the bad
+    // member's included, are in b.data).
+    void inflate_batch(Batch& b) {
         static const int kThreads = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2));
-        const size_t first = first_io;
+        const size_t first = next_member_;
         size_t end = first, total = 0;
         std::vector<size_t> at;
-        while (end < members_.size() && (total < ((size_t)64 << 20) || end == first)) {
+        // (FQ_BGZF_BATCH: a smaller batch, for the tests of cuts across batches)
+        const char* be = getenv("FQ_BGZF_BATCH");
+        const size_t kBatch = be && atoll(be) > 0 ? (size_t)atoll(be) : (size_t)64 << 20;
+        while (end < members_.size() && (total < kBatch || end == first)) {
             at.push_back(total);
             total += members_[end].isize;
             ++end;
         }
-        out.resize(total);
+        b.data.resize(total);
+        b.base = stream_off_;
         const size_t cnt = end - first;
-        first_io = end;
-        // bad: the lowest index (within the batch) of a member that failed; each thread stops at its
-        // own first failure, which is enough, since its later members could only raise it
+        next_member_ = end;
+        stream_off_ += total;
+        b.last = end >= members_.size();
+        // bad: the lowest index (within the batch) of a member that failed, with how far zlib got
+        // in it; each thread stops at its own first failure, enough since its later members could
+        // only raise it
         std::atomic<size_t> bad{cnt};
+        std::vector<size_t> fail_at(cnt + 1, 0);  // stream offset of the failing gzread byte
         const int nt = (int)std::min<size_t>((size_t)kThreads, cnt);
-        auto fail = [&](size_t i) {
+        auto fail = [&](size_t i, size_t where) {
+            fail_at[i] = where;
             size_t cur = bad.load();
             while (i < cur && !bad.compare_exchange_weak(cur, i)) {
             }
@@ -403,7 +455,7 @@ class BgzfSource {
             z_stream z;
             std::memset(&z, 0, sizeof z);
             if (inflateInit2(&z, -15) != Z_OK) {
-                fail(i0);
+                fail(i0, b.base + at[i0]);
                 return;
             }
             for (size_t i = i0; i < i1 && i < bad.load(); ++i) {
@@ -411,13 +463,20 @@ class BgzfSource {
                 inflateReset(&z);
                 z.next_in = const_cast<Bytef*>(map_ + mb.data);
                 z.avail_in = (uInt)mb.clen;
-                Bytef* o = reinterpret_cast<Bytef*>(&out[0]) + at[i];
+                Bytef* o = reinterpret_cast<Bytef*>(&b.data[0]) + at[i];
                 unsigned char dummy;
                 z.next_out = mb.isize ? o : &dummy;
                 z.avail_out = mb.isize ? (uInt)mb.isize : 1u;
-                if (inflate(&z, Z_FINISH) != Z_STREAM_END || z.total_out != mb.isize ||
-                    (uint32_t)crc32(crc32(0, nullptr, 0), o, mb.isize) != mb.crc) {
-                    fail(i);
+                const int rc = inflate(&z, Z_FINISH);
+                if (rc != Z_STREAM_END) {
+                    // a data error (or a member longer than its ISIZE): zlib fails while producing
+                    // the byte after the ones it wrote
+                    fail(i, b.base + at[i] + std::min<size_t>(z.total_out, mb.isize));
+                    break;
+                }
+                if (z.total_out != mb.isize || (uint32_t)crc32(crc32(0, nullptr, 0), o, mb.isize) != mb.crc) {
+                    // the trailer check fails after the member's last byte
+                    fail(i, b.base + at[i] + (z.total_out ? z.total_out - 1 : 0));
                     break;
                 }
             }
@@ -427,19 +486,30 @@ class BgzfSource {
         for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
         if (nt > 0) work(0);
         for (auto& x : th) x.join();
-        const size_t b = bad.load();
-        if (b == cnt) return true;
-        out.resize(at[b]);  // the members before the first bad one
-        return false;
+        const size_t bi = bad.load();
+        if (bi == cnt) return;
+        b.ok = false;
+        b.last = true;
+        next_member_ = members_.size();  // nothing after a bad member
+        b.keep = fail_at[bi] / call_ * call_;  // the failing call's start
+        // (the bytes of the members after the bad one are not part of the stream)
+        const size_t inside = at[bi] + members_[first + bi].isize;
+        if (b.data.size() > inside) b.data.resize(inside);
     }
     const unsigned char* map_;
     size_t size_;
+    size_t call_;  // the reference's gzread request (its buffer size)
     std::vector<Member> members_;
-    size_t next_ = 0;          // first member not yet inflated (or being inflated ahead)
-    std::string buf_, ahead_buf_;
-    size_t pos_ = 0;
-    bool bad_ = false;  // a member failed: buf_ holds the last good bytes
-    std::future<bool> ahead_;  // the next batch, inflating while buf_ is read
+    size_t next_member_ = 0;  // first member not yet inflated (or being inflated ahead)
+    size_t stream_off_ = 0;   // stream offset of that member
+    std::deque<Batch> q_;       // inflated batches in stream order; the front one is being read
+    size_t pos_ = 0;            // bytes of q_.front() handed out
+    size_t limit_ = 0;          // stream offset up to which bytes may go out
+    bool started_ = false;
+    bool done_ = false;         // no batch to fetch after the queued ones
+    bool bad_ = false;          // ... because the stream is corrupt at limit_
+    bool reported_ = false;     // read() has returned false for it
+    std::future<Batch> ahead_;  // the next batch, inflating while the queued ones are read
 };
 
 // ---- whole gzip files through libdeflate ----
@@ -612,7 +682,7 @@ class GzAhead {
 FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     : phred64_(phred64), bsize_((uint64_t)buf_size) {
     if (ends_with(path, ".gz")) {
-        if ((bgzf_ = BgzfSource::open(path))) return;
+        if ((bgzf_ = BgzfSource::open(path, (size_t)bsize_))) return;
         path_ = path;
         // inflated whole on a thread of its own (so the mates of a pair inflate side by side), then
         // parsed like a mapped plain file; zlib's stream reader if that fails (settle())

@@ -205,14 +205,21 @@ def test_fqtool_raw_stream_small_windows_matches_reference(case, devices, tmp_pa
     E.check_outputs(case, str(outd))
 
 
-@pytest.mark.parametrize("kind", ["bgzf", "multi"])
-def test_corrupt_member_keeps_the_good_prefix(kind, host, oracle, tmp_path):
+@pytest.mark.parametrize("kind", ["bgzf", "bgzf_small_batches", "multi"])
+def test_corrupt_member_keeps_the_good_prefix(kind, host, oracle, tmp_path, monkeypatch):
     """A CRC32 flipped in a middle member of read 1's .gz: the tool processes exactly the bytes the
-    stream delivered before the failure and reports the error.  BGZF (members inflated in parallel):
-    every member before the bad one, in order.  Any other gzip (zlib's stream reader, read in the
-    reference's 1 MiB gzread calls, src/fqreader.cpp:28-35): every call before the one that fails.
+    reference's stream delivers before the failure and reports the error.  The reference reads every
+    gzip file in 1 MiB gzread calls (src/fqreader.cpp:28-35) and the call that meets the bad CRC
+    returns -1, so the stream ends at that call's start -- the bad member's bytes before it included.
+    Both readers here follow that: BGZF (members inflated in parallel, batches handed out up to their
+    last call boundary until the next is known) and any other gzip (zlib's stream reader).
     Expected: the outputs of the same command on plain files holding that prefix (read 2 whole)."""
     member, bad = 0xFF00, 40
+    if kind == "bgzf_small_batches":
+        # ~256 KiB inflate batches: the bad member lies batches after the one holding the cut, so
+        # the hold-back of each batch's bytes past its last 1 MiB boundary is what keeps them out
+        monkeypatch.setenv("FQ_BGZF_BATCH", str(1 << 18))
+        kind = "bgzf"
     raw = {}
     for name in ("r1.fq.gz", "r2.fq.gz"):
         with open(os.path.join(E.INPUTS, name), "rb") as f:
@@ -240,7 +247,7 @@ def test_corrupt_member_keeps_the_good_prefix(kind, host, oracle, tmp_path):
                 end = off + len(gzip.compress(data[bad * member:(bad + 1) * member], 6))
             comp[end - 8] ^= 0x5A  # the member's CRC32
             stop = (bad + 1) * member  # decompressed end of the bad member
-            keep = bad * member if kind == "bgzf" else (stop - 1) // (1 << 20) * (1 << 20)
+            keep = (stop - 1) // (1 << 20) * (1 << 20)  # the start of the gzread call that meets the bad CRC
         (gz / name).write_bytes(bytes(comp))
         (plain / name[:-3]).write_bytes(data[:keep])
     argv = E.argv_for("fqtool", "td_pe_qag", str(out_gz))
