@@ -78,8 +78,9 @@ clean:
 .PHONY: all engine host oracle clean
 
 # ThreadSanitizer build of the host pipeline (test infrastructure, CPU only): the tool's host sources
-# instrumented, linked against oracle/cpu_engine.cpp (the oracle standing in for the engine's
-# host-pack subset) instead of the GPU engine.  tests/test_tsan_cpu.py runs it (FQ_TEXT_MODE=0).
+# instrumented, linked against oracle/cpu_engine.cpp (the oracle standing in for the engine: host
+# packs, text packs and raw streams restated on the CPU) instead of the GPU engine.
+# tests/test_tsan_cpu.py runs it.
 TSANDIR    := build/tsan
 TSANFLAGS  := -std=c++17 -O1 -g -fPIC -pthread -fsanitize=thread
 tsan: $(TSANDIR)/fqtool
@@ -98,3 +99,24 @@ $(TSANDIR)/fqtool: $(patsubst $(HOSTDIR)/%.cpp,$(TSANDIR)/host_%.o,$(HOST_SRCS))
 	    -L$(TSANDIR) -lfqengine -Wl,-rpath,'$$ORIGIN' -lz
 
 .PHONY: tsan
+
+# The same host pipeline against the CPU stand-in, uninstrumented (test infrastructure, CPU only):
+# tests/test_raw_cpu.py runs the raw-stream and text-pack paths of the tool on the CPU with it.
+CPUHDIR    := build/cpuhost
+CPUHFLAGS  := -std=c++17 -O2 -g -fPIC -pthread
+cpuhost: $(CPUHDIR)/fqtool
+
+$(CPUHDIR)/host_%.o: $(HOSTDIR)/%.cpp $(HOST_HDRS)
+	@mkdir -p $(CPUHDIR)
+	$(CXX) $(CPUHFLAGS) -c $< -o $@
+
+$(CPUHDIR)/libfqengine.so: oracle/cpu_engine.cpp oracle/fq_oracle.c oracle/fq_oracle.h include/fqengine.h
+	@mkdir -p $(CPUHDIR)
+	gcc -std=c11 -O2 -g -fPIC -c oracle/fq_oracle.c -o $(CPUHDIR)/fq_oracle.o
+	$(CXX) $(CPUHFLAGS) -Iinclude -Ioracle -shared -o $@ oracle/cpu_engine.cpp $(CPUHDIR)/fq_oracle.o -lm
+
+$(CPUHDIR)/fqtool: $(patsubst $(HOSTDIR)/%.cpp,$(CPUHDIR)/host_%.o,$(HOST_SRCS)) $(HOSTDIR)/main.cpp $(CPUHDIR)/libfqengine.so
+	$(CXX) $(CPUHFLAGS) -o $@ $(HOSTDIR)/main.cpp $(patsubst $(HOSTDIR)/%.cpp,$(CPUHDIR)/host_%.o,$(HOST_SRCS)) \
+	    -L$(CPUHDIR) -lfqengine -Wl,-rpath,'$$ORIGIN' -lz
+
+.PHONY: cpuhost

@@ -89,8 +89,20 @@ void ByteBuf::release() {
 
 std::atomic<uint64_t> g_pinned_regrows{0}, g_pinned_bytes{0};
 static std::mutex g_retired_m;
-static std::vector<void*> g_retired;  // page-locked blocks outgrown mid-run (freed by the exit)
+// page-locked blocks outgrown mid-run: freed by the exit, or by free_retired_pinned() once the run's
+// engines are gone (in-process callers of fqh_run)
+static std::vector<std::pair<void*, size_t>> g_retired;
 static size_t g_retired_bytes = 0;
+
+void free_retired_pinned() {
+    std::lock_guard<std::mutex> g(g_retired_m);
+    for (auto& b : g_retired) {
+        fq_host_free(b.first);
+        g_pinned_bytes -= b.second;
+    }
+    g_retired.clear();
+    g_retired_bytes = 0;
+}
 
 void ByteBuf::reserve(size_t n) {
     if (n <= cap_) return;
@@ -125,7 +137,7 @@ void ByteBuf::reserve(size_t n) {
         // process ends instead of draining the pipeline here (up to 256 MiB of such blocks)
         std::lock_guard<std::mutex> g(g_retired_m);
         if (g_retired_bytes + cap_ <= ((size_t)256 << 20)) {
-            g_retired.push_back(p_);
+            g_retired.emplace_back(p_, cap_);
             g_retired_bytes += cap_;
             p_ = nullptr;
             cap_ = size_ = 0;

@@ -2249,8 +2249,12 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
         if (det.valid()) det.wait();  // the pre-pass's messages come first, as in the reference
         else if (det_on) det_done.set_value();  // (it never started: release the reader's gate)
         std::cerr << "ERROR: " << e.what() << std::endl;
+        free_retired_pinned();
         return 255;
     }
+    // (the engines are gone: the page-locked blocks outgrown during the run can go too, so an
+    // in-process caller does not keep them registered for its lifetime)
+    free_retired_pinned();
     return 0;
 }
 

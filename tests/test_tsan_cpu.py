@@ -39,3 +39,24 @@ def test_bgzf_inputs_under_tsan(workers, tsan_build, tmp_path):
             (inp / name).write_bytes(bgzf(gzip.decompress(f.read()), member=30_000))
     err, reports = T.run_case("td_pe_qag", str(out), workers, devices=2, inputs=str(inp))
     assert reports == 0, err[-6000:]
+
+
+@pytest.mark.parametrize("case,egress", [("td_pe_qag", "text"), ("td_pe_merge", "text"), ("synth_pe_c3", "text"),
+                                         ("td_se_q", "text"), ("td_pe_qag", "host"), ("td_pe_merge", "host")])
+def test_raw_stream_under_tsan(case, egress, tsan_build, tmp_path):
+    """The raw stream on three engines (plain inputs, 4 KiB first window, 7-pair packs): the window
+    reader thread, the per-engine threads with RawMulti's ordered enqueue / launch hand-offs and
+    stage queues, end_locked, the host reader's resume, and (egress "host") the records-only
+    formatter handing staging windows back."""
+    env = {"FQ_RAW_WINDOW0": "4096"}
+    if egress == "host":
+        env["FQ_RAW_EGRESS"] = "host"
+    err, reports = T.run_case(case, str(tmp_path), 4, devices=3, mode="raw", env_extra=env, pack_pairs=7)
+    assert "raw stream on 3 engines" in err, err[-3000:]
+    assert reports == 0, err[-6000:]
+
+
+@pytest.mark.parametrize("case", ["td_pe_gz", "td_pe_merge"])
+def test_text_packs_under_tsan(case, tsan_build, tmp_path):
+    err, reports = T.run_case(case, str(tmp_path), 4, devices=2, mode="text", pack_pairs=7)
+    assert reports == 0, err[-6000:]
