@@ -227,6 +227,7 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
     if (e2e_pairs + cpu_pairs) * rec_bytes * 1.2 > free:  # keep to the space the box has
         e2e_pairs = max(0, min(e2e_pairs, int(free / 1.2 / rec_bytes) - cpu_pairs))
         n = max(cpu_pairs, e2e_pairs)
+    file_legs = (2 * e2e_pairs + 2 * cpu_pairs) * rec_bytes * 1.2 < free  # (the file leg's outputs beside the inputs)
     dev = torch.device("cuda:0")
     bufs = [torch.empty(abi.batch_bytes(n, STRIDE), dtype=torch.uint8, device=dev) for _ in range(4)]
     lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
@@ -248,9 +249,19 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
         log(f"FASTQ written in {time.perf_counter() - t0:.1f}s ({cpu_pairs} + {e2e_pairs} pairs)")
         opts = ["-q", "-a", "--detect_pe_adapter", "-g"]
 
-        def e2e(extra):
+        def e2e(extra, outputs="null", inp=None, pairs=None):
+            """outputs: "null" (/dev/null), "file" (plain FASTQ files beside the inputs: the writer
+            threads put every output byte into the page cache), "gz" (BGZF .gz files, members
+            compressed on the pool; src/writer.cpp's gzip output)"""
             tool = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
-            cmd = [tool, "-i", big[0], "-I", big[1], "-o", "/dev/null", "-O", "/dev/null", *extra, "-w", str(workers),
+            inp = inp or big
+            pairs = pairs or e2e_pairs
+            outs = {"null": ["/dev/null", "/dev/null"],
+                    "file": [os.path.join(tmp, "out1.fq"), os.path.join(tmp, "out2.fq")],
+                    "gz": [os.path.join(tmp, "out1.fq.gz"), os.path.join(tmp, "out2.fq.gz")]}[outputs]
+            if "--merge_output" in extra and outputs != "null":
+                extra = [outs[0] if (k > 0 and extra[k - 1] == "--merge_output") else a for k, a in enumerate(extra)]
+            cmd = [tool, "-i", inp[0], "-I", inp[1], "-o", outs[0], "-O", outs[1], *extra, "-w", str(workers),
                    "-J", os.path.join(tmp, "amd.json"), "-H", os.path.join(tmp, "amd.html")]
             # one untimed run first, on the small sample: the binary's first start on a box (its
             # libraries and code objects read in, the GPU's first process setup) is not the pipeline
@@ -264,25 +275,40 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
                 # while that is still going finds HIP's start-up 0.1-0.15 s slower
                 # (profiles/r04_e2e_pause_50M.txt)
                 time.sleep(E2E_PAUSE_S)
+                for f in outs:  # (each run writes its outputs afresh)
+                    if f != "/dev/null" and os.path.exists(f):
+                        os.remove(f)
                 t0 = time.perf_counter()
                 p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
                 dt = time.perf_counter() - t0
                 if p.returncode != 0:
                     raise RuntimeError("fqtool failed: " + p.stderr[-2000:])
                 runs.append((dt, [l for l in p.stderr.splitlines() if "fqtool-amd:" in l]))
+            out_bytes = sum(os.path.getsize(f) for f in set(outs) if f != "/dev/null" and os.path.exists(f))
+            for f in outs:
+                if f != "/dev/null" and os.path.exists(f):
+                    os.remove(f)
             dt, tool_log = sorted(runs, key=lambda r: r[0])[1]
-            gb = (os.path.getsize(big[0]) + os.path.getsize(big[1])) / 1e9
-            return {"value": round(2 * e2e_pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": e2e_pairs,
-                    "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
-                    "runs_wall_s": [round(r[0], 3) for r in runs], "pause_between_runs_s": E2E_PAUSE_S,
-                    "options": " ".join(extra),
-                    "path": e2e_path(tool_log),
-                    "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
+            gb = (os.path.getsize(inp[0]) + os.path.getsize(inp[1])) / 1e9
+            r = {"value": round(2 * pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": pairs,
+                 "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
+                 "runs_wall_s": [round(r[0], 3) for r in runs], "pause_between_runs_s": E2E_PAUSE_S,
+                 "options": " ".join(extra), "outputs": outputs,
+                 "path": e2e_path(tool_log),
+                 "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
+            if outputs != "null":
+                r["output_GB"] = round(out_bytes / 1e9, 3)
+            return r
 
         if big:
             out["e2e"] = e2e(opts)
             # BASELINE config 4 (-m): every pair's output is the merged stream (to /dev/null)
             out["e2e_c4"] = e2e(["-q", "-a", "-g", "--enable_cut_right", "-m", "--merge_output", "/dev/null"])
+            # the writers timed: the same C3 run with plain FASTQ output files (page cache), and
+            # BGZF .gz outputs (-z 4, the reference's default level) on the CPU-baseline sample
+            if os.environ.get("FQ_BENCH_FILE_LEGS", "1") != "0" and file_legs:
+                out["e2e_file"] = e2e(opts, outputs="file")
+                out["e2e_gz"] = e2e(opts, outputs="gz", inp=small, pairs=cpu_pairs)
         ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
         if os.path.exists(ref):
             w = min(16, workers)
@@ -734,6 +760,8 @@ def run_rank(args):
         "paths": paths,
         "e2e": None,
         "e2e_c4": None,
+        "e2e_file": None,
+        "e2e_gz": None,
         "acc_sha256": acc_digest,
         "parity_sample": sample,
     }
@@ -743,6 +771,8 @@ def run_rank(args):
         out["cpu_baseline"] = legs["cpu_baseline"]
         out["e2e"] = legs["e2e"]
         out["e2e_c4"] = legs.get("e2e_c4")
+        out["e2e_file"] = legs.get("e2e_file")
+        out["e2e_gz"] = legs.get("e2e_gz")
         log(f"e2e {legs['e2e']}")
         log(f"e2e_c4 {legs.get('e2e_c4')}")
     runner.close()

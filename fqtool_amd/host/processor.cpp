@@ -896,7 +896,13 @@ void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p,
             for (size_t i = i0; i < i1; ++i) {
                 const fq_text_rec& R = T[i];
                 const fq_read_result& r = rr(i, m);
-                if (out_ok(i)) {
+                if (out_ok(i) && r.start == 0 && r.len == R.len) {
+                    // an untrimmed record is its input text as it stands (raw records are "plain":
+                    // four lines, each ending in '\n'): one copy
+                    const size_t nb = (size_t)R.name_len + R.strand_len + 2 * (size_t)R.len + 4;
+                    std::memcpy(d, t + R.name_off, nb);
+                    d += nb;
+                } else if (out_ok(i)) {
                     std::memcpy(d, t + R.name_off, R.name_len);
                     d += R.name_len;
                     *d++ = '\n';
