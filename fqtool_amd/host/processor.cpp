@@ -1903,8 +1903,10 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
     // does not compete with HIP start-up and the engines' allocations.
     std::promise<void> det_done;
     std::future<Detection> det;
+    bool det_started = false;  // (det_done is then set by the detection, even once det is joined)
     const bool det_on = o.detect_pe_adapter && !o.in2.empty();
     auto start_detection = [&] {
+        det_started = true;
         det = std::async(std::launch::async, [&o, &det_done] {
             Detection d;
             try {
@@ -2253,7 +2255,7 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
         }
     } catch (const std::exception& e) {
         if (det.valid()) det.wait();  // the pre-pass's messages come first, as in the reference
-        else if (det_on) det_done.set_value();  // (it never started: release the reader's gate)
+        else if (det_on && !det_started) det_done.set_value();  // (it never started: release the reader's gate)
         std::cerr << "ERROR: " << e.what() << std::endl;
         free_retired_pinned();
         return 255;

@@ -1,0 +1,148 @@
+// null_engine.cpp -- PROFILING AID ONLY: an engine library (include/fqengine.h's C-ABI) whose raw
+// streams cost nothing, so the fqtool binary's host feed -- the window reader (pread into staging
+// windows), the per-engine threads with RawMulti's ordered hand-offs, the formatter hand-off and
+// the writers -- runs at its own ceiling with G "infinitely fast" engines (tools/host_feed.py).
+//
+// Raw windows: the host cuts windows of whole pairs (RawMulti), so a window's pairs are its bytes
+// over the fixed record size of the synthetic input (FQ_NULL_REC1 / FQ_NULL_REC2 bytes per record),
+// nothing is carried, nothing stops the stream, and every record passes untrimmed: the pack's output
+// is as long as its input (the output buffers are not written -- as with the GPU's D2H copies, the
+// host pays nothing for them -- so the writers write stale bytes).  Records and accumulators stay
+// zero.  Text and host packs complete at once, untouched; only the raw stream is meant to run here.
+// Built by tools/host_feed.py into build/nullhost/libfqengine.so, loaded through LD_LIBRARY_PATH.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/fqengine.h"
+
+struct fq_engine {
+    fq_params p;
+    size_t acc_words = 0;
+    std::string err;
+    struct Done {
+        uint64_t seq;
+        fq_text_out* out;
+        uint64_t bytes[2];
+    };
+    std::deque<Done> pending;
+    std::deque<fq_raw_window> queued;
+    uint64_t rec[2] = {0, 0};
+    uint64_t carry[2] = {0, 0};  // bytes after the last whole record (one engine: windows cut anywhere)
+};
+struct fq_dup {
+    int unused;
+};
+struct fq_kmer_set {
+    int unused;
+};
+
+extern "C" {
+
+int fq_engine_create(const fq_params* params, int, int32_t, int32_t, fq_engine** out) {
+    if (!params || !out) return FQ_E_INVALID;
+    fq_engine* e = new fq_engine();
+    e->p = *params;
+    e->acc_words = fq_acc_words(params->insert_size_max, params->max_cycles);
+    const char* r1 = std::getenv("FQ_NULL_REC1");
+    const char* r2 = std::getenv("FQ_NULL_REC2");
+    e->rec[0] = r1 ? std::strtoull(r1, nullptr, 10) : 0;
+    e->rec[1] = r2 ? std::strtoull(r2, nullptr, 10) : e->rec[0];
+    *out = e;
+    return FQ_OK;
+}
+int fq_engine_destroy(fq_engine* e) {
+    delete e;
+    return FQ_OK;
+}
+size_t fq_engine_acc_words(const fq_engine* e) { return e ? e->acc_words : 0; }
+int fq_engine_read_acc(fq_engine* e, uint64_t* host, size_t words) {
+    if (!e || !host || words < e->acc_words) return FQ_E_INVALID;
+    std::memset(host, 0, e->acc_words * 8);
+    return FQ_OK;
+}
+int fq_engine_reset_acc(fq_engine*) { return FQ_OK; }
+int fq_engine_sync(fq_engine*) { return FQ_OK; }
+const char* fq_engine_last_error(const fq_engine* e) { return e ? e->err.c_str() : "no engine"; }
+
+int fq_engine_submit(fq_engine* e, const fq_batch*, fq_read_result*, uint64_t seq_no) {
+    e->pending.push_back({seq_no, nullptr, {0, 0}});
+    return FQ_OK;
+}
+int fq_engine_submit_text(fq_engine* e, const fq_text_batch* tb, fq_read_result*, fq_text_out* out, uint64_t seq_no) {
+    e->pending.push_back({seq_no, out, {tb->text_bytes[0], tb->text_bytes[1]}});
+    return FQ_OK;
+}
+int fq_engine_poll(fq_engine* e, int, uint64_t* seq_no) {
+    if (e->pending.empty()) return 0;
+    const fq_engine::Done d = e->pending.front();
+    e->pending.pop_front();
+    if (d.out) {
+        d.out->bytes[0] = d.bytes[0];
+        d.out->bytes[1] = d.bytes[1];
+    }
+    if (seq_no) *seq_no = d.seq;
+    return 1;
+}
+
+int fq_engine_raw_begin(fq_engine* e, uint64_t, uint64_t) {
+    if (!e->rec[0]) {
+        e->err = "null engine: set FQ_NULL_REC1 (bytes per record of the fixed-width input)";
+        return FQ_E_INVALID;
+    }
+    e->queued.clear();
+    e->carry[0] = e->carry[1] = 0;
+    return FQ_OK;
+}
+int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w) {
+    e->queued.push_back(*w);
+    return FQ_OK;
+}
+int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64_t seq_no) {
+    if (e->queued.empty()) return FQ_E_INVALID;
+    const fq_raw_window w = e->queued.front();
+    e->queued.pop_front();
+    std::memset(r, 0, sizeof *r);
+    const int mates = e->p.paired ? 2 : 1;
+    uint64_t pairs = ~0ull;
+    for (int m = 0; m < mates; ++m) pairs = std::min(pairs, (e->carry[m] + w.n[m]) / e->rec[m]);
+    r->pairs = (int32_t)pairs;
+    r->max_len = 150;
+    for (int m = 0; m < mates; ++m) {
+        r->text_bytes[m] = pairs * e->rec[m];
+        e->carry[m] = e->carry[m] + w.n[m] - r->text_bytes[m];
+        r->carry[m] = e->carry[m];
+    }
+    out->adapter_bytes[0] = out->adapter_bytes[1] = 0;
+    out->text.bytes[0] = out->text.bytes[1] = 0;
+    e->pending.push_back({seq_no, &out->text, {r->text_bytes[0], mates > 1 ? r->text_bytes[1] : 0}});
+    return FQ_OK;
+}
+int fq_engine_raw_end(fq_engine* e) {
+    e->queued.clear();
+    return FQ_OK;
+}
+
+int fq_host_alloc(size_t bytes, void** out) {
+    *out = std::aligned_alloc(4096, (bytes + 4095) / 4096 * 4096);
+    return *out ? FQ_OK : FQ_E_NOMEM;
+}
+int fq_host_free(void* p) {
+    std::free(p);
+    return FQ_OK;
+}
+
+int fq_dup_create(int, int32_t, fq_dup**) { return FQ_E_INVALID; }
+int fq_dup_destroy(fq_dup*) { return FQ_OK; }
+int fq_dup_merge(fq_dup*, const fq_dup*) { return FQ_E_INVALID; }
+int fq_dup_stat(fq_dup*, int32_t, uint64_t*, uint64_t*, uint64_t*) { return FQ_E_INVALID; }
+int fq_engine_set_dup(fq_engine*, fq_dup*) { return FQ_OK; }
+int fq_kmer_open(int, const uint8_t*, const uint32_t*, int32_t, fq_kmer_set**) { return FQ_E_INVALID; }
+int fq_kmer_close(fq_kmer_set*) { return FQ_OK; }
+int fq_kmer_count(fq_kmer_set*, int32_t, int32_t, int32_t, uint32_t*) { return FQ_E_INVALID; }
+int fq_kmer_find(fq_kmer_set*, int32_t, int32_t, int32_t, uint32_t, uint64_t*, size_t, size_t*) { return FQ_E_INVALID; }
+
+}  // extern "C"
