@@ -227,7 +227,6 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
     if (e2e_pairs + cpu_pairs) * rec_bytes * 1.2 > free:  # keep to the space the box has
         e2e_pairs = max(0, min(e2e_pairs, int(free / 1.2 / rec_bytes) - cpu_pairs))
         n = max(cpu_pairs, e2e_pairs)
-    file_legs = (2 * e2e_pairs + 2 * cpu_pairs) * rec_bytes * 1.2 < free  # (the file leg's outputs beside the inputs)
     dev = torch.device("cuda:0")
     bufs = [torch.empty(abi.batch_bytes(n, STRIDE), dtype=torch.uint8, device=dev) for _ in range(4)]
     lens = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(2)]
@@ -247,6 +246,11 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
         torch.cuda.empty_cache()
         os.sync()  # (the files' dirty pages written back now, not during the first timed run)
         log(f"FASTQ written in {time.perf_counter() - t0:.1f}s ({cpu_pairs} + {e2e_pairs} pairs)")
+        # the file leg's outputs go beside the inputs: room for one run's outputs (about the inputs' size)
+        free = shutil.disk_usage(tmp).free
+        file_legs = e2e_pairs * rec_bytes * 1.1 < free
+        if not file_legs:
+            log(f"file legs skipped: {free / 1e9:.1f} GB free beside the inputs")
         opts = ["-q", "-a", "--detect_pe_adapter", "-g"]
 
         def e2e(extra, outputs="null", inp=None, pairs=None):

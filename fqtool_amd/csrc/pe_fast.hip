@@ -138,6 +138,12 @@ namespace {
 #ifndef FQ_ST_PF2
 #define FQ_ST_PF2 1  // removed-mode Stats: column words requested two chunks ahead (no wait on the atomics)
 #endif
+#ifndef FQ_OVX2
+#define FQ_OVX2 0  // overlap exact check: word pairs by ds_read2st64 + 64-bit shifts, the 50-position test peeled
+#endif
+#ifndef FQ_MRG2
+#define FQ_MRG2 0  // merged-part Stats: groups unrolled (immediate row offsets), qualities through a tile buffer
+#endif
 #ifndef FQ_OV_SH64
 #define FQ_OV_SH64 1  // overlap candidates: planes realigned by 64-bit shifts (one block per pass)
 #endif
@@ -360,6 +366,36 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
     const uint32_t* B = col + (p2 >> 4) * 64 + c2;
     constexpr int kN = kFN * 64;                       // the N-mask field, kChunks words further
     const uint32_t last = posmask(ol - 16 * (nw - 1));  // valid positions of the last word
+#if FQ_OVX2
+    // Each stream's words j and j + 1 come as one register pair (one ds_read2st64 each), realigned
+    // by a full-rate 64-bit shift -- instead of a v_alignbit (half rate) on words carried over from
+    // the previous step, whose rotation also cost four moves a word.  The first four words, which
+    // decide the rejection within 50 positions, are peeled off the loop that counts the rest.
+    auto mism_at = [&](int j) -> uint32_t {
+        auto pr = [&](const uint32_t* W, int f, uint32_t s) -> uint32_t {
+            const unsigned long long v = (unsigned long long)W[64 * (j + 1) + f] << 32 | W[64 * j + f];
+            unsigned long long r;
+            asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "v"(s), "v"(v));
+            return (uint32_t)r;
+        };
+        const uint32_t a = pr(A, 0, (uint32_t)s1), wa = pr(A, kN, (uint32_t)s1);
+        const uint32_t b = pr(B, 0, (uint32_t)s2), wb = pr(B, kN, (uint32_t)s2);
+        uint32_t mism = ((fold2(a ^ b) & ~(wa | wb)) | (wa ^ wb) | (wa >> 1)) & 0x55555555u;
+        if (j == nw - 1) mism &= last;
+        return mism;
+    };
+    int j = 0;
+    for (; j < 4 && j < nw; ++j) {
+        const uint32_t mism = mism_at(j);
+        if (j == 3) d50 = D + __popc(mism & 5u);
+        D += __popc(mism);
+    }
+    if (nw > 3 && d50 >= K) {  // (the break happens within 50: rejected whatever follows)
+        diff_out = D;
+        return false;
+    }
+    for (; j < nw; ++j) D += __popc(mism_at(j));
+#else
     uint32_t a0 = A[0], an0 = A[kN], b0 = B[0], bn0 = B[kN];
     for (int j = 0; j < nw; ++j) {
         const uint32_t a1 = A[64 * (j + 1)], an1 = A[64 * (j + 1) + kN];
@@ -376,6 +412,7 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
         if (j == 3 && d50 >= K) break;  // rejected whatever follows (the break happens within 50)
         a0 = a1; an0 = an1; b0 = b1; bn0 = bn1;
     }
+#endif
     if (nw <= 3) d50 = D;  // (ol <= 48: every position is within 50)
     diff_out = D;
     // break (rejection) happens iff the K-th mismatch lies within the first min(ol,50) positions
@@ -853,9 +890,11 @@ __device__ inline bool cut_right_w4(const fq_params& p, const uint8_t* Q, int nc
 // Returns bit 0 (hand the pair over: exotic bytes where they are not taken, allow_exotic false),
 // bit 1 (the read holds exotic bytes) and, from bit 2 on, the count staging took for 'N's.  xp: the lane's column word of row chunk 0 (read 2: its
 // reverse complement, stepped by wstep).
+typedef __attribute__((address_space(3))) uint32_t LdsU32;  // (LDS pointers: a generic one costs the caller
+                                                            // a 64-bit flat address held across the tile)
 template <bool PAIRED>
-__device__ __attribute__((noinline)) int lower_flags(const uint8_t* S, uint32_t* xp, int wstep, int nch, int L, bool rc,
-                                                    uint32_t rsel, uint32_t* pfx, int step, bool allow_exotic) {
+__device__ __attribute__((noinline)) int lower_flags(const uint8_t* S, LdsU32* xp, int wstep, int nch, int L, bool rc,
+                                                    uint32_t rsel, LdsU32* pfx, int step, bool allow_exotic) {
     constexpr int cst = FQ_TILE_READS * FQ_CHUNK;
     bool exotic = false;
     int ntot = 0;
@@ -1071,7 +1110,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                                                          unsigned long long* __restrict__ acc, int* __restrict__ slow_tiles,
                                                          int* __restrict__ slow_count, unsigned long long* __restrict__ xfix) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = MERGE ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;  // an SGPR frees merge !FIX from its one spill
     using LY = Layout<LEAN, MERGE, PAIRED>;
     constexpr int kWaves = LY::kWaves, kThreads = LY::kThreads;
     uint32_t* col = lds + wave * LY::kWaveW;  // code / N columns: word field*64 + lane
@@ -1368,8 +1408,10 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     ad_ok = ad_ok && (a == 'A' || a == 'C' || a == 'G' || a == 'T' || my_ad[i] == 'N');
                 }
                 const bool allow = !MERGE && !p.complexity_enabled && ad_ok;
-                const int lf = lower_flags<PAIRED>(S, col + lane_x + (rc ? (kChunks - 1) * 64 : 0), wstep, nch, L, rc, rsel,
-                                                   LY::kPfx ? col + kCodeW + lane_x : nullptr, LY::kPfxStep, allow);
+                // (LDS pointers from word offsets: no generic pointer to hold across the tile)
+                auto lds_at = [&](const uint32_t* q) { return (LdsU32*)(size_t)(4u * (uint32_t)(q - lds)); };
+                const int lf = lower_flags<PAIRED>(S, lds_at(col + lane_x + (rc ? (kChunks - 1) * 64 : 0)), wstep, nch, L, rc,
+                                                   rsel, LY::kPfx ? lds_at(col + kCodeW + lane_x) : nullptr, LY::kPfxStep, allow);
                 hard = (lf & 1) != 0;
                 xe = (lf & 2) != 0;
                 nbf -= (uint32_t)(lf >> 2);
@@ -2224,6 +2266,88 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 else return RowQual{Q2, b.stride >> 2}.word(max(wi, 0));
             };
             uint32_t qw5[5];
+#if FQ_MRG2
+            if constexpr (!kRot && !LY::kQLds) {
+                // The lane's groups J = mate + 2k unrolled (k < kMrgIter): the cell rows of group k are
+                // 2048 k bytes on (an immediate of the atomics), and its quality dwords 1024 k bytes
+                // back in the row.  The dwords come through a buffer over the wave's tile of read 2's
+                // quality plane: an offset outside the tile (a dummy position before the row) reads 0
+                // instead of faulting, so no clamping; the 5 offsets are computed once.
+                constexpr int kMrgIter = (kMaxLen + 31) / 32;
+                const size_t tile_off = (size_t)__builtin_amdgcn_readfirstlane(t) * FQ_TILE_READS * (size_t)b.stride;
+                const __amdgpu_buffer_rsrc_t qr2 = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)(b.qual2 + tile_off), (short)0, FQ_TILE_READS * b.stride, 0x00020000);
+                int vo[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    const int w = wl0 - 4 * mate + i;
+                    vo[i] = (w >> 2) * (FQ_TILE_READS * FQ_CHUNK) + ((w & 3) << 2) + pl * FQ_CHUNK;
+                }
+#pragma unroll
+                for (int i = 0; i < 5; ++i) qw5[i] = __builtin_amdgcn_raw_buffer_load_b32(qr2, vo[i], 0, 0);
+                // slot nibble to bits 7-9: nibble u of both words by one 64-bit shift (as FQ_ST_SH64)
+#pragma unroll
+                for (int k = 0; k < kMrgIter; ++k) {
+                    const int J = mate + 2 * k;
+                    if (!__any(16 * J < m2)) break;  // (wave-uniform)
+                    if (16 * J < m2) {
+                        const uint32_t cw = field_window_masked(col, kFC, c2, ci0 + 16 * J);
+                        const uint32_t nw = field_window_masked(col, kFN, c2, ci0 + 16 * J);
+                        uint32_t qn[5] = {0u, 0u, 0u, 0u, 0u};
+                        if (k + 1 < kMrgIter)
+#pragma unroll
+                            for (int i = 0; i < 5; ++i) qn[i] = __builtin_amdgcn_raw_buffer_load_b32(qr2, vo[i] - 1024 * (k + 1), 0, 0);
+                        uint32_t qa[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) qa[i] = __builtin_amdgcn_alignbyte(qw5[i + 1], qw5[i], sh);
+                        auto qbyte = [&](int tt) -> uint32_t {  // step tt: part position tt, byte 3 - tt % 4 of qa[3 - tt / 4]
+                            const uint32_t qw = qa[(15 - tt) >> 2];
+                            const int bs = (15 - tt) & 3;
+                            return bs == 0 ? qw & 0xFFu : bs == 3 ? qw >> 24 : __builtin_amdgcn_ubfe(qw, 8 * bs, 8);
+                        };
+                        const int rem = m2 - 16 * J;
+                        const unsigned long long dm = ~0ull << min(4 * max(rem, 0), 63);
+                        uint32_t nlo = spread2to4(cw), nhi = spread2to4(cw >> 16);
+                        const uint32_t dlo = (uint32_t)dm, dhi = rem >= 16 ? 0u : (uint32_t)(dm >> 32);
+                        nlo = (nlo & ~dlo) | (dlo & 0x55555555u);  // 5 = kDummySlot
+                        nhi = (nhi & ~dhi) | (dhi & 0x55555555u);
+                        // nibble u of {nhi, nlo} to bits 7-9: K << 7 (u 0), K << 3 (u 1), K >> (4u - 7)
+                        const unsigned long long K = (unsigned long long)nhi << 32 | nlo;
+                        unsigned long long Ks[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            if (u < 2) asm("v_lshlrev_b64 %0, %2, %1" : "=v"(Ks[u]) : "v"(K), "i"(7 - 4 * u));
+                            else asm("v_lshrrev_b64 %0, %2, %1" : "=v"(Ks[u]) : "v"(K), "i"(4 * u - 7));
+                        }
+#pragma unroll
+                        for (int tt = 0; tt < 16; ++tt) {
+                            const uint32_t ksh = tt < 8 ? (uint32_t)Ks[tt & 7] : (uint32_t)(Ks[tt & 7] >> 32);
+                            uint32_t a;
+                            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xEA" : "=v"(a) : "v"(ksh), "v"(mslot_m), "v"(rb[tt]));
+                            a += 2048u * (uint32_t)k;  // (folds into the ds offset)
+                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)a), kCount1 | (unsigned long long)qbyte(tt),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        uint32_t nv = nw & posmask(rem);
+                        while (nv) {  // N (code 3): from the G slot (3) to the N slot (4)
+                            const int tt = (__ffs(nv) - 1) >> 1;
+                            nv &= nv - 1;
+                            const unsigned long long v =
+                                kCount1 | (unsigned long long)__builtin_amdgcn_ubfe(qa[3 - (tt >> 2)], 8 * (3 - (tt & 3)), 8);
+                            const int c = m1 + 16 * J + tt;
+                            const uint32_t a = xb + (uint32_t)((c >> 4) << 10 | (c & 15) << 3);
+                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + 4u * 128u)), v, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_add(reinterpret_cast<LdsU64*>((size_t)(a + 3u * 128u)), 0ull - v,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) qw5[i] = qn[i];
+                    }
+                }
+            } else
+#endif
+            {
 #pragma unroll
             for (int i = 0; i < 5; ++i) qw5[i] = qword(wl0 - 4 * mate + i);
             for (int J = mate; 16 * J < m2; J += 2) {
@@ -2295,6 +2419,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 for (int i = 0; i < 5; ++i) qw5[i] = qn[i];
 #pragma unroll
                 for (int t = 0; t < 16; ++t) rb[t] += 2048u;  // (J + 2: two cycle rows on)
+            }
             }
         }
         if (valid && !(abl & 4) && !removed_mode) {
