@@ -139,10 +139,10 @@ namespace {
 #define FQ_ST_PF2 1  // removed-mode Stats: column words requested two chunks ahead (no wait on the atomics)
 #endif
 #ifndef FQ_OVX2
-#define FQ_OVX2 0  // overlap exact check: word pairs by ds_read2st64 + 64-bit shifts, the 50-position test peeled
+#define FQ_OVX2 1  // overlap exact check: word pairs by ds_read2st64 + 64-bit shifts, the 50-position test peeled
 #endif
 #ifndef FQ_MRG2
-#define FQ_MRG2 0  // merged-part Stats: groups unrolled (immediate row offsets), qualities through a tile buffer
+#define FQ_MRG2 1  // merged-part Stats: groups unrolled (immediate row offsets), qualities through a tile buffer
 #endif
 #ifndef FQ_OV_SH64
 #define FQ_OV_SH64 1  // overlap candidates: planes realigned by 64-bit shifts (one block per pass)
@@ -357,6 +357,7 @@ struct OvOut {
 // The words are read unclamped: p1, p2 >= 0 and p + ol <= the column length, so a look-ahead word
 // past the column (the next field, or the next wave's column: valid LDS) only feeds positions at
 // or beyond ol, which the last word's mask drops.
+template <bool X2>
 __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int p2, int ol, int limit, int K,
                                 int& diff_out) {
     int d50 = 0, D = 0;
@@ -366,7 +367,7 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
     const uint32_t* B = col + (p2 >> 4) * 64 + c2;
     constexpr int kN = kFN * 64;                       // the N-mask field, kChunks words further
     const uint32_t last = posmask(ol - 16 * (nw - 1));  // valid positions of the last word
-#if FQ_OVX2
+    if constexpr (X2) {
     // Each stream's words j and j + 1 come as one register pair (one ds_read2st64 each), realigned
     // by a full-rate 64-bit shift -- instead of a v_alignbit (half rate) on words carried over from
     // the previous step, whose rotation also cost four moves a word.  The first four words, which
@@ -395,7 +396,7 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
         return false;
     }
     for (; j < nw; ++j) D += __popc(mism_at(j));
-#else
+    } else {
     uint32_t a0 = A[0], an0 = A[kN], b0 = B[0], bn0 = B[kN];
     for (int j = 0; j < nw; ++j) {
         const uint32_t a1 = A[64 * (j + 1)], an1 = A[64 * (j + 1) + kN];
@@ -412,7 +413,7 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
         if (j == 3 && d50 >= K) break;  // rejected whatever follows (the break happens within 50)
         a0 = a1; an0 = an1; b0 = b1; bn0 = bn1;
     }
-#endif
+    }
     if (nw <= 3) d50 = D;  // (ol <= 48: every position is within 50)
     diff_out = D;
     // break (rejection) happens iff the K-th mismatch lies within the first min(ol,50) positions
@@ -1114,6 +1115,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
     const int wave = MERGE ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;  // an SGPR frees merge !FIX from its one spill
     using LY = Layout<LEAN, MERGE, PAIRED>;
     constexpr int kWaves = LY::kWaves, kThreads = LY::kThreads;
+    // the paired exact check where it fits the registers (FULL without -m spills with it)
+    constexpr bool kOvx2 = FQ_OVX2 && (LEAN || MERGE);
     uint32_t* col = lds + wave * LY::kWaveW;  // code / N columns: word field*64 + lane
     uint32_t* qrows = col + kCodeW;           // full variant: quality rows, row = lane
     uint32_t* hist = lds + LY::kColsW;        // [pre1, pre2, post1, post2] x kHistW (post1 x2 with MERGE)
@@ -1609,7 +1612,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     const int ol = min(olA - o, olB);
                     int diff = 0;
                     if (abl & 512) atomicAdd(&g_phase_cycles[0], 1ull);  // profiling: exact checks
-                    if ((abl & 64) || ov_exact(col, c1, mate ? st1 : st1 + o, c2, mate ? off2 + o : off2, ol, limit, K, diff)) {
+                    if ((abl & 64) || ov_exact<kOvx2>(col, c1, mate ? st1 : st1 + o, c2, mate ? off2 + o : off2, ol, limit, K, diff)) {
                         mine = OvOut{true, mate ? -o : o, ol, diff};
                         break;
                     }
@@ -1622,7 +1625,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 const int ol = min(olA - o, olB);
                 int diff = 0;
                 if (abl & 512) atomicAdd(&g_phase_cycles[0], 1ull);  // profiling: exact checks
-                if ((abl & 64) || ov_exact(col, c1, mate ? st1 : st1 + o, c2, mate ? off2 + o : off2, ol, limit, K, diff)) {
+                if ((abl & 64) || ov_exact<kOvx2>(col, c1, mate ? st1 : st1 + o, c2, mate ? off2 + o : off2, ol, limit, K, diff)) {
                     mine = OvOut{true, mate ? -o : o, ol, diff};
                     break;
                 }
