@@ -257,6 +257,7 @@ def load_engine(path=ENGINE_LIB):
     lib.fq_engine_raw_begin.argtypes = [vp, u64, u64]
     lib.fq_engine_raw_enqueue.argtypes = [vp, ctypes.POINTER(FqRawWindow)]
     lib.fq_engine_raw_launch.argtypes = [vp, ctypes.POINTER(FqRawResult), ctypes.POINTER(FqRawOut), u64]
+    lib.fq_engine_raw_wait.argtypes = [vp, ctypes.POINTER(FqRawResult)]
     lib.fq_engine_raw_end.argtypes = [vp]
     lib.fq_host_register.argtypes = [vp, ctypes.c_size_t]
     lib.fq_host_unregister.argtypes = [vp]
@@ -282,7 +283,7 @@ ENGINE_SYMBOLS = [
     "fq_engine_last_kernel_ms", "fq_engine_submit", "fq_engine_submit_text", "fq_engine_poll", "fq_engine_pending", "fq_host_alloc",
     "fq_host_free", "fq_dup_create", "fq_dup_destroy", "fq_dup_reset", "fq_engine_set_dup", "fq_dup_merge",
     "fq_dup_stat", "fq_kmer_open", "fq_kmer_close", "fq_kmer_count", "fq_kmer_find",
-    "fq_engine_raw_begin", "fq_engine_raw_enqueue", "fq_engine_raw_launch", "fq_engine_raw_end", "fq_host_register", "fq_host_unregister",
+    "fq_engine_raw_begin", "fq_engine_raw_enqueue", "fq_engine_raw_launch", "fq_engine_raw_wait", "fq_engine_raw_end", "fq_host_register", "fq_host_unregister",
 ]
 
 

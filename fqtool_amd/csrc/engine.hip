@@ -777,16 +777,9 @@ int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w) {
     return FQ_OK;
 }
 
-int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64_t seq_no) {
-    if (!e || !r || !out) return FQ_E_INVALID;
-    if (e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_launch without an enqueued window");
-    HIP_TRY(e, hipSetDevice(e->device));
-    const int k = e->raw_queued.front();
-    e->raw_queued.pop_front();
-    Slot& s = e->slots[k];
-    HIP_TRY(e, hipEventSynchronize(s.ev_idx));
-    const bool pe = e->p.paired;
-    const int mates = pe ? 2 : 1;
+// the oldest enqueued window's index, once its copy back has landed
+static void raw_result_of(const fq_engine* e, const Slot& s, fq_raw_result* r) {
+    const int mates = e->p.paired ? 2 : 1;
     std::memset(r, 0, sizeof *r);
     const int n = s.h_rstate[0].n;
     r->pairs = n;
@@ -798,6 +791,30 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
         r->max_len = std::max(r->max_len, st.max_len);
         if (st.overflow || st.first_bad == n) r->stop = 1;
     }
+}
+
+int fq_engine_raw_wait(fq_engine* e, fq_raw_result* r) {
+    if (!e) return FQ_E_INVALID;
+    if (e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_wait without an enqueued window");
+    HIP_TRY(e, hipSetDevice(e->device));
+    const Slot& s = e->slots[e->raw_queued.front()];
+    HIP_TRY(e, hipEventSynchronize(s.ev_idx));
+    if (r) raw_result_of(e, s, r);
+    return FQ_OK;
+}
+
+int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64_t seq_no) {
+    if (!e || !r || !out) return FQ_E_INVALID;
+    if (e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_launch without an enqueued window");
+    HIP_TRY(e, hipSetDevice(e->device));
+    const int k = e->raw_queued.front();
+    e->raw_queued.pop_front();
+    Slot& s = e->slots[k];
+    HIP_TRY(e, hipEventSynchronize(s.ev_idx));  // (returns at once after fq_engine_raw_wait)
+    const bool pe = e->p.paired;
+    const int mates = pe ? 2 : 1;
+    raw_result_of(e, s, r);
+    const int n = r->pairs;
     out->text.bytes[0] = out->text.bytes[1] = 0;
     out->adapter_bytes[0] = out->adapter_bytes[1] = 0;
     if (n <= 0) {

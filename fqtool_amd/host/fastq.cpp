@@ -2,6 +2,7 @@
 #include "fastq.h"
 
 #include <algorithm>
+#include <climits>
 #include <cerrno>
 #include <atomic>
 #include <chrono>
@@ -1155,6 +1156,10 @@ void Pack::clear() {
     n = 0;
     raw = false;
     recs = false;
+    zc = false;
+    segs[0].clear();
+    segs[1].clear();
+    hold.reset();
     stage = -1;
     rout.results = nullptr;
     rout.rec[0] = rout.rec[1] = nullptr;
@@ -1494,6 +1499,38 @@ void Writer::write_raw(const char* p, size_t n, Pool* pool) {
     std::vector<std::string> blocks;
     for (size_t o = 0; o < n; o += blk) blocks.emplace_back(p + o, std::min(blk, n - o));
     write(blocks, pool);
+}
+
+void Writer::write_segs(const iovec* v, size_t n) {
+    if (!fp_) throw std::runtime_error("write to a closed output");
+    if (gzip_) throw std::runtime_error("byte ranges go to plain outputs only");
+    if (std::fflush(fp_) != 0) throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
+    const int fd = fileno(fp_);
+    std::vector<iovec> part;  // (a short write resumes inside a range)
+    for (size_t i = 0; i < n;) {
+        const size_t k = std::min<size_t>(n - i, (size_t)IOV_MAX);
+        part.assign(v + i, v + i + k);
+        i += k;
+        iovec* q = part.data();
+        size_t left = k;
+        while (left) {
+            const ssize_t w = ::writev(fd, q, (int)left);
+            if (w < 0) {
+                if (errno == EINTR) continue;
+                throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
+            }
+            size_t got = (size_t)w;
+            while (left && got >= q->iov_len) {
+                got -= q->iov_len;
+                ++q;
+                --left;
+            }
+            if (left) {
+                q->iov_base = static_cast<char*>(q->iov_base) + got;
+                q->iov_len -= got;
+            }
+        }
+    }
 }
 
 void Writer::write(const std::vector<std::string>& blocks, Pool* pool) {

@@ -12,6 +12,7 @@
 // from the text on a thread pool.  Writer restates src/writer.cpp (gzip level -z or plain).
 #pragma once
 
+#include <sys/uio.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -282,6 +283,13 @@ struct Pack {
     char* rbuf[2] = {nullptr, nullptr};
     uint64_t rwin[2] = {0, 0}, rcin[2] = {0, 0}, rccap = 0;
     std::function<void(int)> stage_release;  // (records-only: the formatter returns stages through it)
+    // records-only egress to plain outputs (zero copy): each mate's output is a list of byte ranges
+    // -- runs of records that pass untrimmed, straight from the staging window, and the trimmed
+    // records formatted into out_text[m] -- written with writev; `hold` keeps the window until the
+    // writers are through with it
+    bool zc = false;
+    std::vector<iovec> segs[2];
+    std::shared_ptr<void> hold;
 
     // -c: pairs whose bases the engine corrected read their seq/qual from a corrected copy
     // (fix[i] -> seq1 qual1 seq2 qual2 back to back; nullptr = the original text)
@@ -359,6 +367,9 @@ class Writer {
     void write(const std::string& s) { write(std::vector<std::string>{s}); }
     // n bytes from p as they are (gzip: in blocks compressed in parallel on the pool)
     void write_raw(const char* p, size_t n, Pool* pool = nullptr);
+    // plain outputs only: the byte ranges in order (writev)
+    void write_segs(const iovec* v, size_t n);
+    bool gzip() const { return gzip_; }
     void close();  // flushes; throws on a short write or a failed close (full disk)
 
    private:

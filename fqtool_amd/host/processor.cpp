@@ -406,6 +406,15 @@ class Queue {  // bounded FIFO between pipeline threads; push/pop return at once
         not_full_.notify_one();
         return true;
     }
+    // pop_recent without waiting: 1 taken, 0 empty (not closed), -1 closed and drained
+    int try_pop_recent(T& v) {
+        std::lock_guard<std::mutex> l(m_);
+        if (q_.empty()) return closed_ ? -1 : 0;
+        v = std::move(q_.back());
+        q_.pop_back();
+        not_full_.notify_one();
+        return 1;
+    }
     // 1: v taken; 0: empty (not closed); -1: closed and drained
     int try_pop(T& v) {
         std::lock_guard<std::mutex> l(m_);
@@ -452,17 +461,26 @@ class AsyncWriter {
         if (err_) std::rethrow_exception(err_);
         bool any = false;
         for (const auto& s : blocks) any = any || !s.empty();
-        if (any) q_.push(Job{std::move(blocks), nullptr, 0, nullptr});
+        if (any) q_.push(Job{std::move(blocks), nullptr, 0, nullptr, nullptr});
     }
     // queue n bytes at p (which stay valid until `done` runs); the writer thread runs it once the
     // bytes are written (or dropped after a write error)
     void write_raw(const char* p, size_t n, std::function<void()> done) {
-        if (err_ || !q_.push(Job{{}, p, n, done})) {
+        if (err_ || !q_.push(Job{{}, p, n, done, nullptr})) {
             done();  // (the writer has stopped: nothing will take the text)
             if (err_) std::rethrow_exception(err_);
             throw std::runtime_error("write to a closed output");
         }
     }
+    // queue byte ranges (plain outputs; they stay valid until `done` runs), as write_raw
+    void write_segs(const std::vector<iovec>* segs, std::function<void()> done) {
+        if (err_ || !q_.push(Job{{}, nullptr, 0, done, segs})) {
+            done();
+            if (err_) std::rethrow_exception(err_);
+            throw std::runtime_error("write to a closed output");
+        }
+    }
+    bool gzip() const { return w_.gzip(); }
     void close() {
         if (closed_) return;
         closed_ = true;
@@ -484,6 +502,7 @@ class AsyncWriter {
         const char* raw;
         size_t raw_n;
         std::function<void()> done;
+        const std::vector<iovec>* segs = nullptr;
     };
     void loop() {
         Job j;
@@ -491,7 +510,8 @@ class AsyncWriter {
             while (q_.pop(j)) {
                 if (j.done) {
                     try {
-                        w_.write_raw(j.raw, j.raw_n, pool_);
+                        if (j.segs) w_.write_segs(j.segs->data(), j.segs->size());
+                        else w_.write_raw(j.raw, j.raw_n, pool_);
                     } catch (...) {
                         j.done();
                         throw;
@@ -573,6 +593,33 @@ void OutputSet::write_text(const char* t1, size_t n1, const char* t2, size_t n2,
     }
     if (err) std::rethrow_exception(err);
 }
+
+void OutputSet::write_text_segs(const std::vector<iovec>& s1, const std::vector<iovec>& s2, std::function<void()> done) {
+    if (!(w1_ && (!paired_ || w2_))) {
+        done();
+        return;
+    }
+    auto left = std::make_shared<std::atomic<int>>(w2_ ? 2 : 1);
+    auto fin = [left, done] {
+        if (left->fetch_sub(1) == 1) done();
+    };
+    std::exception_ptr err;
+    try {
+        w1_->write_segs(&s1, fin);
+    } catch (...) {
+        err = std::current_exception();
+    }
+    if (w2_) {
+        try {
+            w2_->write_segs(&s2, fin);
+        } catch (...) {
+            if (!err) err = std::current_exception();
+        }
+    }
+    if (err) std::rethrow_exception(err);
+}
+
+bool OutputSet::plain_pair_outputs() const { return (!w1_ || !w1_->gzip()) && (!w2_ || !w2_->gzip()); }
 
 void OutputSet::write_merged_text(const char* t, size_t n, std::function<void()> done) {
     if (!wm_) {
@@ -783,9 +830,12 @@ void Sink::consume(const Pack& pk, const fq_read_result* res) {
     pairs_ += (uint64_t)pk.n;
 }
 
+bool Sink::plain_pair_outputs() const { return outs_ && !merge_ && outs_->plain_pair_outputs(); }
+
 void Sink::consume_text(const Pack& pk, std::function<void()> done) {
     pairs_ += (uint64_t)pk.n;
-    if (merge_) outs_->write_merged_text(pk.out_text[0].data(), pk.tout.bytes[0], std::move(done));
+    if (pk.zc) outs_->write_text_segs(pk.segs[0], pk.segs[1], std::move(done));
+    else if (merge_) outs_->write_merged_text(pk.out_text[0].data(), pk.tout.bytes[0], std::move(done));
     else outs_->write_text(pk.out_text[0].data(), pk.tout.bytes[0], pk.out_text[1].data(), pk.tout.bytes[1], std::move(done));
 }
 
@@ -817,11 +867,13 @@ struct Stopped {};  // another pipeline stage failed and closed the queues
 struct RawPrev {
     char* buf[2] = {nullptr, nullptr};
     uint64_t end[2] = {0, 0};
-    int stage = -1;
-    std::function<void(int)> release;
+    std::shared_ptr<void> hold;  // the previous pack's window, until the next carry is copied from it
 };
 
-void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p, Pool& pool, AdapterCounts& ac) {
+// zc (zero copy, plain outputs): the output is byte ranges (Pack::segs) -- runs of records that pass
+// untrimmed stay in the staging window, only trimmed records are formatted (into out_text) -- and
+// the pack holds its window until the writers are through with it.
+void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p, Pool& pool, AdapterCounts& ac, bool zc) {
     const int mates = pk.paired ? 2 : 1;
     for (int m = 0; m < mates; ++m) {
         char* base = pk.rbuf[m];
@@ -835,10 +887,13 @@ void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p,
         }
         pk.base[m] = base;
     }
-    if (prev.stage >= 0 && prev.release) prev.release(prev.stage);
-    prev.stage = pk.stage;
-    prev.release = pk.stage_release;
+    std::shared_ptr<void> hold;  // (the last owner returns the window to the reader)
+    if (pk.stage >= 0 && pk.stage_release)
+        hold = std::shared_ptr<void>(nullptr, [rel = pk.stage_release, st = pk.stage](void*) { rel(st); });
     pk.stage = -1;
+    prev.hold = hold;  // (the previous window goes back here, unless its writers still hold it)
+    pk.zc = zc;
+    if (zc) pk.hold = hold;
     for (int m = 0; m < mates; ++m) {
         prev.buf[m] = const_cast<char*>(pk.base[m]);
         prev.end[m] = pk.rccap + pk.rwin[m];
@@ -858,6 +913,7 @@ void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p,
     };
     const int parts = std::max(1, std::min(pool.size() * 2, (int)((n + 4095) / 4096)));
     std::vector<size_t> osz((size_t)parts * 2, 0), esz((size_t)parts * 2, 0);
+    auto untrimmed = [](const fq_text_rec& R, const fq_read_result& r) { return r.start == 0 && r.len == R.len; };
     pool.run(parts, [&](int k) {
         const size_t i0 = n * (size_t)k / (size_t)parts, i1 = n * (size_t)(k + 1) / (size_t)parts;
         for (int m = 0; m < mates; ++m) {
@@ -865,7 +921,7 @@ void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p,
             size_t o = 0, e = 0;
             for (size_t i = i0; i < i1; ++i) {
                 const fq_read_result& r = rr(i, m);
-                if (out_ok(i)) o += (size_t)T[i].name_len + T[i].strand_len + 2 * (size_t)r.len + 4;
+                if (out_ok(i) && !(zc && untrimmed(T[i], r))) o += (size_t)T[i].name_len + T[i].strand_len + 2 * (size_t)r.len + 4;
                 if (adapters) e += entry_bytes(r);
             }
             osz[(size_t)(2 * k + m)] = o;
@@ -886,6 +942,7 @@ void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p,
         pk.tout.text[m] = pk.out_text[m].data();
         pk.tout.bytes[m] = otot[m];
     }
+    std::vector<std::vector<iovec>> psegs(zc ? (size_t)parts * 2 : 0);
     pool.run(parts, [&](int k) {
         const size_t i0 = n * (size_t)k / (size_t)parts, i1 = n * (size_t)(k + 1) / (size_t)parts;
         for (int m = 0; m < mates; ++m) {
@@ -893,15 +950,27 @@ void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p,
             const char* t = pk.base[m];
             char* d = pk.out_text[m].data() + osz[(size_t)(2 * k + m)];
             char* ed = pk.out_text[m].data() + otot[m] + esz[(size_t)(2 * k + m)];
+            std::vector<iovec>* sg = zc ? &psegs[(size_t)(2 * k + m)] : nullptr;
+            auto range = [sg](const char* a, size_t len) {  // (contiguous with the last range: one range)
+                if (!sg->empty() && static_cast<const char*>(sg->back().iov_base) + sg->back().iov_len == a)
+                    sg->back().iov_len += len;
+                else
+                    sg->push_back(iovec{const_cast<char*>(a), len});
+            };
             for (size_t i = i0; i < i1; ++i) {
                 const fq_text_rec& R = T[i];
                 const fq_read_result& r = rr(i, m);
-                if (out_ok(i) && r.start == 0 && r.len == R.len) {
+                const char* d0 = d;
+                if (out_ok(i) && untrimmed(R, r)) {
                     // an untrimmed record is its input text as it stands (raw records are "plain":
-                    // four lines, each ending in '\n'): one copy
+                    // four lines, each ending in '\n'): one copy, or (zc) a range of the window
                     const size_t nb = (size_t)R.name_len + R.strand_len + 2 * (size_t)R.len + 4;
-                    std::memcpy(d, t + R.name_off, nb);
-                    d += nb;
+                    if (zc) {
+                        range(t + R.name_off, nb);
+                    } else {
+                        std::memcpy(d, t + R.name_off, nb);
+                        d += nb;
+                    }
                 } else if (out_ok(i)) {
                     std::memcpy(d, t + R.name_off, R.name_len);
                     d += R.name_len;
@@ -915,6 +984,7 @@ void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p,
                     std::memcpy(d, t + R.qual_off + r.start, r.len);
                     d += r.len;
                     *d++ = '\n';
+                    if (zc) range(d0, (size_t)(d - d0));
                 }
                 if (adapters && entry_bytes(r)) {
                     ed[0] = (char)(r.ad_len & 0xFF);
@@ -933,6 +1003,18 @@ void format_raw_recs(Pack& pk, RawPrev& prev, bool adapters, const fq_params& p,
             }
         }
     });
+    if (zc)
+        for (int m = 0; m < mates; ++m) {
+            std::vector<iovec>& v = pk.segs[m];
+            v.clear();
+            for (int k = 0; k < parts; ++k)
+                for (const iovec& x : psegs[(size_t)(2 * k + m)]) {
+                    if (!v.empty() && static_cast<char*>(v.back().iov_base) + v.back().iov_len == x.iov_base)
+                        v.back().iov_len += x.iov_len;
+                    else
+                        v.push_back(x);
+                }
+        }
     if (adapters)
         for (int m = 0; m < mates; ++m) ac.add_entries(m, pk.out_text[m].data() + otot[m], etot[m], p, &pool);
 }
@@ -1128,7 +1210,19 @@ struct RawMulti {
     }
     // offset of the k-th (1-based) line feed in [p, p + n)
     static uint64_t nth_lf(const char* p, size_t n, size_t k) {
-        for (size_t i = 0; i < n; ++i)
+        size_t i = 0;
+        const __m128i nl = _mm_set1_epi8('\n');
+        for (; i + 16 <= n; i += 16) {  // 16 bytes a step; the k-th within a step by its bit mask
+            unsigned mk = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i)), nl));
+            const size_t c = (size_t)__builtin_popcount(mk);
+            if (c < k) {
+                k -= c;
+                continue;
+            }
+            while (--k) mk &= mk - 1;
+            return i + (uint64_t)__builtin_ctz(mk);
+        }
+        for (; i < n; ++i)
             if (p[i] == '\n' && --k == 0) return i;
         throw std::runtime_error("raw window: line feed count mismatch");
     }
@@ -1249,6 +1343,7 @@ struct Lane {
     uint64_t raw_pairs = 0, raw_packs = 0;  // what the raw stream took
     double raw_read_s = 0, raw_stage_wait_s = 0, raw_ready_wait_s = 0;  // window reader: preads, waits
     double raw_pack_wait_s = 0, raw_enqueue_s = 0;  // dispatcher: waiting for a spare pack, enqueue calls
+    double raw_turn_wait_s = 0, raw_idx_wait_s = 0;  // several engines: waiting for the turn, for the own index
     std::string raw_end;                    // why it ended
 
     RawResume run_raw(const std::string* files, int mates, int target, Queue<std::unique_ptr<Pack>>& spare, Pool& pool) {
@@ -1666,10 +1761,33 @@ struct Lane {
                 }
                 if (stop_now || enq.empty()) break;
                 const RawMulti::Win w = enq.front();
+                // Before the turn, on this engine's own time: its window's index (fq_engine_raw_wait)
+                // and a spare pack if one is free.  The turn then only decides the window (the
+                // earlier ones are decided: launch it, or end the stream in it) and passes on; the
+                // launch follows outside it.  (A pack is waited for in the turn only: the earliest
+                // window always gets the next pack back, so the packs in flight cannot all sit with
+                // later windows.)
+                std::unique_ptr<Pack> pk;
+                fq_raw_result r{};
+                if (!w.end) {
+                    const auto x0 = std::chrono::steady_clock::now();
+                    if (fq_engine_raw_wait(e, &r) != FQ_OK)
+                        throw std::runtime_error(std::string("fq_engine_raw_wait: ") + fq_engine_last_error(e));
+                    raw_idx_wait_s += since(x0);
+                    if (spare.try_pop_recent(pk) < 0) throw Stopped();
+                }
+                auto give_back = [&] {
+                    if (pk) spare.push(std::move(pk));
+                };
                 {
+                    const auto t0w = std::chrono::steady_clock::now();
                     std::unique_lock<std::mutex> lk(R.m);
                     R.cv.wait(lk, [&] { return R.stopped || R.next_launch == w.id; });
-                    if (R.stopped) break;
+                    raw_turn_wait_s += since(t0w);
+                    if (R.stopped) {
+                        give_back();
+                        break;
+                    }
                     if (w.end) {  // the input ends (or no whole pair fits): the host reader goes on
                         RawResumeInfo rr;
                         rr.done = true;
@@ -1682,12 +1800,30 @@ struct Lane {
                         enq.pop_front();
                         break;
                     }
+                    if (!pk) {  // (the turn stays ours while the lock is released)
+                        lk.unlock();
+                        const auto p0 = std::chrono::steady_clock::now();
+                        const bool got = spare.pop_recent(pk);
+                        raw_pack_wait_s += since(p0);
+                        lk.lock();
+                        if (!got) throw Stopped();
+                        if (R.stopped) {  // (an error elsewhere)
+                            give_back();
+                            break;
+                        }
+                    }
+                    if (r.pairs != w.pairs || r.stop) {  // the GPU path stops inside this window
+                        RawResumeInfo rr;
+                        for (int m = 0; m < R.mates; ++m) rr.off[m] = w.start[m] + w.n[m] - r.carry[m];
+                        rr.next_seq = w.id + 1;
+                        R.end_locked(rr, std::string(r.stop ? "irregular record" : "short window") + " in window " +
+                                             std::to_string(w.id) + " (" + std::to_string(r.pairs) + " of " +
+                                             std::to_string(w.pairs) + " pairs)");
+                    }
+                    R.next_launch = w.id + 1;
+                    R.cv.notify_all();
                 }
                 enq.pop_front();
-                std::unique_ptr<Pack> pk;
-                const auto p0 = std::chrono::steady_clock::now();
-                if (!spare.pop_recent(pk)) throw Stopped();
-                raw_pack_wait_s += since(p0);
                 pk->clear();
                 pk->raw = true;
                 pk->text_mode = true;
@@ -1702,9 +1838,8 @@ struct Lane {
                     pk->out_text[m].resize_uninit(cap);
                     pk->rout.text.text[m] = m < R.mates ? pk->out_text[m].data() : nullptr;
                 }
-                fq_raw_result r{};
                 const auto e0 = std::chrono::steady_clock::now();
-                if (fq_engine_raw_launch(e, &r, &pk->rout, w.id) != FQ_OK) {
+                if (fq_engine_raw_launch(e, &r, &pk->rout, w.id) != FQ_OK) {  // (r as fq_engine_raw_wait gave it)
                     R.free_stages.push(w.stage);
                     throw std::runtime_error(std::string("fq_engine_raw_launch: ") + fq_engine_last_error(e));
                 }
@@ -1714,19 +1849,6 @@ struct Lane {
                 pk->max_cycles = max_cycles;
                 R.pairs += (uint64_t)r.pairs;
                 ++R.packs;
-                {
-                    std::lock_guard<std::mutex> lk(R.m);
-                    if (r.pairs != w.pairs || r.stop) {  // the GPU path stops inside this window
-                        RawResumeInfo rr;
-                        for (int m = 0; m < R.mates; ++m) rr.off[m] = w.start[m] + w.n[m] - r.carry[m];
-                        rr.next_seq = w.id + 1;
-                        R.end_locked(rr, std::string(r.stop ? "irregular record" : "short window") + " in window " +
-                                             std::to_string(w.id) + " (" + std::to_string(r.pairs) + " of " +
-                                             std::to_string(w.pairs) + " pairs)");
-                    }
-                    R.next_launch = w.id + 1;
-                    R.cv.notify_all();
-                }
                 while (!inflight.empty() && complete_oldest(false)) {
                 }
                 if ((int)inflight.size() >= raw_depth) complete_oldest();
@@ -1962,7 +2084,20 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
                                o.unpaired1.empty() && o.unpaired2.empty() &&
                                (o.merge ? paired && !o.merge_out.empty() && !o.discard_unmerged
                                         : !o.out1.empty() && (!paired || !o.out2.empty()));
+        // records-only raw packs to plain outputs go out as byte ranges of their windows (zero copy)
+        const char* zc_env = std::getenv("FQ_RAW_ZC");  // (profiling: 0 formats every record)
+        const bool zc_ok = outs.plain_pair_outputs() && !(zc_env && std::string(zc_env) == "0");
         std::vector<std::unique_ptr<Lane>> lanes;
+        // (before the lanes go, on any exit: the writers finish with the windows and packs they hold)
+        struct OutsCloser {
+            Sink& s;
+            ~OutsCloser() {
+                try {
+                    s.close();
+                } catch (...) {
+                }
+            }
+        } outs_closer{outs};
         const int cyc0 = std::max(16, round16(o.merge ? 2 * est : est)), stride0 = round16(std::max(est, 16));
         for (int g = 0; g < G; ++g) {
             lanes.emplace_back(new Lane(devices[(size_t)g], depth));
@@ -2110,7 +2245,7 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
             });
         }
         AdapterCounts ac;
-        uint64_t reads = 0;
+        uint64_t reads = 0, recs_packs = 0, zc_packs = 0;
         double format_s = 0;
         std::thread formatter([&] {
             try {
@@ -2121,11 +2256,16 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
                     if (pk->seq_no != k) throw std::runtime_error("packs reached the formatter out of order");
                     const fq_params p = o.to_params(pk->max_cycles);
                     if (pk->raw && pk->recs) {  // records-only egress: the text is formatted here
-                        format_raw_recs(*pk, raw_prev, o.adapter_trimming, p, pool, ac);
+                        format_raw_recs(*pk, raw_prev, o.adapter_trimming, p, pool, ac, zc_ok);
                         format_s += since(f0);
+                        ++recs_packs;
+                        zc_packs += pk->zc;
                         reads += (uint64_t)pk->n * (paired ? 2 : 1);
                         Pack* raw = pk.release();
-                        outs.consume_text(*raw, [raw, &spare] { spare.push(std::unique_ptr<Pack>(raw)); });
+                        outs.consume_text(*raw, [raw, &spare] {
+                            raw->hold.reset();  // (zc: the window goes back once the writers are through)
+                            spare.push(std::unique_ptr<Pack>(raw));
+                        });
                         continue;
                     }
                     if (pk->text_mode) {  // the engine wrote the output text
@@ -2217,17 +2357,27 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
             hs << build_html(o, acc, ac, html_time_now());
         }
         teardown.logged = std::chrono::steady_clock::now();
+        auto sum_lanes = [&](double Lane::*f) {
+            double t = 0;
+            for (auto& l : lanes) t += (*l).*f;
+            return t;
+        };
         log("fqtool-amd: " + std::to_string(reads) + " reads on " + std::to_string(G) + " engine(s)" +
             (raw_mode && rm ? " (raw stream on " + std::to_string(G) + " engines: host-cut pair windows, GPU record indexing, "
                               "ingest/egress: " + std::to_string(rm->pairs.load()) + " pairs in " + std::to_string(rm->packs.load()) +
                               " packs, ended: " + rm->why + "; window reads " + std::to_string(rm->read_s) +
-                              " s, reader waiting for a stage " + std::to_string(rm->stage_wait_s) + " s)"
+                              " s, reader waiting for a stage " + std::to_string(rm->stage_wait_s) + " s; engines waiting for their index " +
+                              std::to_string(sum_lanes(&Lane::raw_idx_wait_s)) + " s, for their turn " +
+                              std::to_string(sum_lanes(&Lane::raw_turn_wait_s)) + " s, for a pack " +
+                              std::to_string(sum_lanes(&Lane::raw_pack_wait_s)) + " s)"
              : raw_mode ? " (raw stream: GPU record indexing, ingest/egress: " + std::to_string(lanes[0]->raw_pairs) + " pairs in " +
                             std::to_string(lanes[0]->raw_packs) + " packs, ended: " + lanes[0]->raw_end + "; window reads " +
                             std::to_string(lanes[0]->raw_read_s) + " s, reader waiting for a stage " +
                             std::to_string(lanes[0]->raw_stage_wait_s) + " s, dispatcher waiting for windows " +
                             std::to_string(lanes[0]->raw_ready_wait_s) + " s, for a pack " + std::to_string(lanes[0]->raw_pack_wait_s) +
-                            " s, in enqueue " + std::to_string(lanes[0]->raw_enqueue_s) + " s)"
+                            " s, in enqueue " + std::to_string(lanes[0]->raw_enqueue_s) + " s" +
+                            (recs_packs ? "; records-only egress: " + std::to_string(recs_packs) + " packs, " + std::to_string(zc_packs) +
+                                              " as byte ranges of their windows" : std::string()) + ")"
                       : text_mode ? " (text packs: GPU ingest/egress)" : "") + ", wall " +
             std::to_string(since(t0)) + " s, engine submit " + std::to_string(submit_s) + " s, wait " + std::to_string(wait_s) + " s; pre-pass " +
             std::to_string(prepass_s) + " s, adapter detection (concurrent) " + std::to_string(detect_s) + " s, format " + std::to_string(format_s) + " s, parse " + std::to_string(parse_s) +

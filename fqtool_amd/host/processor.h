@@ -37,6 +37,9 @@ class OutputSet {
     // out1 / out2 text as is (waits until both writers have taken it)
     // queue engine-assembled output text of both mates; `done` runs once both are written
     void write_text(const char* t1, size_t n1, const char* t2, size_t n2, std::function<void()> done);
+    // the same as byte ranges (plain outputs: writev); the ranges stay valid until `done` runs
+    void write_text_segs(const std::vector<iovec>& s1, const std::vector<iovec>& s2, std::function<void()> done);
+    bool plain_pair_outputs() const;  // out1 / out2 (those that exist) are not gzip
     // -m: a text pack's merged stream (the merged output; out1 / out2 get nothing)
     void write_merged_text(const char* t, size_t n, std::function<void()> done);
     void close();  // flushes and closes every file
@@ -65,6 +68,7 @@ class Sink {
     // write a text pack's engine-assembled output (no split); `done` runs (on a writer thread) once
     // the pack's text is written
     void consume_text(const Pack& pk, std::function<void()> done);
+    bool plain_pair_outputs() const;  // text packs may go out as byte ranges (Pack::zc)
     void close();
 
    private:

@@ -449,6 +449,11 @@ typedef struct fq_raw_out {
 int fq_engine_raw_begin(fq_engine* e, uint64_t window_cap, uint64_t carry_cap);
 int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w);
 int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64_t seq_no);
+/* Waits until the oldest enqueued (not launched) window is indexed and reports its pack's pairs,
+ * stop, carry and text bytes as fq_engine_raw_launch of it will (r may be null); that launch then
+ * does not wait.  A caller ordering launches over several engines waits here, on each engine's own
+ * thread, before it takes its turn (no counterpart in the reference: its reader is one thread). */
+int fq_engine_raw_wait(fq_engine* e, fq_raw_result* r);
 /* Leaves raw mode: waits for the copies and indexing of windows enqueued and never launched (their
  * host bytes may then be reused) and drops them; launched packs are polled as usual.  The engine
  * takes other packs, or a new fq_engine_raw_begin once nothing is in flight. */

@@ -536,6 +536,26 @@ int fq_engine_raw_enqueue(fq_engine* e, const fq_raw_window* w) {
     return FQ_OK;
 }
 
+static void raw_result_of(const fq_engine* e, const RawWin& w, fq_raw_result* r) {
+    std::memset(r, 0, sizeof *r);
+    r->pairs = w.n;
+    r->max_len = w.max_len;
+    for (int m = 0; m < (e->p.paired ? 2 : 1); ++m) {
+        r->carry[m] = w.overflow[m] ? (uint64_t)w.carry_in[m] + w.nraw[m] : (uint64_t)(w.avail[m] - w.consumed[m]);
+        r->text_bytes[m] = w.consumed[m];
+        if (w.overflow[m] || w.first_bad[m] == w.n) r->stop = 1;
+    }
+}
+
+int fq_engine_raw_wait(fq_engine* e, fq_raw_result* r) {
+    if (!e) return FQ_E_INVALID;
+    if (e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_wait without an enqueued window");
+    const std::shared_ptr<RawWin> w = e->raw_queued.front();
+    e->wait(w->indexed);
+    if (r) raw_result_of(e, *w, r);
+    return FQ_OK;
+}
+
 int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64_t seq_no) {
     if (!e || !r || !out) return FQ_E_INVALID;
     if (e->raw_queued.empty()) return fail(e, FQ_E_INVALID, "fq_engine_raw_launch without an enqueued window");
@@ -544,15 +564,8 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     e->wait(w->indexed);  // (the window's index: waits as the device's launch does)
     const bool pe = e->p.paired;
     const int mates = pe ? 2 : 1;
-    std::memset(r, 0, sizeof *r);
+    raw_result_of(e, *w, r);
     const int n = w->n;
-    r->pairs = n;
-    r->max_len = w->max_len;
-    for (int m = 0; m < mates; ++m) {
-        r->carry[m] = w->overflow[m] ? (uint64_t)w->carry_in[m] + w->nraw[m] : (uint64_t)(w->avail[m] - w->consumed[m]);
-        r->text_bytes[m] = w->consumed[m];
-        if (w->overflow[m] || w->first_bad[m] == n) r->stop = 1;
-    }
     out->text.bytes[0] = out->text.bytes[1] = 0;
     out->adapter_bytes[0] = out->adapter_bytes[1] = 0;
     if (n <= 0) {

@@ -44,7 +44,7 @@ RAW_CASES = ("td_pe_qag", "td_pe_plain", "td_pe_detect", "synth_pe_c3", "synth_p
              "edge_pe_dup", "td_se_q", "td_pe_merge", "synth_pe_c4", "edge_pe_merge")
 
 
-@pytest.mark.parametrize("devices", ["0", "0,0,0"])
+@pytest.mark.parametrize("devices", ["0", "0,0,0", "0,0,0,0"])
 @pytest.mark.parametrize("case", E.ok_cases())
 def test_raw_stream_small_windows_cpu(case, devices, cpu_build, tmp_path):
     ind, outd = tmp_path / "in", tmp_path / "out"
@@ -63,21 +63,33 @@ def test_raw_stream_small_windows_cpu(case, devices, cpu_build, tmp_path):
     if case in RAW_CASES:
         assert "raw stream" in err, err[-1000:]
         if multi:
-            assert "raw stream on 3 engines" in err, err[-1000:]
+            assert "raw stream on %d engines" % len(devices.split(",")) in err, err[-1000:]
     E.check_outputs(case, str(outd))
 
 
-@pytest.mark.parametrize("case", ["td_pe_qag", "synth_pe_c3", "td_pe_merge", "synth_se_c2", "edge_pe_all"])
-def test_records_only_egress_cpu(case, cpu_build, tmp_path):
-    """FQ_RAW_EGRESS=host: the engine returns records and line offsets, the host formats from its
-    staging windows (the carry in front of each window included)."""
+@pytest.mark.parametrize("zc", ["1", "0"])
+@pytest.mark.parametrize("case", ["td_pe_qag", "synth_pe_c3", "td_pe_merge", "synth_se_c2", "edge_pe_all", "td_pe_plain",
+                                  "td_se_q", "polygr_pe"])
+def test_records_only_egress_cpu(case, zc, cpu_build, tmp_path):
+    """FQ_RAW_EGRESS=host (one engine): the engine returns records and line offsets, the host formats
+    from its staging windows (the carry in front of each window included) -- with plain outputs as
+    byte ranges of the windows written by writev (FQ_RAW_ZC=1, the default), or copied (0)."""
     ind, outd = tmp_path / "in", tmp_path / "out"
     ind.mkdir()
     outd.mkdir()
-    argv = plain_inputs(E.argv_for(CPU_BIN, case, str(outd)), str(ind)) + ["--pack_pairs", "7", "--devices", "0,0,0"]
-    env = dict(os.environ, FQ_RAW_WINDOW0="4096", FQ_RAW_EGRESS="host")
+    argv = plain_inputs(E.argv_for(CPU_BIN, case, str(outd)), str(ind)) + ["--pack_pairs", "7"]
+    env = dict(os.environ, FQ_RAW_WINDOW0="4096", FQ_RAW_EGRESS="host", FQ_RAW_ZC=zc)
     p = subprocess.run(argv, capture_output=True, cwd=outd, timeout=300, env=env)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
+    err = p.stderr.decode(errors="replace")
+    if case in RAW_CASES:
+        assert "raw stream" in err, err[-1000:]
+        import re
+        m = re.search(r"records-only egress: (\d+) packs, (\d+) as byte ranges", err)
+        if "-m" not in E.manifest()[case]["args"].split():
+            assert m and int(m.group(1)) > 0, err[-1000:]
+            plain = not any(a.endswith(".gz") for a in argv if a.startswith(str(outd)))
+            assert int(m.group(2)) == (int(m.group(1)) if zc == "1" and plain else 0), err[-1000:]
     E.check_outputs(case, str(outd))
 
 

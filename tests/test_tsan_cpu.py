@@ -41,18 +41,26 @@ def test_bgzf_inputs_under_tsan(workers, tsan_build, tmp_path):
     assert reports == 0, err[-6000:]
 
 
-@pytest.mark.parametrize("case,egress", [("td_pe_qag", "text"), ("td_pe_merge", "text"), ("synth_pe_c3", "text"),
-                                         ("td_se_q", "text"), ("td_pe_qag", "host"), ("td_pe_merge", "host")])
-def test_raw_stream_under_tsan(case, egress, tsan_build, tmp_path):
-    """The raw stream on three engines (plain inputs, 4 KiB first window, 7-pair packs): the window
-    reader thread, the per-engine threads with RawMulti's ordered enqueue / launch hand-offs and
-    stage queues, end_locked, the host reader's resume, and (egress "host") the records-only
-    formatter handing staging windows back."""
+@pytest.mark.parametrize("case,devices", [("td_pe_qag", 3), ("td_pe_merge", 3), ("synth_pe_c3", 3), ("td_se_q", 3),
+                                          ("td_pe_qag", 4), ("td_pe_merge", 4)])
+def test_raw_stream_under_tsan(case, devices, tsan_build, tmp_path):
+    """The raw stream on three / four engines (plain inputs, 4 KiB first window, 7-pair packs): the
+    window reader thread, the per-engine threads with RawMulti's index waits, ordered turns and
+    stage queues, end_locked, and the host reader's resume."""
     env = {"FQ_RAW_WINDOW0": "4096"}
-    if egress == "host":
-        env["FQ_RAW_EGRESS"] = "host"
-    err, reports = T.run_case(case, str(tmp_path), 4, devices=3, mode="raw", env_extra=env, pack_pairs=7)
-    assert "raw stream on 3 engines" in err, err[-3000:]
+    err, reports = T.run_case(case, str(tmp_path), 4, devices=devices, mode="raw", env_extra=env, pack_pairs=7)
+    assert "raw stream on %d engines" % devices in err, err[-3000:]
+    assert reports == 0, err[-6000:]
+
+
+@pytest.mark.parametrize("case,zc", [("td_pe_qag", "1"), ("synth_pe_c3", "1"), ("td_se_q", "1"), ("td_pe_qag", "0")])
+def test_records_only_egress_under_tsan(case, zc, tsan_build, tmp_path):
+    """Records-only egress on one engine (FQ_RAW_EGRESS=host): the formatter copies each carry from
+    the previous window and hands windows back through shared holds; with zero copy (FQ_RAW_ZC=1)
+    the writer threads write byte ranges of the windows and release them when done."""
+    env = {"FQ_RAW_WINDOW0": "4096", "FQ_RAW_EGRESS": "host", "FQ_RAW_ZC": zc}
+    err, reports = T.run_case(case, str(tmp_path), 4, devices=1, mode="raw", env_extra=env, pack_pairs=7)
+    assert "records-only egress" in err, err[-3000:]
     assert reports == 0, err[-6000:]
 
 

@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--workers", default="16", help="comma list of -w values")
     ap.add_argument("--out", default="null", choices=["null", "file"])
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--egress", default="text", help="comma list: text (engine output text), host (records-only, "
+                    "byte ranges), hostcopy (records-only, copied); host* run on one engine only")
     args = ap.parse_args()
     libdir = build_null_engine()
     tool = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
@@ -78,16 +80,24 @@ def main():
         gb = 2 * args.pairs * REC / 1e9
         print(json.dumps({"input_GB": round(gb, 3), "pairs": args.pairs, "written_s": round(time.time() - t0, 1),
                           "host_cpus": os.cpu_count()}), flush=True)
-        env = dict(os.environ, LD_LIBRARY_PATH=libdir, FQ_NULL_REC1=str(REC), FQ_NULL_REC2=str(REC))
-        for w in [int(x) for x in args.workers.split(",")]:
-            for g in [int(x) for x in args.engines.split(",")]:
+        env = dict(os.environ, LD_LIBRARY_PATH=libdir, FQ_NULL_REC1=str(REC), FQ_NULL_REC2=str(REC), FQ_NULL_LEN=str(READ_LEN))
+        runs = []
+        for eg in args.egress.split(","):
+            for w in [int(x) for x in args.workers.split(",")]:
+                for g in [int(x) for x in args.engines.split(",")]:
+                    if eg == "text" or g == 1:
+                        runs.append((eg, w, g))
+        for eg, w, g in runs:
+                env_run = dict(env)
+                if eg != "text":
+                    env_run.update(FQ_RAW_EGRESS="host", FQ_RAW_ZC="1" if eg == "host" else "0")
                 outs = ["/dev/null", "/dev/null"] if args.out == "null" else [os.path.join(tmp, "o1.fq"), os.path.join(tmp, "o2.fq")]
                 cmd = [tool, "-i", ins[0], "-I", ins[1], "-o", outs[0], "-O", outs[1], "-q", "-g", "-w", str(w),
                        "--devices", ",".join(["0"] * g), "-J", os.path.join(tmp, "r.json"), "-H", os.path.join(tmp, "r.html")]
                 for rep in range(args.repeat):
                     time.sleep(1.0)
                     t0 = time.perf_counter()
-                    p = subprocess.run(cmd, capture_output=True, text=True, env=env)
+                    p = subprocess.run(cmd, capture_output=True, text=True, env=env_run)
                     dt = time.perf_counter() - t0
                     if p.returncode != 0:
                         print(json.dumps({"engines": g, "workers": w, "error": p.stderr[-1500:]}), flush=True)
@@ -97,12 +107,13 @@ def main():
                     def stamp(key):
                         mm = re.search(key + r" ([0-9.]+) s", line)
                         return float(mm.group(1)) if mm else None
-                    print(json.dumps({"engines": g, "workers": w, "out": args.out, "rep": rep, "wall_s": round(dt, 3),
+                    print(json.dumps({"engines": g, "workers": w, "out": args.out, "egress": eg, "rep": rep, "wall_s": round(dt, 3),
                                       "input_GB_s": round(gb / dt, 2), "Mreads_s": round(2 * args.pairs / dt / 1e6, 1),
                                       "window_reads_s": stamp("window reads"),
                                       "reader_waiting_for_stage_s": stamp("reader waiting for a stage"),
                                       "pipeline_done_at_s": stamp("pipeline done at"),
                                       "first_pack_at_s": stamp("first pack submitted at"),
+                                      "format_s": stamp("format"),
                                       "path": "raw stream on %d engines" % g if "raw stream on" in line else
                                               ("raw stream" if "raw stream" in line else "other")}), flush=True)
                     for f in outs:

@@ -32,6 +32,9 @@ struct fq_engine {
     std::deque<fq_raw_window> queued;
     uint64_t rec[2] = {0, 0};
     uint64_t carry[2] = {0, 0};  // bytes after the last whole record (one engine: windows cut anywhere)
+    uint64_t ccap = 0;           // carry capacity (records-only egress: offsets into [carry | window])
+    int len = 150;               // read length of the fixed-width records (FQ_NULL_LEN)
+    uint64_t max_batch = 0;      // pairs a pack takes at most (as the engine's)
 };
 struct fq_dup {
     int unused;
@@ -42,15 +45,18 @@ struct fq_kmer_set {
 
 extern "C" {
 
-int fq_engine_create(const fq_params* params, int, int32_t, int32_t, fq_engine** out) {
+int fq_engine_create(const fq_params* params, int, int32_t max_batch, int32_t, fq_engine** out) {
     if (!params || !out) return FQ_E_INVALID;
     fq_engine* e = new fq_engine();
+    e->max_batch = (uint64_t)max_batch;
     e->p = *params;
     e->acc_words = fq_acc_words(params->insert_size_max, params->max_cycles);
     const char* r1 = std::getenv("FQ_NULL_REC1");
     const char* r2 = std::getenv("FQ_NULL_REC2");
     e->rec[0] = r1 ? std::strtoull(r1, nullptr, 10) : 0;
     e->rec[1] = r2 ? std::strtoull(r2, nullptr, 10) : e->rec[0];
+    const char* ln = std::getenv("FQ_NULL_LEN");
+    if (ln) e->len = std::atoi(ln);
     *out = e;
     return FQ_OK;
 }
@@ -88,7 +94,8 @@ int fq_engine_poll(fq_engine* e, int, uint64_t* seq_no) {
     return 1;
 }
 
-int fq_engine_raw_begin(fq_engine* e, uint64_t, uint64_t) {
+int fq_engine_raw_begin(fq_engine* e, uint64_t, uint64_t carry_cap) {
+    e->ccap = (carry_cap + 4095) / 4096 * 4096;
     if (!e->rec[0]) {
         e->err = "null engine: set FQ_NULL_REC1 (bytes per record of the fixed-width input)";
         return FQ_E_INVALID;
@@ -109,8 +116,10 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     const int mates = e->p.paired ? 2 : 1;
     uint64_t pairs = ~0ull;
     for (int m = 0; m < mates; ++m) pairs = std::min(pairs, (e->carry[m] + w.n[m]) / e->rec[m]);
+    pairs = std::min(pairs, e->max_batch);
     r->pairs = (int32_t)pairs;
-    r->max_len = 150;
+    r->max_len = e->len;
+    uint64_t cin[2] = {e->carry[0], e->carry[1]};
     for (int m = 0; m < mates; ++m) {
         r->text_bytes[m] = pairs * e->rec[m];
         e->carry[m] = e->carry[m] + w.n[m] - r->text_bytes[m];
@@ -118,7 +127,48 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
     }
     out->adapter_bytes[0] = out->adapter_bytes[1] = 0;
     out->text.bytes[0] = out->text.bytes[1] = 0;
+    if (out->results) {  // records-only egress: every pair passes, every fourth trimmed by 10 bases
+        const int L = e->len;
+        for (uint64_t i = 0; i < pairs; ++i)
+            for (int m = 0; m < mates; ++m) {
+                fq_read_result& rr = out->results[mates * i + m];
+                std::memset(&rr, 0, sizeof rr);
+                rr.code = FQ_PASS_FILTER;
+                rr.len = (uint16_t)(i % 4 == 3 ? L - 10 : L);
+                if (i % 4 == 3) {
+                    rr.flags = FQ_RF_AD_SEQ;
+                    rr.ad_pos = (uint16_t)(L - 10);
+                    rr.ad_len = 10;
+                }
+                fq_text_rec& t = out->rec[m][i];
+                t.name_off = (uint32_t)(e->ccap - cin[m] + i * e->rec[m]);
+                t.name_len = (uint16_t)(e->rec[m] - 2 * (uint64_t)L - 5);
+                t.seq_off = t.name_off + t.name_len + 1;
+                t.strand_off = t.seq_off + (uint32_t)L + 1;
+                t.strand_len = 1;
+                t.qual_off = t.strand_off + 2;
+                t.len = (uint16_t)L;
+            }
+    }
     e->pending.push_back({seq_no, &out->text, {r->text_bytes[0], mates > 1 ? r->text_bytes[1] : 0}});
+    return FQ_OK;
+}
+int fq_engine_raw_wait(fq_engine* e, fq_raw_result* r) {
+    if (e->queued.empty()) return FQ_E_INVALID;
+    if (r) {  // (the same figures the launch computes, without taking the window)
+        std::memset(r, 0, sizeof *r);
+        const fq_raw_window& w = e->queued.front();
+        const int mates = e->p.paired ? 2 : 1;
+        uint64_t pairs = ~0ull;
+        for (int m = 0; m < mates; ++m) pairs = std::min(pairs, (e->carry[m] + w.n[m]) / e->rec[m]);
+        pairs = std::min(pairs, e->max_batch);
+        r->pairs = (int32_t)pairs;
+        r->max_len = 150;
+        for (int m = 0; m < mates; ++m) {
+            r->text_bytes[m] = pairs * e->rec[m];
+            r->carry[m] = e->carry[m] + w.n[m] - r->text_bytes[m];
+        }
+    }
     return FQ_OK;
 }
 int fq_engine_raw_end(fq_engine* e) {
