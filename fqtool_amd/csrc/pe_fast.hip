@@ -147,6 +147,12 @@ namespace {
 #ifndef FQ_OV_SH64
 #define FQ_OV_SH64 1  // overlap candidates: planes realigned by 64-bit shifts (one block per pass)
 #endif
+#ifndef FQ_OV12
+#define FQ_OV12 0  // overlap candidates at the default limit 5 from the first 12 positions (not 16): slower (a false candidate in any lane costs the wave an exact check; profiles/r05_ab_ov12_stvcc.txt)
+#endif
+#ifndef FQ_ST_VCC
+#define FQ_ST_VCC 0  // removed-mode Stats: the rotation selects as VCC-masked v_cndmask_e32 (no gain measured, profiles/r05_ab_ov12_stvcc.txt)
+#endif
 #ifndef FQ_PREFETCH
 #define FQ_PREFETCH 0  // profiling: after staging, pull the first FQ_PREFETCH chunks of the wave's next tile
                        // toward L2 with LDS-DMA loads (0: off; measured slower at 10)
@@ -569,6 +575,29 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
             const uint32_t fl = (uint32_t)__builtin_amdgcn_sbfe((int)fu, j, 1);
             return (hs ^ fh) | (ls ^ fl);
         };
+        uint32_t lt;
+#if FQ_OV12
+        if (K == 5) {
+            // the default limit: an accepted offset has < 5 mismatches in its first min(ol, 50)
+            // positions, so in its first 12 (ol >= 16 here) -- a weaker filter than 16 positions
+            // (~0.3 random candidates per 120 offsets instead of ~0.004, each one exact check) at
+            // three quarters of the cost
+            uint32_t ones = 0u, twos = 0u, fours = 0u, twosA, twosB, foursA, foursB, eightsA;
+            csa(twosA, ones, ones, m(0), m(1));
+            csa(twosB, ones, ones, m(2), m(3));
+            csa(foursA, twos, twos, twosA, twosB);
+            csa(twosA, ones, ones, m(4), m(5));
+            csa(twosB, ones, ones, m(6), m(7));
+            csa(foursB, twos, twos, twosA, twosB);
+            csa(eightsA, fours, fours, foursA, foursB);
+            csa(twosA, ones, ones, m(8), m(9));
+            csa(twosB, ones, ones, m(10), m(11));
+            csa(foursA, twos, twos, twosA, twosB);
+            // count = ones + 2 twos + 4 (fours + foursA) + 8 eightsA < 5
+            lt = ~(eightsA | (fours & foursA) | ((fours | foursA) & (twos | ones)));
+        } else
+#endif
+        {
         // 16 vectors -> bit-sliced 5-bit counts, Harley-Seal carry-save order (few live values)
         uint32_t ones = 0u, twos = 0u, fours = 0u, eights = 0u, sixteen, twosA, twosB, foursA, foursB, eightsA, eightsB;
         csa(twosA, ones, ones, m(0), m(1));
@@ -585,7 +614,6 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
         csa(twosB, ones, ones, m(14), m(15));
         csa(foursB, twos, twos, twosA, twosB);
         csa(eightsB, fours, fours, foursA, foursB);
-        uint32_t lt;
         if (K == 5) {  // the default overlap_diff_limit: count < 5 <=> no 8s or 16s, not (4 and (2 or 1))
             lt = ~(eights | eightsA | eightsB | (fours & (twos | ones)));
         } else {  // count < K, bit-sliced against the wave-uniform K
@@ -603,6 +631,7 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
                 }
             }
             if (K > 31) lt = ~0u;
+        }
         }
         const int nb = cnt - 32 * bk;  // valid offsets of this block
         cand[bk] = lt & (nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u));
@@ -2027,7 +2056,12 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             // post block at other cycles, below, and read 2's own bases only to its pre block)
             const int wlen = post_on && !(MERGE && merged && mate) ? wn : 0;
             const int dsel = r >> 2, rr4 = 4 * (r & 7);
-            const bool rswap = r >= 8;
+            [[maybe_unused]] const bool rswap = r >= 8;
+#if FQ_ST_VCC
+            // the lanes whose rotation takes the next dword / the other half (dsel & 2 == rswap)
+            const unsigned long long msel1 = __builtin_amdgcn_ballot_w64((dsel & 1) != 0);
+            const unsigned long long msel2 = __builtin_amdgcn_ballot_w64((dsel & 2) != 0);
+#endif
             // LDS byte address of rotated position t's cell in slot 0 of chunk 0 (this mate's rows):
             // bits 8-11 are clear, the slot nibble is or-ed in (rcell)
             static_assert((LY::kColsW * 4) % 4096 == 0, "removed-mode rows: 4 KiB aligned");
@@ -2170,12 +2204,40 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     }
 #endif
                     // rotate by r positions: rotated position t is 16F + (t + r) % 16
+#if FQ_ST_VCC
+                    // (the ten selects against two per-lane masks: left to itself the compiler keeps
+                    // both masks in SGPR pairs and issues v_cndmask_b32_e64 at half rate; with the
+                    // mask in VCC the e32 form issues at full rate)
+                    uint32_t xa, xb, a0, a1, a2, a3;
+                    {
+                        uint32_t t0, t1, t2, t3;
+                        asm("s_mov_b64 vcc, %[m1]\n\t"
+                            "v_cndmask_b32_e32 %[t0], %[q0], %[q1], vcc\n\t"
+                            "v_cndmask_b32_e32 %[t1], %[q1], %[q2], vcc\n\t"
+                            "v_cndmask_b32_e32 %[t2], %[q2], %[q3], vcc\n\t"
+                            "v_cndmask_b32_e32 %[t3], %[q3], %[q0], vcc\n\t"
+                            "s_mov_b64 vcc, %[m2]\n\t"
+                            "v_cndmask_b32_e32 %[a0], %[t0], %[t2], vcc\n\t"
+                            "v_cndmask_b32_e32 %[a1], %[t1], %[t3], vcc\n\t"
+                            "v_cndmask_b32_e32 %[a2], %[t2], %[t0], vcc\n\t"
+                            "v_cndmask_b32_e32 %[a3], %[t3], %[t1], vcc\n\t"
+                            "v_cndmask_b32_e32 %[xa], %[lo], %[hi], vcc\n\t"
+                            "v_cndmask_b32_e32 %[xb], %[hi], %[lo], vcc"
+                            : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [a0] "=&v"(a0),
+                              [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [xa] "=&v"(xa), [xb] "=&v"(xb)
+                            : [m1] "s"(msel1), [m2] "s"(msel2), [q0] "v"(q0), [q1] "v"(q1), [q2] "v"(q2), [q3] "v"(q3),
+                              [lo] "v"(lo), [hi] "v"(hi)
+                            : "vcc");
+                    }
+                    const uint32_t klo = __builtin_amdgcn_alignbit(xb, xa, rr4), khi = __builtin_amdgcn_alignbit(xa, xb, rr4);
+#else
                     const uint32_t xa = rswap ? hi : lo, xb = rswap ? lo : hi;
                     const uint32_t klo = __builtin_amdgcn_alignbit(xb, xa, rr4), khi = __builtin_amdgcn_alignbit(xa, xb, rr4);
                     const uint32_t t0 = (dsel & 1) ? q1 : q0, t1 = (dsel & 1) ? q2 : q1;
                     const uint32_t t2 = (dsel & 1) ? q3 : q2, t3 = (dsel & 1) ? q0 : q3;
                     const uint32_t a0 = (dsel & 2) ? t2 : t0, a1 = (dsel & 2) ? t3 : t1;
                     const uint32_t a2 = (dsel & 2) ? t0 : t2, a3 = (dsel & 2) ? t1 : t3;
+#endif
                     // quality bytes (< 128 here): the low word of a cell increment
                     const uint32_t qr[4] = {__builtin_amdgcn_alignbyte(a1, a0, r & 3), __builtin_amdgcn_alignbyte(a2, a1, r & 3),
                                             __builtin_amdgcn_alignbyte(a3, a2, r & 3), __builtin_amdgcn_alignbyte(a0, a3, r & 3)};
