@@ -1346,7 +1346,7 @@ struct Lane {
     double raw_turn_wait_s = 0, raw_idx_wait_s = 0;  // several engines: waiting for the turn, for the own index
     std::string raw_end;                    // why it ended
 
-    RawResume run_raw(const std::string* files, int mates, int target, Queue<std::unique_ptr<Pack>>& spare, Pool& pool) {
+    RawResume run_raw(const std::string* files, int mates, int target, int est_len, Queue<std::unique_ptr<Pack>>& spare, Pool& pool) {
         RawResume rr;
         int fd[2] = {-1, -1};
         uint64_t size[2] = {0, 0};
@@ -1371,7 +1371,12 @@ struct Lane {
         // make smaller packs: every page-locked byte costs ~40 ms/GiB again when the process exits,
         // tools/micro/exit_cost), 16 MiB of
         // carry (partial records, the mates' imbalance); six windows in the engine at once
-        const uint64_t wcap = (uint64_t)48 << 20, ccap = (uint64_t)16 << 20;
+        // (smaller packs, --pack_pairs: windows of ~1.3 packs of the estimated record size, so the
+        // page-locked stages shrink with them)
+        const uint64_t rec_est = 2 * (uint64_t)std::max(est_len, 16) + 72;
+        const uint64_t wfit = ((uint64_t)(1.3 * (double)target * (double)rec_est) + ((uint64_t)1 << 20)) & ~(((uint64_t)1 << 20) - 1);
+        const uint64_t wcap = std::min<uint64_t>((uint64_t)48 << 20, std::max<uint64_t>((uint64_t)4 << 20, wfit));
+        const uint64_t ccap = (uint64_t)16 << 20;
         // records-only egress (FQ_RAW_EGRESS=host): the engine sends back records and line offsets,
         // the formatter writes the output from the staging window, which then keeps the carry
         // capacity free in front of the window bytes (the device buffer's layout)
@@ -2228,7 +2233,7 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
                         rr.done = true;
                         try {
                             const std::string files[2] = {o.in1, o.in2};
-                            rr = l->run_raw(files, paired ? 2 : 1, (int)pack_n, spare, pool);
+                            rr = l->run_raw(files, paired ? 2 : 1, (int)pack_n, est, spare, pool);
                         } catch (...) {
                             raw_p.set_value(rr);
                             throw;
