@@ -1408,6 +1408,56 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
 Writer::Writer(const std::string& path, int level) : gzip_(ends_with(path, ".gz")), level_(level) {
     fp_ = std::fopen(path.c_str(), "wb");
     if (!fp_) throw std::runtime_error("cannot open " + path);
+    struct stat st;
+    positional_ = !gzip_ && fstat(fileno(fp_), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+void Writer::write_at(uint64_t off, const char* p, size_t n) {
+    const int fd = fileno(fp_);
+    while (n) {
+        const ssize_t w = ::pwrite(fd, p, n, (off_t)off);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
+        }
+        if (w == 0) throw std::runtime_error("write failed: no progress");
+        p += w;
+        n -= (size_t)w;
+        off += (uint64_t)w;
+    }
+}
+
+void Writer::write_segs_at(uint64_t off, const iovec* v, size_t n) {
+    const int fd = fileno(fp_);
+    std::vector<iovec> part;  // (a short write resumes inside a range)
+    for (size_t i = 0; i < n;) {
+        const size_t k = std::min<size_t>(n - i, (size_t)IOV_MAX);
+        part.assign(v + i, v + i + k);
+        i += k;
+        iovec* q = part.data();
+        size_t left = k;
+        while (left && q->iov_len == 0) ++q, --left;
+        while (left) {
+            const ssize_t w = ::pwritev(fd, q, (int)left, (off_t)off);
+            if (w < 0) {
+                if (errno == EINTR) continue;
+                throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
+            }
+            if (w == 0) throw std::runtime_error("write failed: no progress");
+            off += (uint64_t)w;
+            size_t got = (size_t)w;
+            while (left && got >= q->iov_len) {
+                got -= q->iov_len;
+                ++q;
+                --left;
+            }
+            if (left) {
+                q->iov_base = static_cast<char*>(q->iov_base) + got;
+                q->iov_len -= got;
+            }
+            while (left && q->iov_len == 0) ++q, --left;
+        }
+    }
 }
 
 namespace {
@@ -1491,6 +1541,10 @@ void Writer::close() {
 void Writer::write_raw(const char* p, size_t n, Pool* pool) {
     if (!fp_) throw std::runtime_error("write to a closed output");
     if (!n) return;
+    if (positional_) {
+        write_at(claim(n), p, n);
+        return;
+    }
     if (!gzip_) {
         if (std::fwrite(p, 1, n, fp_) != n) throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
         return;
@@ -1504,6 +1558,12 @@ void Writer::write_raw(const char* p, size_t n, Pool* pool) {
 void Writer::write_segs(const iovec* v, size_t n) {
     if (!fp_) throw std::runtime_error("write to a closed output");
     if (gzip_) throw std::runtime_error("byte ranges go to plain outputs only");
+    if (positional_) {
+        size_t bytes = 0;
+        for (size_t i = 0; i < n; ++i) bytes += v[i].iov_len;
+        write_segs_at(claim(bytes), v, n);
+        return;
+    }
     if (std::fflush(fp_) != 0) throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
     const int fd = fileno(fp_);
     std::vector<iovec> part;  // (a short write resumes inside a range)
@@ -1535,6 +1595,11 @@ void Writer::write_segs(const iovec* v, size_t n) {
 
 void Writer::write(const std::vector<std::string>& blocks, Pool* pool) {
     if (!fp_) throw std::runtime_error("write to a closed output");
+    if (positional_) {
+        for (const auto& s : blocks)
+            if (!s.empty()) write_at(claim(s.size()), s.data(), s.size());
+        return;
+    }
     if (!gzip_) {
         for (const auto& s : blocks) put(fp_, s);
         return;

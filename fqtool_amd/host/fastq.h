@@ -370,11 +370,24 @@ class Writer {
     // plain outputs only: the byte ranges in order (writev)
     void write_segs(const iovec* v, size_t n);
     bool gzip() const { return gzip_; }
+    // Plain regular files are written with pwrite at offsets claimed in output order (no stdio
+    // buffer), so several threads can write claimed ranges at once (AsyncWriter); claim() is
+    // called in order by one thread, write_at / write_segs_at from any.
+    bool positional() const { return positional_; }
+    uint64_t claim(size_t n) {
+        const uint64_t o = off_;
+        off_ += n;
+        return o;
+    }
+    void write_at(uint64_t off, const char* p, size_t n);
+    void write_segs_at(uint64_t off, const iovec* v, size_t n);
     void close();  // flushes; throws on a short write or a failed close (full disk)
 
    private:
     FILE* fp_ = nullptr;
     bool gzip_ = false;
+    bool positional_ = false;
+    uint64_t off_ = 0;
     bool any_member_ = false;
     int level_ = 4;
 };

@@ -94,6 +94,9 @@ def run(tool, r1, r2, d, tag, cfg, workers, extra=(), null_out=False):
         env[k] = v
         cmd.remove(tok)
     env["FQ_TIMING_MONO"] = "1"  # (the tool's steady-clock stamps: exec and exit time from outside)
+    for k in ("o1.fq", "o2.fq", "m.fq"):  # (a fresh file each run: rewriting a truncated one makes
+        if o[k] != "/dev/null" and os.path.exists(o[k]):  # some file systems write it back at close)
+            os.remove(o[k])
     t0 = time.perf_counter()
     m0 = time.monotonic()
     p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Every golden e2e case through the ThreadSanitizer build of the host pipeline (tests/tsan_util.py):
 host packs at -w 4 and -w 16 on two engines (one for -d), then the raw stream (plain inputs, 4 KiB
-first window, 7-pair packs, three engines) with the text egress and with the records-only egress
-(FQ_RAW_EGRESS=host): outputs checked against the reference's, TSan reports counted.
+first window, 7-pair packs) with the engine's output text on three and four engines and with the
+records-only egress on one engine (FQ_RAW_EGRESS=host, byte ranges and copied): outputs checked
+against the reference's, TSan reports counted.
 python tools/tsan_sweep.py > profiles/r05_tsan_sweep.txt   (SWEEP=raw: the raw-stream part only)"""
 import os
 import sys
@@ -25,16 +26,20 @@ for case in E.ok_cases() if os.environ.get("SWEEP", "all") != "raw" else []:
             print(f"{case:30s} -w {w:2d}  outputs = reference  TSan reports {n}  ({time.time() - t0:.1f}s)", flush=True)
             if n:
                 print(err[-8000:], flush=True)
+# raw stream: the engine's output text on three and four engines; records-only egress (one engine)
+# as byte ranges of the windows (zc) and copied
 for case in E.ok_cases():
-    for egress in ("text", "host"):
+    for egress, devices in (("text", 3), ("text", 4), ("zc", 1), ("copy", 1)):
         env = {"FQ_RAW_WINDOW0": "4096"}
-        if egress == "host":
-            env["FQ_RAW_EGRESS"] = "host"
+        if egress != "text":
+            env.update(FQ_RAW_EGRESS="host", FQ_RAW_ZC="1" if egress == "zc" else "0")
         with tempfile.TemporaryDirectory() as d:
             t0 = time.time()
-            err, n = T.run_case(case, d, 4, devices=3, mode="raw", env_extra=env, pack_pairs=7)
+            err, n = T.run_case(case, d, 4, devices=devices, mode="raw", env_extra=env, pack_pairs=7)
             total += n
-            path = "raw stream on 3 engines" if "raw stream on 3 engines" in err else "raw stream, 1 engine" if "raw stream" in err else "host packs (options)"
+            path = (f"raw stream on {devices} engines" if f"raw stream on {devices} engines" in err else
+                    "raw, records-only" if "records-only egress" in err else
+                    "raw stream, 1 engine" if "raw stream" in err else "host packs (options)")
             print(f"{case:30s} raw egress {egress:4s} ({path:24s})  outputs = reference  TSan reports {n}  ({time.time() - t0:.1f}s)", flush=True)
             if n:
                 print(err[-8000:], flush=True)
