@@ -68,6 +68,10 @@ struct Slot {
     int* d_err = nullptr;  // this pack's device error word (cleared at submit, set by its kernels)
     int* h_err = nullptr;  // pinned: d_err as of this pack's kernels
     bool busy = false;      // events recorded and not yet waited for
+    // raw packs: the output text is copied back once its size is known (issue_copies)
+    bool copy_pending = false;
+    char* copy_dst[2] = {nullptr, nullptr};
+    size_t copy_cap[2] = {0, 0};
 };
 
 // A submitted pack, in submission order, until fq_engine_poll reports it.
@@ -387,10 +391,52 @@ static int check_err(fq_engine* e) {
     return FQ_OK;
 }
 
+// Raw packs' copies back, exactly sized: a pack's kernels end by copying its output sizes to the
+// host (on the compute stream, event ev_kern); once they are in, its text + adapter entries are
+// copied back on the out stream (in submission order; the link chain orders the copies of engines
+// sharing a GPU).  Copying the capacity bound instead carried the gap left by trimmed and dropped
+// records and, with -m, mate 1's whole input-sized bound for its few entry bytes (the e2e C4 leg's
+// copies back took 1.44x the C3 leg's).  upto = a slot: waits for the sizes of the packs up to
+// and including that slot's; -1: issues what is ready, stopping at the first pack whose sizes are
+// not in; -2: waits for all.
+static int issue_copies(fq_engine* e, int upto) {
+    for (Pending& q : e->pending) {
+        if (q.done) continue;
+        Slot& s = e->slots[q.slot];
+        if (s.copy_pending) {
+            if (upto == -1) {
+                const hipError_t st = hipEventQuery(s.ev_kern);
+                if (st == hipErrorNotReady) break;
+                if (st != hipSuccess) return hip_fail(e, st, "hipEventQuery");
+            } else {
+                HIP_TRY(e, hipEventSynchronize(s.ev_kern));
+            }
+            s.copy_pending = false;
+            LinkChain& lc = link_chain(e->device);
+            std::lock_guard<std::mutex> g(lc.m);
+            if (lc.out && lc.out_owner != e) HIP_TRY(e, hipStreamWaitEvent(e->s_out, lc.out, 0));
+            for (int m = 0; m < 2 && !prof_no_egress(); ++m) {
+                if (!s.copy_dst[m]) continue;
+                const unsigned long long ad = s.h_total[2 + m];  // (~0: the entries overflowed, reported at retire)
+                const size_t bytes = std::min<size_t>(s.copy_cap[m], (size_t)s.h_total[m] + (ad == ~0ull ? 0 : (size_t)ad));
+                if (bytes) HIP_TRY(e, hipMemcpyAsync(s.copy_dst[m], s.d_out[m], bytes, hipMemcpyDeviceToHost, e->s_out));
+            }
+            HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
+            lc.out = s.ev_done, lc.out_owner = e;
+        }
+        if (q.slot == upto) break;
+    }
+    return FQ_OK;
+}
+
 // Waits for slot k's pack (if any) and records its completion in the pending list.
 static int retire_slot(fq_engine* e, int k) {
     Slot& s = e->slots[k];
     if (!s.busy) return FQ_OK;
+    if (s.copy_pending) {
+        const int rc = issue_copies(e, k);
+        if (rc != FQ_OK) return rc;
+    }
     HIP_TRY(e, hipEventSynchronize(s.ev_done));
     s.busy = false;
     for (Pending& q : e->pending)
@@ -873,24 +919,20 @@ int fq_engine_raw_launch(fq_engine* e, fq_raw_result* r, fq_raw_out* out, uint64
                                               s.d_scan, s.scan_bytes, s.d_out[m], s.d_total + m, back[m], s.d_total + 2 + m,
                                               e->stream));
     }
+    // the output sizes (and the error word) behind the kernels; the text follows once they are in
+    HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipEventRecord(s.ev_kern, e->stream));
-    HIP_TRY(e, hipStreamWaitEvent(e->s_out, s.ev_kern, 0));
-    {
-        LinkChain& lc = link_chain(e->device);
-        std::lock_guard<std::mutex> g(lc.m);
-        if (lc.out && lc.out_owner != e) HIP_TRY(e, hipStreamWaitEvent(e->s_out, lc.out, 0));
-        HIP_TRY(e, hipMemcpyAsync(s.h_total, s.d_total, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->s_out));
-        for (int m = 0; m < mates && !prof_no_egress(); ++m)
-            HIP_TRY(e, hipMemcpyAsync(out->text.text[m], s.d_out[m], back[m], hipMemcpyDeviceToHost, e->s_out));
-        HIP_TRY(e, hipMemcpyAsync(s.h_err, s.d_err, sizeof(int), hipMemcpyDeviceToHost, e->s_out));
-        HIP_TRY(e, hipEventRecord(s.ev_done, e->s_out));
-        lc.out = s.ev_done, lc.out_owner = e;
+    for (int m = 0; m < 2; ++m) {
+        s.copy_dst[m] = m < mates ? out->text.text[m] : nullptr;
+        s.copy_cap[m] = m < mates ? back[m] : 0;
     }
+    s.copy_pending = true;
     s.busy = true;
     s.text_out = &out->text;
     s.raw_out = out;
     e->pending.push_back(Pending{seq_no, k, false, 0});
-    return FQ_OK;
+    return issue_copies(e, -1);
 }
 
 int fq_engine_raw_end(fq_engine* e) {
@@ -918,9 +960,12 @@ int fq_engine_poll(fq_engine* e, int wait, uint64_t* seq_no) {
     if (!e) return FQ_E_INVALID;
     if (e->pending.empty()) return 0;
     HIP_TRY(e, hipSetDevice(e->device));
+    int rc0 = issue_copies(e, -1);  // (raw packs whose sizes are in: their copies back start now)
+    if (rc0 != FQ_OK) return rc0;
     Pending& q = e->pending.front();
     if (!q.done) {
         Slot& s = e->slots[q.slot];
+        if (s.copy_pending && !wait) return 0;
         if (!wait) {
             const hipError_t st = hipEventQuery(s.ev_done);
             if (st == hipErrorNotReady) return 0;
@@ -1005,6 +1050,8 @@ int fq_engine_reset_acc(fq_engine* e) {
 int fq_engine_sync(fq_engine* e) {
     if (!e) return FQ_E_INVALID;
     HIP_TRY(e, hipSetDevice(e->device));
+    const int rc = issue_copies(e, -2);  // (the copies back of every raw pack launched)
+    if (rc != FQ_OK) return rc;
     HIP_TRY(e, hipDeviceSynchronize());
     return check_err(e);
 }

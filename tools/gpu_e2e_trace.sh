@@ -3,6 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
+export FQ_TIMING=1  # (the binary otherwise ends with _exit, before the profiler writes its files)
 D=$(mktemp -d /tmp/fqtrace_XXXX)
 timeout -k 10 300 python -c "
 import sys; sys.path.insert(0, 'tools'); sys.path.insert(0, '.')
