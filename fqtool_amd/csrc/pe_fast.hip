@@ -1364,8 +1364,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                     q30 += __popc(qm & 0x40404040u);  // q > '?' (= bit 6: q < 128 here; qm already masked)
                     lowf += __popc(~(qm + limq_v) & m80);        // q < limit
                     // whole-read quality total: only -e reads it (passFilter's mean quality),
-                    // which runs on the XTRA instantiation (and the merge variant)
-                    if (!LEAN && (XTRA || MERGE)) tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);
+                    // which runs on the XTRA instantiations (with -m the merge variant's)
+                    if (!LEAN && XTRA) tqf = __builtin_amdgcn_sad_u8(qm, 0u, tqf);
                     if (!LEAN) lr |= ~(qm + limr) & (0x80808080u & bm);         // q < cut_right threshold
 #if FQ_STG2
                     kkj[j] = kk;
@@ -2743,7 +2743,7 @@ hipError_t FQ_LAUNCH(const fq_params& p, const fq_batch& b, fq_read_result* res,
     // -c, UMI and -e (the whole-read quality total) run on the XTRA instantiations (lean is false then)
     const bool xtra = p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0 || p.avg_qual_limit > 0;
     const int pad = p.reserved[2] > 0 && p.reserved[2] <= 4096 ? p.reserved[2] : 0;  // profiling: extra LDS (LEAN)
-    if (p.merge_enabled && (p.correction_enabled || p.umi_front1 > 0 || p.umi_front2 > 0))  // -c / UMI with -m
+    if (p.merge_enabled && xtra)  // -c / UMI / -e with -m
         launch_variant<false, true, true, true>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, 0, stream);
     else if (p.merge_enabled)
         launch_variant<false, true, true, false>(p, b, res, acc, slow_tiles, slow_count, xfix, grid, 0, stream);

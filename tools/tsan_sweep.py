@@ -17,6 +17,7 @@ import tsan_util as T  # noqa: E402
 
 T.build()
 total = 0
+skip_rest = False
 for case in E.ok_cases() if os.environ.get("SWEEP", "all") != "raw" else []:
     for w in (4, 16):
         with tempfile.TemporaryDirectory() as d:
@@ -30,6 +31,9 @@ for case in E.ok_cases() if os.environ.get("SWEEP", "all") != "raw" else []:
 # as byte ranges of the windows (zc) and copied
 for case in E.ok_cases():
     for egress, devices in (("text", 3), ("text", 4), ("zc", 1), ("copy", 1)):
+        if egress != "text" or devices != 3:
+            if skip_rest:  # (options that keep the case off the raw stream: one run says so)
+                continue
         env = {"FQ_RAW_WINDOW0": "4096"}
         if egress != "text":
             env.update(FQ_RAW_EGRESS="host", FQ_RAW_ZC="1" if egress == "zc" else "0")
@@ -40,6 +44,7 @@ for case in E.ok_cases():
             path = (f"raw stream on {devices} engines" if f"raw stream on {devices} engines" in err else
                     "raw, records-only" if "records-only egress" in err else
                     "raw stream, 1 engine" if "raw stream" in err else "host packs (options)")
+            skip_rest = path == "host packs (options)"
             print(f"{case:30s} raw egress {egress:4s} ({path:24s})  outputs = reference  TSan reports {n}  ({time.time() - t0:.1f}s)", flush=True)
             if n:
                 print(err[-8000:], flush=True)
