@@ -150,6 +150,12 @@ namespace {
 #ifndef FQ_OV12
 #define FQ_OV12 0  // overlap candidates at the default limit 5 from the first 12 positions (not 16): slower (a false candidate in any lane costs the wave an exact check; profiles/r05_ab_ov12_stvcc.txt)
 #endif
+#ifndef FQ_FASTMASK
+#define FQ_FASTMASK 1  // posmask at the hot sites and staging's partial-chunk byte masks by v_med3 + 64-bit shifts (neutral to -0.5 %, profiles/r05_ab_fastmask_runshift.txt)
+#endif
+#ifndef FQ_OV_RUNSHIFT
+#define FQ_OV_RUNSHIFT 0  // overlap candidates: the fixed window's code masks by one 64-bit shift + two sign shifts (+2 %: rejected, profiles/r05_ab_fastmask_runshift.txt)
+#endif
 #ifndef FQ_ST_VCC
 #define FQ_ST_VCC 0  // removed-mode Stats: the rotation selects as VCC-masked v_cndmask_e32 (no gain measured, profiles/r05_ab_ov12_stvcc.txt)
 #endif
@@ -279,6 +285,37 @@ __device__ __forceinline__ uint32_t fold2(uint32_t x) { return (x | (x >> 1)) & 
 __device__ __forceinline__ uint32_t posmask(int n) {
     return n >= 16 ? 0x55555555u : n <= 0 ? 0u : (((1u << (2 * n)) - 1u) & 0x55555555u);
 }
+// the same at the hot sites of every variant: 2n clamped to [0, 32] by one v_med3, then the low
+// word of ~(~0 << 2n) by one full-rate 64-bit shift (the compare / select form costs two
+// half-rate shifts and two v_cndmask with their wait states)
+__device__ __forceinline__ uint32_t posmask_v(int n) {
+#if FQ_FASTMASK
+    int c;
+    asm("v_med3_i32 %0, %1, 0, 32" : "=v"(c) : "v"(n + n));
+    unsigned long long x;
+    asm("v_lshlrev_b64 %0, %1, -1" : "=v"(x) : "v"(c));
+    return ~(uint32_t)x & 0x55555555u;
+#else
+    return posmask(n);
+#endif
+}
+
+// byte masks of the first n4 / 4 bytes of a 16-byte chunk, dwords 0-3 (n4 = 4 x bytes, any value):
+// per 8-byte half ~((~0 << c) << c) with c = 4 x its bytes clamped to [0, 32]
+[[maybe_unused]] __device__ __forceinline__ void chunk_bytemask(int n4, uint32_t m[4]) {
+    int c0, c1;
+    asm("v_med3_i32 %0, %1, 0, 32" : "=v"(c0) : "v"(n4));
+    asm("v_med3_i32 %0, %1, 0, 32" : "=v"(c1) : "v"(n4 - 32));
+    unsigned long long a, b;
+    asm("v_lshlrev_b64 %0, %1, -1" : "=v"(a) : "v"(c0));
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(a) : "v"(c0), "v"(a));
+    asm("v_lshlrev_b64 %0, %1, -1" : "=v"(b) : "v"(c1));
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(b) : "v"(c1), "v"(b));
+    m[0] = ~(uint32_t)a;
+    m[1] = ~(uint32_t)(a >> 32);
+    m[2] = ~(uint32_t)b;
+    m[3] = ~(uint32_t)(b >> 32);
+}
 
 // byte mask of the first `n` bytes of a dword
 __device__ __forceinline__ uint32_t bytemask(int n) {
@@ -372,7 +409,7 @@ __device__ inline bool ov_exact(const uint32_t* col, int c1, int p1, int c2, int
     const uint32_t* A = col + (p1 >> 4) * 64 + c1;  // code word w of read 1's window: A[64 w]
     const uint32_t* B = col + (p2 >> 4) * 64 + c2;
     constexpr int kN = kFN * 64;                       // the N-mask field, kChunks words further
-    const uint32_t last = posmask(ol - 16 * (nw - 1));  // valid positions of the last word
+    const uint32_t last = posmask_v(ol - 16 * (nw - 1));  // valid positions of the last word
     if constexpr (X2) {
     // Each stream's words j and j + 1 come as one register pair (one ds_read2st64 each), realigned
     // by a full-rate 64-bit shift -- instead of a v_alignbit (half rate) on words carried over from
@@ -543,6 +580,12 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
     uint32_t L0, H0, L1, H1;
     planes(L0, H0);
     const uint32_t fu = unzip2(fixed);
+#if FQ_OV_RUNSHIFT
+    // fixed position j's code bits at bit 31 of each word of Y << j: low word fl_j (bit j of fu),
+    // high word fh_j (bit 16 + j); broadcast by an arithmetic shift each (full rate, vs two v_bfe)
+    const uint32_t fur = __builtin_bitreverse32(fu);
+    const unsigned long long Y0 = (unsigned long long)(fur << 16) << 32 | fur;
+#endif
     int nblk = 2;  // blocks holding some lane's offsets (wave-uniform)
 #pragma unroll
     for (int k = 2; k < kOvBlocks; ++k)
@@ -571,8 +614,15 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
             const uint32_t hs = j ? __builtin_amdgcn_alignbit(H1, H0, j) : H0;
             const uint32_t ls = j ? __builtin_amdgcn_alignbit(L1, L0, j) : L0;
 #endif
+#if FQ_OV_RUNSHIFT
+            unsigned long long Yj = Y0;
+            if (j) asm("v_lshlrev_b64 %0, %2, %1" : "=v"(Yj) : "v"(Y0), "i"(j));
+            const uint32_t fh = (uint32_t)((int)(uint32_t)(Yj >> 32) >> 31);
+            const uint32_t fl = (uint32_t)((int)(uint32_t)Yj >> 31);
+#else
             const uint32_t fh = (uint32_t)__builtin_amdgcn_sbfe((int)fu, 16 + j, 1);
             const uint32_t fl = (uint32_t)__builtin_amdgcn_sbfe((int)fu, j, 1);
+#endif
             return (hs ^ fh) | (ls ^ fl);
         };
         uint32_t lt;
@@ -751,11 +801,11 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, in
         // scan breaks at the second non-G base; the loop below runs only for the reads it leaves open
         // (a polyG tail, or per < 8).
         if (maxMM >= 1) {
-            const uint32_t valid = posmask(n), x = xg & valid, x2 = x & (x - 1u);
+            const uint32_t valid = posmask_v(n), x = xg & valid, x2 = x & (x - 1u);
             const int s2 = (__ffs(x2) - 1) >> 1;
             if (x2 && (maxMM == 1 || s2 + 1 < 2 * per)) {
                 iend = s2;
-                const uint32_t gm = ~x & valid & posmask(s2);  // G bases before the break
+                const uint32_t gm = ~x & valid & posmask_v(s2);  // G bases before the break
                 if (gm) lastG = (31 - __clz(gm)) >> 1;
             }
         }
@@ -765,12 +815,12 @@ __device__ inline int polyg_bits(const uint32_t* col, int c, bool rc, int st, in
         // A polyG tail (the reads the shortcut above leaves open): its all-G groups change nothing
         // but firstGpos, so they are passed over at ~16 VALU a group (the loop below spends ~45)
         if (iend == n) {
-            while (16 * (g + 1) < n && (xg & posmask(n - 16 * g)) == 0u) xg = nong(++g);
+            while (16 * (g + 1) < n && (xg & posmask_v(n - 16 * g)) == 0u) xg = nong(++g);
             if (g > 0) lastG = 16 * g - 1;  // (scan indices below 16 g are all G)
         }
 #endif
         for (; 16 * g < n && iend == n; ++g) {
-            const uint32_t valid = posmask(n - 16 * g);
+            const uint32_t valid = posmask_v(n - 16 * g);
 #if FQ_PG3
             uint32_t x = xg & valid;
             // the next group's column words are requested before this group is decided (a G tail
@@ -1337,14 +1387,17 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 // send the tile to the general kernel, so q + c (c < 128) never carries into the
                 // next byte for the bytes that count.  FULL: every byte is inside the read (the
                 // common case, no byte masks).
+                uint32_t pbm[4], pbms[4];  // (FQ_FASTMASK: a partial chunk's byte masks, made once)
+                // (not in the full non-merge variants: the eight live masks spill there)
+                constexpr bool kChunkMask = FQ_FASTMASK && (LEAN || MERGE);
                 auto dword = [&](int j, auto full_c) {
                     constexpr bool FULL = decltype(full_c)::value;
                     if (LY::kQLds) qrow[4 * k + j] = qw[j];
-                    const uint32_t bm = FULL ? 0xFFFFFFFFu : bytemask(Lk - 4 * j);
+                    const uint32_t bm = FULL ? 0xFFFFFFFFu : kChunkMask ? pbm[j] : bytemask(Lk - 4 * j);
                     // read 2 (the column holds its reverse complement): the chunk's bytes reversed
                     // (dword 3 - j byte-swapped, one v_perm), so its codes come out in column order
                     const uint32_t sr = PAIRED ? __builtin_amdgcn_perm(sw[3 - j], sw[j], rsel) : sw[j];
-                    const uint32_t bms = FULL ? 0xFFFFFFFFu : rc ? ~bytemask(16 - Lk - 4 * j) : bm;
+                    const uint32_t bms = FULL ? 0xFFFFFFFFu : kChunkMask ? pbms[j] : rc ? ~bytemask(16 - Lk - 4 * j) : bm;
                     const uint32_t kk = (sr >> 1) & 0x07070707u;
                     // canonical byte for the 3-bit key: A C T G (0-3), N (7)
                     const uint32_t canon = __builtin_amdgcn_perm(0x4E000000u, 0x47544341u, kk);
@@ -1378,6 +1431,20 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 #pragma unroll
                     for (int j = 0; j < 4; ++j) dword(j, std::true_type{});
                 } else {
+                    if constexpr (kChunkMask) {
+                    // the first Lk bytes; read 2's staged bytes are the last Lk (its chunk reversed)
+                    const int n4 = 4 * Lk;
+                    chunk_bytemask(n4, pbm);
+                    if (PAIRED) {
+                        uint32_t rm[4];
+                        chunk_bytemask(64 - n4, rm);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) pbms[j] = rc ? ~rm[j] : pbm[j];
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) pbms[j] = pbm[j];
+                    }
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) dword(j, std::false_type{});
                 }
@@ -1397,7 +1464,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 if (!LEAN) lowr = shift_in_sign(lowr, lr | (0u - lr));  // (sign set iff lr != 0)
                 // N flags are kept only for positions inside the read (later passes rely on it);
                 // read 2's chunk is reversed: its positions inside the read are the high ones
-                const uint32_t vmask = full ? 0x55555555u : rc ? 0x55555555u & ~posmask(16 - Lk) : posmask(Lk);
+                const uint32_t vmask = full ? 0x55555555u : rc ? 0x55555555u & ~posmask_v(16 - Lk) : posmask_v(Lk);
                 uint32_t fck = tr4x4(cc);
                 const uint32_t fwk = tr4x4(nn4) & vmask;
                 nbf += __popc(fwk);
@@ -1623,7 +1690,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             const int olA = mate ? n2 : n1, olB = mate ? n1 : n2;
             const uint32_t fixed = field_window(col, kFC, mate ? c1 : c2, mate ? st1 : off2);
             const int cnt = max(0, olA - req);
-            const uint32_t pm = posmask(olB);
+            const uint32_t pm = posmask_v(olB);
             OvOut mine{false, 0, 0, 0};
             if (abl & 512) atomicAdd(&g_phase_cycles[1], 1ull);  // profiling: scanning lanes
             // bit-plane candidates when every lane compares full 16-position windows
