@@ -90,8 +90,31 @@ namespace {
 #ifndef FQ_SCAL_PAD
 #define FQ_SCAL_PAD 1  // per-read scalar copies 17 u64 apart: one LDS bank pair per copy (0: 16, profiling)
 #endif
+#ifndef FQ_STATS_PRIO
+#define FQ_STATS_PRIO 3  // s_setprio during the Stats passes (see FQ_PRIO_TRIM)
+#endif
+#ifndef FQ_STATS_PRIO_ALL
+#define FQ_STATS_PRIO_ALL 1  // (with FQ_STATS_PRIO) the merged part's Stats too
+#endif
+#ifndef FQ_PRIO_TRIM
+#define FQ_PRIO_TRIM 1  // s_setprio after staging (trimAndCut)
+// Issue priority rising with a wave's progress through its tile: staging 0, trimAndCut and polyG 1,
+// overlap to passFilter 2, Stats 3 -- the waves nearest the end of their tile issue first, so the
+// 16 waves of a CU spread over the phases and the memory / LDS work of the late phases (the Stats
+// pass's quality re-reads and atomics) overlaps the VALU of the early ones.  C3 -10 %, C4 -13 %,
+// C5 -10 %, C2 -3 % against staging-only priority (profiles/r05_ab_prio_*.txt).
+#endif
+#ifndef FQ_PRIO_POLYG
+#define FQ_PRIO_POLYG 1  // s_setprio from polyG on
+#endif
+#ifndef FQ_PRIO_OV
+#define FQ_PRIO_OV 2  // from the overlap analysis on
+#endif
+#ifndef FQ_PRIO_FILTER
+#define FQ_PRIO_FILTER 2  // from passFilter on
+#endif
 #ifndef FQ_STAGE_PRIO
-#define FQ_STAGE_PRIO 1  // s_setprio during staging: the loads of staging waves go out first (-2 %)
+#define FQ_STAGE_PRIO 0  // s_setprio during staging (round 4: 1, -2 % against none; with the later phases above it, 0)
 #endif
 #ifndef FQ_DESYNC
 #define FQ_DESYNC 0  // profiling: initial s_sleep stagger of co-resident waves
@@ -1306,7 +1329,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 
         // ---------------- staging ----------------
 #if FQ_STAGE_PRIO
-        __builtin_amdgcn_s_setprio(FQ_STAGE_PRIO);  // profiling: staging waves issue first
+        __builtin_amdgcn_s_setprio(FQ_STAGE_PRIO);
 #endif
         // chunk-interleaved batch tiles (include/fqengine.h): chunk k of this lane's row is 512 B
         // after chunk k-1, so each chunk load of the wave is one (PE: two planes x 32 rows) or
@@ -1568,8 +1591,8 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#if FQ_STAGE_PRIO
-        __builtin_amdgcn_s_setprio(0);
+#if FQ_STAGE_PRIO || FQ_PRIO_TRIM
+        __builtin_amdgcn_s_setprio(FQ_PRIO_TRIM);  // (the phases after staging, up to polyG)
 #endif
 #if FQ_PREFETCH
         // The wave's next tile is one contiguous run of R * stride bytes per plane (R = 32 pairs or
@@ -1646,6 +1669,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 
         FQ_STAMP(1)
         // ---------------- polyG (src/peprocessor.cpp:295-299) ----------------
+#if FQ_PRIO_POLYG || FQ_PRIO_OV || FQ_PRIO_FILTER
+        __builtin_amdgcn_s_setprio(FQ_PRIO_POLYG);  // (issue priority by phase: FQ_PRIO_TRIM)
+#endif
         if (both && p.polyg_enabled && !(abl & 8)) {
             int bases;
             n = polyg_bits(col, lane, rc, st, n, p.polyg_max_mismatch, g_inv, g_per, p.polyg_compare_req, bases);
@@ -1737,6 +1763,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             return ov;
         };
         // ---------------- overlap + adapters (src/peprocessor.cpp:302-333) ----------------
+#if FQ_PRIO_POLYG || FQ_PRIO_OV || FQ_PRIO_FILTER
+        __builtin_amdgcn_s_setprio(FQ_PRIO_OV);
+#endif
         Overlap ov1{0, 0, 0, 0};  // (merge) the first analysis and the windows it saw
         int n1a = -1, n2a = -1;
         bool ad_ov = false, corr = false;  // (corr: -c changed a base of the pair)
@@ -1835,6 +1864,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
 
         FQ_STAMP(4)
         // ---------------- passFilter (src/filter.cpp:3-52) ----------------
+#if FQ_PRIO_POLYG || FQ_PRIO_OV || FQ_PRIO_FILTER
+        __builtin_amdgcn_s_setprio(FQ_PRIO_FILTER);
+#endif
         int code = FQ_FAIL_LENGTH;
         uint32_t w20 = 0, w30 = 0;  // Q20/Q30 of the window, for the post stats
         int low = 0, tq = 0, nb = 0;
@@ -2114,6 +2146,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 sadd(&sc[9], ((unsigned long long)w20 << 32) | w30);
             }
         }
+#if FQ_STATS_PRIO
+        __builtin_amdgcn_s_setprio(FQ_STATS_PRIO);  // (the Stats pass: highest, FQ_PRIO_TRIM)
+#endif
         if (valid && !(abl & 4) && removed_mode) {
             // Every kept window is a prefix [0, wlen): each base goes to exactly one cell, kept or
             // removed (pre = kept + removed at the flush), one LDS atomic per base.  Per chunk the
@@ -2349,6 +2384,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
                 }
             }
         }
+#if FQ_STATS_PRIO && !FQ_STATS_PRIO_ALL
+        __builtin_amdgcn_s_setprio(0);
+#endif
         // read 2's merged-part start, known to both lanes of the pair (all lanes swap)
         const int ws2 = MERGE ? (mate ? ws : xor32(ws)) : 0;
         if (MERGE && removed_mode && valid && !(abl & 4) && merged && post_on) {
@@ -2554,6 +2592,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             }
             }
         }
+#if FQ_STATS_PRIO && FQ_STATS_PRIO_ALL
+        __builtin_amdgcn_s_setprio(0);
+#endif
         if (valid && !(abl & 4) && !removed_mode) {
             const int wlen = post_on ? wn : 0;  // post window [ws, ws + wlen)
             // merged pairs: both parts go to read 1's post block, read 2's part reversed and
