@@ -94,7 +94,7 @@ namespace {
 #define FQ_STATS_PRIO 3  // s_setprio during the Stats passes (see FQ_PRIO_TRIM)
 #endif
 #ifndef FQ_STATS_PRIO_ALL
-#define FQ_STATS_PRIO_ALL 1  // (with FQ_STATS_PRIO) the merged part's Stats too
+#define FQ_STATS_PRIO_ALL 2  // (with FQ_STATS_PRIO) 1: up to the end of the merged part's Stats; 2: on to the end of the tile (C3 -1 %)
 #endif
 #ifndef FQ_PRIO_TRIM
 #define FQ_PRIO_TRIM 1  // s_setprio after staging (trimAndCut)
@@ -1328,7 +1328,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
         int L = valid ? (int)(mate ? b.len2[idx] : b.len1[idx]) : 0;
 
         // ---------------- staging ----------------
-#if FQ_STAGE_PRIO
+#if FQ_STAGE_PRIO || FQ_STATS_PRIO_ALL == 2
         __builtin_amdgcn_s_setprio(FQ_STAGE_PRIO);
 #endif
         // chunk-interleaved batch tiles (include/fqengine.h): chunk k of this lane's row is 512 B
@@ -2592,7 +2592,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             }
             }
         }
-#if FQ_STATS_PRIO && FQ_STATS_PRIO_ALL
+#if FQ_STATS_PRIO && FQ_STATS_PRIO_ALL == 1
         __builtin_amdgcn_s_setprio(0);
 #endif
         if (valid && !(abl & 4) && !removed_mode) {
