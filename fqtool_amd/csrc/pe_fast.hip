@@ -167,6 +167,9 @@ namespace {
 #ifndef FQ_MRG2
 #define FQ_MRG2 1  // merged-part Stats: groups unrolled (immediate row offsets), qualities through a tile buffer
 #endif
+#ifndef FQ_ADSEQ_LDSBITS
+#define FQ_ADSEQ_LDSBITS 0  // adseq_search's candidate scan: the adapter's bit words from LDS (FixedLds) instead of v_bfe
+#endif
 #ifndef FQ_OV_SH64
 #define FQ_OV_SH64 1  // overlap candidates: planes realigned by 64-bit shifts (one block per pass)
 #endif
@@ -175,9 +178,6 @@ namespace {
 #endif
 #ifndef FQ_FASTMASK
 #define FQ_FASTMASK 1  // posmask at the hot sites and staging's partial-chunk byte masks by v_med3 + 64-bit shifts (neutral to -0.5 %, profiles/r05_ab_fastmask_runshift.txt)
-#endif
-#ifndef FQ_OV_RUNSHIFT
-#define FQ_OV_RUNSHIFT 0  // overlap candidates: the fixed window's code masks by one 64-bit shift + two sign shifts (+2 %: rejected, profiles/r05_ab_fastmask_runshift.txt)
 #endif
 #ifndef FQ_ST_VCC
 #define FQ_ST_VCC 0  // removed-mode Stats: the rotation selects as VCC-masked v_cndmask_e32 (no gain measured, profiles/r05_ab_ov12_stvcc.txt)
@@ -224,7 +224,15 @@ constexpr int kSmallW = 2 * ((kSmallU64 + 1) & ~1);
 constexpr int kInsW = (512 + 1 + 1) & ~1;                 // insert-size histogram, u32 per workgroup
 // per-read scalars are spread over kScalCopies LDS copies (lane % copies), each
 // [4 stats][reads, length_sum, q20, q30] u64; the merge variant keeps 8 (LDS budget)
-constexpr int kAdW = 2 * FQ_MAX_ADAPTER / 4 + 16;  // adapter bytes of both mates + adseq_search's window words
+// adseq_search's adapter columns (per mate: 2-bit codes; read 2's reversed and complemented)
+constexpr int kAdCW = 10;    // words of an adapter column (positions < FQ_MAX_ADAPTER, + one look-ahead)
+constexpr int kAdRc = 144;   // read 2's adapter column: index y holds position kAdRc - 1 - y
+static_assert(kAdRc >= FQ_MAX_ADAPTER + 15 && kAdRc + 16 <= 16 * kAdCW && FQ_MAX_ADAPTER + 16 <= 16 * kAdCW, "adapter column");
+// adapter bytes of both mates, adseq_search's window words [2][8], adapter columns [2][kAdCW] and the
+// (fh, fl) words of each mate's first window [2][16][2]
+constexpr int kAdWinOff = 2 * FQ_MAX_ADAPTER / 4, kAdColOff = kAdWinOff + 16, kAdBitOff = kAdColOff + 2 * kAdCW;
+constexpr int kAdW = kAdBitOff + 2 * 16 * 2;
+static_assert(kAdBitOff % 2 == 0, "(fh, fl) pairs 8-byte aligned");
 constexpr int kScalStride = FQ_SCAL_PAD ? 17 : 16;  // u64 per scalar copy (17: copies on distinct LDS bank pairs)
 constexpr int kPfW = FQ_PREFETCH ? 64 : 0;             // LDS-DMA prefetch sink (never read)
 // Every variant re-reads qualities from the rows in L2 (no LDS quality rows) and runs 16 waves
@@ -582,7 +590,31 @@ __device__ __forceinline__ void csa(uint32_t& hi, uint32_t& lo, uint32_t a, uint
 // bit planes H and L over positions; for compared position j the mismatch vector over the 32
 // offsets of a block is ((H >> j) ^ FH_j) | ((L >> j) ^ FL_j) (FH_j, FL_j = the bits of fixed[j]
 // spread over a word), and the 16 vectors are summed per offset with carry-save adders.
-__device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint32_t fixed, int K, int cnt,
+// Compared position j's fixed code bits, each as a word of 0s or 1s (fh: high bit, fl: low bit):
+//  * FixedOwn: from the lane's own fixed word (the overlap: a window of the other mate), two v_bfe;
+//  * FixedLds: precomputed in LDS (trimBySequence: the adapter's first 16 codes, the same for every
+//    lane of a mate), one broadcast ds_read_b64 and no VALU.
+struct FixedOwn {
+    uint32_t fu;  // unzip2(fixed)
+    __device__ __forceinline__ void next_block() {}
+    __device__ __forceinline__ void bits(int j, uint32_t& fh, uint32_t& fl) const {
+        fh = (uint32_t)__builtin_amdgcn_sbfe((int)fu, 16 + j, 1);
+        fl = (uint32_t)__builtin_amdgcn_sbfe((int)fu, j, 1);
+    }
+};
+struct FixedLds {
+    uint32_t f;  // LDS byte address of [j] = (fh, fl)
+    // (opaque per block: hoisted out of the block loop, the 32 words would stay live and spill)
+    __device__ __forceinline__ void next_block() { asm volatile("" : "+v"(f)); }
+    __device__ __forceinline__ void bits(int j, uint32_t& fh, uint32_t& fl) const {
+        typedef __attribute__((address_space(3))) const uint32_t LdsW;
+        const LdsW* w = reinterpret_cast<const LdsW*>((size_t)f);
+        fh = w[2 * j];
+        fl = w[2 * j + 1];
+    }
+};
+template <class FX>
+__device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, FX fx, int K, int cnt,
                                      uint32_t cand[kOvBlocks]) {
     // planes of the 32 positions from mpos + 32 * i (i = block): low-bit plane, high-bit plane,
     // from a stream of the column's code words (two new LDS words per block).  Unclamped: mpos >= 0,
@@ -602,13 +634,6 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
     };
     uint32_t L0, H0, L1, H1;
     planes(L0, H0);
-    const uint32_t fu = unzip2(fixed);
-#if FQ_OV_RUNSHIFT
-    // fixed position j's code bits at bit 31 of each word of Y << j: low word fl_j (bit j of fu),
-    // high word fh_j (bit 16 + j); broadcast by an arithmetic shift each (full rate, vs two v_bfe)
-    const uint32_t fur = __builtin_bitreverse32(fu);
-    const unsigned long long Y0 = (unsigned long long)(fur << 16) << 32 | fur;
-#endif
     int nblk = 2;  // blocks holding some lane's offsets (wave-uniform)
 #pragma unroll
     for (int k = 2; k < kOvBlocks; ++k)
@@ -618,6 +643,7 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
         if (bk >= nblk) cand[bk] = 0u;
 #pragma unroll 1
     for (int bk = 0; bk < nblk; ++bk) {
+        fx.next_block();
         if (bk < kOvBlocks - 1) planes(L1, H1);
         else L1 = H1 = 0u;
         // mismatch vector of compared position j over the block's 32 offsets
@@ -637,15 +663,8 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
             const uint32_t hs = j ? __builtin_amdgcn_alignbit(H1, H0, j) : H0;
             const uint32_t ls = j ? __builtin_amdgcn_alignbit(L1, L0, j) : L0;
 #endif
-#if FQ_OV_RUNSHIFT
-            unsigned long long Yj = Y0;
-            if (j) asm("v_lshlrev_b64 %0, %2, %1" : "=v"(Yj) : "v"(Y0), "i"(j));
-            const uint32_t fh = (uint32_t)((int)(uint32_t)(Yj >> 32) >> 31);
-            const uint32_t fl = (uint32_t)((int)(uint32_t)Yj >> 31);
-#else
-            const uint32_t fh = (uint32_t)__builtin_amdgcn_sbfe((int)fu, 16 + j, 1);
-            const uint32_t fl = (uint32_t)__builtin_amdgcn_sbfe((int)fu, j, 1);
-#endif
+            uint32_t fh, fl;
+            fx.bits(j, fh, fl);
             return (hs ^ fh) | (ls ^ fl);
         };
         uint32_t lt;
@@ -717,44 +736,68 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, uint
 // whose window holds at most min(n - pos, alen) / 8 byte mismatches against the adapter.  The
 // reference tests every pos byte by byte; here a code-level lower bound over the first (up to) 16
 // compared positions rejects almost every pos without touching bytes, and only survivors get the
-// reference's exact byte test, in pos order.  The bound counts code mismatches only (an N or a
-// lowercase base shares its code with some upper-case letter), so it never exceeds the byte
-// count: a pos it rejects has more mismatches than allowed.  Valid for adapters of >= 20 upper-case
-// ACGT bytes (start = -4, and the windows of every negative pos lie inside the adapter's first 20
-// positions); the kernel start sets adw[5] and the window words (see pe_fast_kernel).
+// reference's test, in pos order.  The bound counts code mismatches only (an N or a lowercase base
+// shares its code with some upper-case letter), so it never exceeds the byte count: a pos it
+// rejects has more mismatches than allowed.  Valid for adapters of >= 20 upper-case ACGT bytes
+// (start = -4, and the windows of every negative pos lie inside the adapter's first 20 positions);
+// the kernel start sets adw[5], the window words, the adapter column and its bit words (see
+// pe_fast_kernel).
 //  * pos in [0, n - 16]: full 16-position windows, all at once (ov_candidates; bound < alen/8 + 1,
-//    a superset of every pos's own allowance);
+//    a superset of every pos's own allowance).  The adapter's bits per compared position are the
+//    same for every lane of a mate, so they come from LDS (FixedLds) instead of two v_bfe a position;
 //  * pos in -4..-1 and [n - 15, n - 5]: one masked window each against that pos's allowance.
+// The survivors' test is the reference's byte comparison restated on the columns, 16 positions a
+// step: with an upper-case ACGT adapter a read byte differs from the adapter byte iff its code
+// differs or it is not an upper-case A C G T (an N, a lowercase or an exotic byte: the N word's
+// flags), so the mismatch count is one popcount per 16 positions (no per-byte loop whose length
+// one lane's candidate imposes on its wave).
 // Read 2's column is the reverse complement (forward position j of the read window at column
 // kMaxLen - 1 - st - j), so its windows run down the column and its adapter words are stored
 // reversed and complemented; `fixed` word k = codes of adapter positions k .. k + 15.
-template <class SQ>
-__device__ inline bool adseq_search(const uint32_t* col, int c, bool rc, int st, int n, const uint32_t* adw, SQ r,
-                                    const uint8_t* ad, int alen, int& pos_out) {
-    auto exact = [&](int pos) -> bool {  // the reference's inner loop at one pos
+__device__ inline bool adseq_search(const uint32_t* col, int c, bool rc, int st, int n, const uint32_t* adw,
+                                    const uint32_t* adc, uint32_t adf, int alen, int& pos_out) {
+    // The reference's inner loop at pos (src/adaptertrimmer.cpp:59-71) on the columns, 16 positions a
+    // step: with an upper-case ACGT adapter a read byte differs from the adapter's iff its code
+    // differs or it is not an upper-case A C G T (an N, a lowercase or an exotic byte: the N word's
+    // flags).  (Read windows by field_window_masked: only in-read positions are compared; adapter
+    // windows from the mate's adapter column.)
+    auto exact = [&](int pos) -> bool {
         const int cmplen = min(n - pos, alen), allowed = cmplen / 8;
         int mm = 0;
-        for (int i = max(0, -pos); i < cmplen; ++i)
-            if (ad[i] != r(i + pos) && ++mm > allowed) return false;
-        return true;
+#pragma unroll 1
+        for (int i = max(0, -pos); i < cmplen; i += 16) {
+            const int m = min(16, cmplen - i), q = pos + i;
+            const int sc = rc ? kMaxLen - 16 - st - q : st + q;
+            const uint32_t rw = field_window_masked(col, kFC, c, sc), rn = field_window_masked(col, kFN, c, sc);
+            const int x = rc ? kAdRc - 16 - i : i;
+            const uint32_t* aq = adc + (x >> 4);
+            const uint32_t aw = __builtin_amdgcn_alignbit(aq[1], aq[0], 2 * (x & 15));
+            const uint32_t mask = rc ? 0x55555555u & ~posmask(16 - m) : posmask(m);
+            mm += __popc((fold2(rw ^ aw) | rn | (rn >> 1)) & mask);
+        }
+        return mm <= allowed;
     };
-    // the 16-position window of forward read positions [j0, j0 + 16) against adapter word k, the
-    // first m read positions compared
-    auto bound = [&](int j0, int k, int m) -> int {
-        const int s = rc ? kMaxLen - 16 - st - j0 : st + j0;
-        const uint32_t mask = rc ? 0x55555555u & ~posmask(16 - m) : posmask(m);
-        return __popc(fold2(field_window(col, kFC, c, s) ^ adw[k]) & mask);
-    };
-    for (int pos = -4; pos < 0; ++pos) {
-        if (pos >= n - 4) return false;
-        if (bound(0, -pos, min(n, 16)) <= min(n - pos, alen) / 8 && exact(pos)) {
-            pos_out = pos;
-            return true;
+    // pos -4 .. -1: the read's first 16 positions (one window) against adapter words 4 .. 1, the
+    // first min(n, 16) read positions compared
+    {
+        const uint32_t r0 = field_window(col, kFC, c, rc ? kMaxLen - 16 - st : st);
+        const int m0 = min(n, 16);
+        const uint32_t mask = rc ? 0x55555555u & ~posmask(16 - m0) : posmask(m0);
+        for (int pos = -4; pos < 0; ++pos) {
+            if (pos >= n - 4) return false;
+            if (__popc(fold2(r0 ^ adw[-pos]) & mask) <= min(n - pos, alen) / 8 && exact(pos)) {
+                pos_out = pos;
+                return true;
+            }
         }
     }
     if (n >= 16) {
         uint32_t cand[kOvBlocks];
-        ov_candidates(col, c, rc ? kMaxLen - st - n : st, adw[0], alen / 8 + 1, n - 15, cand);
+#if FQ_ADSEQ_LDSBITS
+        ov_candidates(col, c, rc ? kMaxLen - st - n : st, FixedLds{adf}, alen / 8 + 1, n - 15, cand);
+#else
+        ov_candidates(col, c, rc ? kMaxLen - st - n : st, FixedOwn{unzip2(adw[0])}, alen / 8 + 1, n - 15, cand);
+#endif
         for (;;) {  // candidates in pos order: read 1 from the lowest offset, read 2 from the highest
             int k = -1;
             if (!rc) {
@@ -775,11 +818,21 @@ __device__ inline bool adseq_search(const uint32_t* col, int c, bool rc, int st,
             }
         }
     }
-    for (int pos = max(0, n - 15); pos < n - 4; ++pos) {
-        const int m = n - pos;  // < 16 <= alen: every compared position is in the window
-        if (bound(pos, 0, m) <= m / 8 && exact(pos)) {
-            pos_out = pos;
-            return true;
+    // pos n - 15 .. n - 5: m = n - pos < 16 <= alen positions, all inside the read's last 16, against
+    // the adapter's first m -- decided exactly from one window of the read's codes and flags (read 1:
+    // its last m fields shifted down to the adapter's first m; read 2, whose window runs backwards:
+    // the adapter word, reversed, shifted down instead)
+    {
+        const int se = rc ? kMaxLen - st - n : st + n - 16;
+        const uint32_t rw = field_window(col, kFC, c, se), rn = field_window(col, kFN, c, se);
+        const uint32_t aw = adw[0];
+        for (int pos = max(0, n - 15); pos < n - 4; ++pos) {
+            const int m = n - pos, sh = 2 * (16 - m);
+            const uint32_t a = rc ? rw : rw >> sh, f = rc ? rn : rn >> sh, b = rc ? aw >> sh : aw;
+            if (__popc((fold2(a ^ b) | f | (f >> 1)) & posmask(m)) <= m / 8) {
+                pos_out = pos;
+                return true;
+            }
         }
     }
     return false;
@@ -1251,6 +1304,28 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             }
         }
         adw[8 * m + k] = w;
+    } else if (threadIdx.x < 12 + 2 * kAdCW) {
+        // adapter columns: mate 0 word w = codes of positions 16 w .. 16 w + 15; mate 1 index y = the
+        // complemented code of position kAdRc - 1 - y (positions past the buffer: code 0, never compared)
+        const int m = (threadIdx.x - 12) / kAdCW, w = (threadIdx.x - 12) % kAdCW;
+        const uint8_t* a = m ? p.adapter2 : p.adapter1;
+        uint32_t v = 0;
+        for (int f = 0; f < 16; ++f) {
+            const int y = 16 * w + f, q = m ? kAdRc - 1 - y : y;
+            if (q >= 0 && q < FQ_MAX_ADAPTER) v |= (uint32_t)(((a[q] >> 1) & 3) ^ (m ? 2 : 0)) << (2 * f);
+        }
+        adw[kAdColOff - kAdWinOff + m * kAdCW + w] = v;
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + 2 * 16) {
+        // (fh, fl) of compared position j of each mate's first window (adw[8 m], as ov_candidates'
+        // FixedOwn would derive them)
+        const int m = (threadIdx.x - 64) >> 4, j = (threadIdx.x - 64) & 15;
+        const uint8_t* a = m ? p.adapter2 : p.adapter1;
+        uint32_t w = 0;
+        for (int f = 0; f < 16; ++f) w |= (uint32_t)((a[f] >> 1) & 3) << (2 * f);
+        if (m) w = pairrev(w) ^ 0xAAAAAAAAu;
+        const uint32_t fu = unzip2(w);
+        adw[kAdBitOff - kAdWinOff + 2 * (16 * m + j)] = 0u - ((fu >> (16 + j)) & 1u);
+        adw[kAdBitOff - kAdWinOff + 2 * (16 * m + j) + 1] = 0u - ((fu >> j) & 1u);
     }
     __syncthreads();
 
@@ -1684,7 +1759,9 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
         auto by_sequence = [&]() {
             int pos;
             const uint32_t* my_adw = adw + 8 * mate;
-            if (my_adw[5] ? adseq_search(col, lane, rc, st, n, my_adw, at(seq, st), my_ad, my_alen, pos)
+            if (my_adw[5] ? adseq_search(col, lane, rc, st, n, my_adw, adw + (kAdColOff - kAdWinOff) + kAdCW * mate,
+                                         (uint32_t)(size_t)(const __attribute__((address_space(3))) uint32_t*)(adw + (kAdBitOff - kAdWinOff) + 32 * mate),
+                                         my_alen, pos)
                           : trim_by_sequence_t(at(seq, st), n, my_ad, my_alen, pos)) {
                 int ad_len;
                 if (pos < 0) {
@@ -1723,7 +1800,7 @@ __global__ void __launch_bounds__((Layout<LEAN, MERGE, PAIRED>::kThreads)) __att
             const bool planes = req >= 16 && !__any(olB < 16) && !(abl & 128);
             if (planes) {
                 uint32_t cand[kOvBlocks];
-                ov_candidates(col, cm, mpos, fixed, K, cnt, cand);
+                ov_candidates(col, cm, mpos, FixedOwn{unzip2(fixed)}, K, cnt, cand);
                 for (;;) {  // candidates in offset order until one passes the exact test
                     int o = -1;
 #pragma unroll

@@ -40,7 +40,7 @@ def synth_device(lib, torch, n, paired, first):
 
 
 @pytest.mark.parametrize("name,n", [("C2", 20_000_017), ("C3", 20_000_017), ("C3", 100_000_000), ("C4", 20_000_017),
-                                    ("C5", 20_000_017), ("C3b", 4_000_005), ("PE_all", 4_000_005),
+                                    ("C5", 20_000_017), ("C3b", 20_000_021), ("PE_all", 4_000_005),
                                     ("PE_correct", 4_000_005), ("PE_correct_x", 4_000_005), ("PE_correct_merge", 4_000_005), ("PE_umi_merge", 4_000_005), ("PE_correct_front", 4_000_005), ("PE_correct_umi_merge", 4_000_005),
                                     ("PE_umi_x", 4_000_005)])
 def test_fullsize_parity(eng_lib, oracle, name, n):
