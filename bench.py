@@ -88,6 +88,21 @@ def sq_profile(cfg, pairs):
     return d, os.path.relpath(paths[-1], REPO)
 
 
+def isa_cpi(cfg):
+    """Average issue cycles per VALU instruction of this workload's fast-kernel instantiation, from the
+    latest committed static ISA budget (tools/isa_budget.py: every instruction of the tile loop priced
+    with the opcode costs measured on gfx950, profiles/r04_micro_opcost2.txt): (value, source) or
+    (None, None)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_isa_cpi.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    e = d.get(cfg)
+    return (e["cycles_per_valu"], os.path.relpath(paths[-1], REPO)) if e else (None, None)
+
+
 def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -705,28 +720,30 @@ def run_rank(args):
     traffic, traffic_src = pmc_traffic(args.config, args.pairs) if world == 1 else (None, None)
     sq, sq_src = sq_profile(args.config, args.pairs) if world == 1 else (None, None)
     valu = None
-    if sq and kavg and sq.get("kernel_ms_trace") and abs(sq["kernel_ms_trace"] / kavg - 1) > 0.05:
+    sq_ms = (sq or {}).get("kernel_ms_trace") or (sq or {}).get("kernel_ms_bench")
+    if sq and kavg and sq_ms and abs(sq_ms / kavg - 1) > 0.05:
         # the committed SQ counters were taken on another build (its kernel time differs from this
         # run's by more than 5 %): not reported as this build's
-        log(f"SQ profile {sq_src} is stale ({sq['kernel_ms_trace']:.3f} ms vs this run's {kavg:.3f} ms): not used")
-        valu = {"stale_profile": sq_src, "profile_kernel_ms": sq["kernel_ms_trace"], "run_kernel_ms": round(kavg, 3)}
+        log(f"SQ profile {sq_src} is stale ({sq_ms:.3f} ms vs this run's {kavg:.3f} ms): not used")
+        valu = {"stale_profile": sq_src, "profile_kernel_ms": sq_ms, "run_kernel_ms": round(kavg, 3)}
         sq = None
-    if sq and kavg and sq.get("counters_per_launch", {}).get("SQ_INSTS_VALU"):
-        # VALU issue fraction: each wave64 VALU instruction holds a SIMD-32 for 2 cycles
-        # (MI355X_MICROARCH.md); peak = 1024 SIMDs x 2.4 GHz; the instruction count is the committed
-        # PMC profile's, the time is this run's HIP-event kernel time
+    if sq and kavg and sq.get("counters_per_launch", {}).get("SQ_INSTS_VALU") and sq.get("kernel_cycles"):
+        # VALU issue: the profiled launch's VALU wave-instructions (SQ_INSTS_VALU, per launch) over the
+        # SIMD cycles of that launch (1024 SIMDs x its kernel cycles, GRBM_GUI_ACTIVE per XCD: the
+        # clock the kernel actually ran at).  `frac_at_2_cycles` prices every VALU at the nominal 2
+        # cycles per wave64 instruction (a lower bound); `issue_frac` at the tile loop's static
+        # average cost per VALU (isa_cpi: VOP3 forms take ~4.4 cycles, VOP2 ~2.3) -- an estimate of
+        # the share of SIMD cycles spent issuing VALU, <= 1 by construction of both counts.
         n_valu = sq["counters_per_launch"]["SQ_INSTS_VALU"]
+        simd_cycles = SIMDS * sq["kernel_cycles"]
+        cpi, cpi_src = isa_cpi(args.config)
         valu = {"insts_per_launch": n_valu, "per_tile": sq.get("valu_per_tile"),
-                "frac": round(n_valu * 2 / (SIMDS * CLOCK_HZ * kavg / 1e3), 4),
-                "frac_at_profiled_clock": sq.get("valu_issue_frac"), "src": sq_src,
-                "wait_frac": sq.get("wait_frac"), "inst_stall_frac": sq.get("inst_stall_frac"),
+                "frac_at_2_cycles": round(n_valu * 2 / simd_cycles, 4),
+                "cycles_per_valu_static": cpi, "cpi_src": cpi_src,
+                "issue_frac": round(n_valu * cpi / simd_cycles, 4) if cpi else None,
+                "kernel_clock_GHz": round(sq["kernel_cycles"] / (sq_ms * 1e-3) / 1e9, 3) if sq_ms else None,
+                "src": sq_src, "wait_frac": sq.get("wait_frac"), "inst_stall_frac": sq.get("inst_stall_frac"),
                 "active_frac": sq.get("active_frac")}
-        act = sq["counters_per_launch"].get("SQ_ACTIVE_INST_VALU")
-        if act and sq.get("kernel_cycles"):
-            # the SIMDs' VALU issue occupancy: SQ_ACTIVE_INST_VALU (quad cycles summed over waves) x 4
-            # over SIMDs x the profiled kernel cycles -- most VOP3 ops hold a SIMD ~4.5 cycles, not 2
-            # (profiles/r03_micro_opcost.txt), so this, not `frac`, is the issue-bound measure
-            valu["issue_busy_frac"] = round(act * 4 / (SIMDS * sq["kernel_cycles"]), 4)
     bytes_per_pair = (2 if paired else 1) * (2 * READ_LEN + 16)  # seq+qual uint8 + 16 B result per read
     achieved = n * bytes_per_pair / (kavg / 1e3) / 1e9 if kavg else None
     out = {
@@ -747,10 +764,10 @@ def run_rank(args):
                    "read_len": READ_LEN, "row_stride": STRIDE,
                    "parallelism": f"dp{world} (pairs sharded, RCCL sum of the accumulator block)"},
         # frac / achieved / peak are the HBM roofline (algorithmic bytes over the kernel time);
-        # `bound` names what limits the kernel: VALU issue when the SQ counters show the SIMDs' issue
-        # busier than HBM is, else HBM
-        "roofline": {"bound": ("valu_issue" if valu and valu.get("issue_busy_frac") and achieved and
-                               valu["issue_busy_frac"] > achieved / HBM_PEAK_GBS + 0.1 else "hbm"),
+        # `bound` names what limits the kernel: VALU issue when the estimated VALU issue share of the
+        # SIMD cycles (valu.issue_frac) is >= 0.75 and above the HBM fraction, else HBM
+        "roofline": {"bound": ("valu_issue" if valu and valu.get("issue_frac") and achieved and
+                               valu["issue_frac"] >= 0.75 and valu["issue_frac"] > achieved / HBM_PEAK_GBS else "hbm"),
                      "frac_of": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": traffic, "traffic_unit": "bytes per launch (PMC)", "traffic_src": traffic_src,
