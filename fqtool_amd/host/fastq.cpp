@@ -90,13 +90,22 @@ void ByteBuf::release() {
 
 std::atomic<uint64_t> g_pinned_regrows{0}, g_pinned_bytes{0};
 static std::mutex g_retired_m;
-// page-locked blocks outgrown mid-run: freed by the exit, or by free_retired_pinned() once the run's
-// engines are gone (in-process callers of fqh_run)
+// page-locked blocks outgrown mid-run: freed by the exit, or, for in-process callers of fqh_run, once
+// no run is left whose copies might still target them (runs may overlap: a block retired by one run
+// stays until every run that was active has ended)
 static std::vector<std::pair<void*, size_t>> g_retired;
 static size_t g_retired_bytes = 0;
+static int g_pinned_runs = 0;
 
-void free_retired_pinned() {
+void pinned_run_begin() {
     std::lock_guard<std::mutex> g(g_retired_m);
+    ++g_pinned_runs;
+}
+
+void pinned_run_end() {
+    std::lock_guard<std::mutex> g(g_retired_m);
+    if (--g_pinned_runs > 0) return;
+    g_pinned_runs = 0;
     for (auto& b : g_retired) {
         fq_host_free(b.first);
         g_pinned_bytes -= b.second;

@@ -36,8 +36,9 @@ namespace fqhost {
 // runs the pre-pass first, src/main.cpp:139-143).
 void set_reader_stderr_gate(std::shared_future<void> gate);
 void reader_stderr(const std::string& s);
-// frees the page-locked blocks that buffers outgrew during a run (call once its engines are gone)
-void free_retired_pinned();
+// page-locked blocks a run outgrew are kept registered until every run active with it has ended
+void pinned_run_begin();
+void pinned_run_end();
 
 // Growable byte buffer that keeps its capacity when cleared (packs are recycled) and does not
 // zero what it allocates.  A pinned buffer takes page-locked memory from the engine

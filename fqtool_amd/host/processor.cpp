@@ -406,6 +406,22 @@ class Queue {  // bounded FIFO between pipeline threads; push/pop return at once
         not_full_.notify_one();
         return true;
     }
+    // pop / pop_recent waiting at most d: 1 taken, 0 timed out, -1 closed and drained
+    int pop_for(T& v, std::chrono::microseconds d, bool recent = false) {
+        std::unique_lock<std::mutex> l(m_);
+        // (system_clock: see Lane::run_raw_multi's wait_polling)
+        if (!not_empty_.wait_until(l, std::chrono::system_clock::now() + d, [&] { return !q_.empty() || closed_; })) return 0;
+        if (q_.empty()) return -1;
+        if (recent) {
+            v = std::move(q_.back());
+            q_.pop_back();
+        } else {
+            v = std::move(q_.front());
+            q_.pop_front();
+        }
+        not_full_.notify_one();
+        return 1;
+    }
     // pop_recent without waiting: 1 taken, 0 empty (not closed), -1 closed and drained
     int try_pop_recent(T& v) {
         std::lock_guard<std::mutex> l(m_);
@@ -467,25 +483,25 @@ class AsyncWriter {
         }
     }
     void write(std::vector<std::string> blocks) {
-        if (err_) std::rethrow_exception(err_);
+        if (failed_) std::rethrow_exception(error());
         bool any = false;
         for (const auto& s : blocks) any = any || !s.empty();
-        if (any) q_.push(Job{std::move(blocks), nullptr, 0, nullptr, nullptr});
+        if (any && !q_.push(Job{std::move(blocks), nullptr, 0, nullptr, nullptr}) && failed_) std::rethrow_exception(error());
     }
     // queue n bytes at p (which stay valid until `done` runs); the writer thread runs it once the
     // bytes are written (or dropped after a write error)
     void write_raw(const char* p, size_t n, std::function<void()> done) {
-        if (err_ || !q_.push(Job{{}, p, n, done, nullptr})) {
+        if (failed_ || !q_.push(Job{{}, p, n, done, nullptr})) {
             done();  // (the writer has stopped: nothing will take the text)
-            if (err_) std::rethrow_exception(err_);
+            if (failed_) std::rethrow_exception(error());
             throw std::runtime_error("write to a closed output");
         }
     }
     // queue byte ranges (plain outputs; they stay valid until `done` runs), as write_raw
     void write_segs(const std::vector<iovec>* segs, std::function<void()> done) {
-        if (err_ || !q_.push(Job{{}, nullptr, 0, done, segs})) {
+        if (failed_ || !q_.push(Job{{}, nullptr, 0, done, segs})) {
             done();
-            if (err_) std::rethrow_exception(err_);
+            if (failed_) std::rethrow_exception(error());
             throw std::runtime_error("write to a closed output");
         }
     }
@@ -498,16 +514,15 @@ class AsyncWriter {
         if (io_) {  // (the ranges claimed so far are written, or failed)
             io_->close();
             for (auto& t : io_t_) t.join();
-            if (io_err_ && !err_) err_ = io_err_;
         }
-        if (!err_) {
+        if (!failed_) {
             try {
                 w_.close();
             } catch (...) {
-                err_ = std::current_exception();
+                fail(std::current_exception());
             }
         }
-        if (err_) std::rethrow_exception(err_);
+        if (failed_) std::rethrow_exception(error());
     }
 
    private:
@@ -526,11 +541,15 @@ class AsyncWriter {
         Io x;
         while (io_->pop(x)) {
             try {
-                if (x.job.segs) w_.write_segs_at(x.off, x.job.segs->data(), x.job.segs->size());
-                else w_.write_at(x.off, x.job.raw, x.job.raw_n);
+                if (!failed_) {  // (after a failure the claimed ranges are dropped)
+                    if (x.job.segs) w_.write_segs_at(x.off, x.job.segs->data(), x.job.segs->size());
+                    else w_.write_at(x.off, x.job.raw, x.job.raw_n);
+                }
             } catch (...) {
-                std::lock_guard<std::mutex> g(io_m_);
-                if (!io_err_) io_err_ = std::current_exception();
+                // (e.g. ENOSPC) visible to the producers at once: their next write rethrows it, the
+                // writer thread stops claiming ranges and releases what is queued
+                fail(std::current_exception());
+                q_.close();
             }
             x.job.done();
         }
@@ -539,6 +558,10 @@ class AsyncWriter {
         Job j;
         try {
             while (q_.pop(j)) {
+                if (failed_) {  // (an I/O thread's write failed: this job is released, the rest below)
+                    if (j.done) j.done();
+                    std::rethrow_exception(error());
+                }
                 if (j.done && io_) {  // claim the range here (output order), write it on an I/O thread
                     size_t n = j.raw_n;
                     if (j.segs) {
@@ -563,21 +586,31 @@ class AsyncWriter {
                 }
             }
         } catch (...) {
-            err_ = std::current_exception();
+            fail(std::current_exception());
             q_.close();  // the producer's next push returns at once; write() rethrows
             while (q_.pop(j))  // (raw jobs queued behind the failure are released)
                 if (j.done) j.done();
         }
     }
+    // the first error of the writer or an I/O thread; producers see failed_ without the lock
+    void fail(std::exception_ptr e) {
+        std::lock_guard<std::mutex> g(err_m_);
+        if (!err_) err_ = e;
+        failed_ = true;
+    }
+    std::exception_ptr error() {
+        std::lock_guard<std::mutex> g(err_m_);
+        return err_;
+    }
     Writer w_;
     Pool* pool_;
     Queue<Job> q_;
+    std::mutex err_m_;
     std::exception_ptr err_;
+    std::atomic<bool> failed_{false};
     bool closed_ = false;
     std::unique_ptr<Queue<Io>> io_;
     std::vector<std::thread> io_t_;
-    std::mutex io_m_;
-    std::exception_ptr io_err_;
     std::thread t_;
 };
 
@@ -1747,6 +1780,29 @@ struct Lane {
         bool have_held = false;
         bool input_done = false;
         bool engine_raw = false;
+        // Every wait of this thread polls its own packs in flight meanwhile: a pack that is done but
+        // not polled holds its staging window and its pack, and the formatter takes packs in input
+        // order, so an engine that waited without polling (for a window, its enqueue turn, its launch
+        // turn or a spare pack) could hold exactly what the others wait for.
+        const auto tick = std::chrono::microseconds(300);
+        auto poll_done = [&] {
+            while (!inflight.empty() && complete_oldest(false)) {
+            }
+        };
+        auto wait_polling = [&](std::unique_lock<std::mutex>& lk, auto pred) {
+            while (!pred()) {
+                if (inflight.empty()) {
+                    R.cv.wait(lk, pred);
+                    return;
+                }
+                // (system_clock: pthread_cond_timedwait, which ThreadSanitizer intercepts; a steady-clock
+                // wait goes through pthread_cond_clockwait, which the toolchain's libtsan does not)
+                if (R.cv.wait_until(lk, std::chrono::system_clock::now() + tick, pred)) return;
+                lk.unlock();
+                poll_done();
+                lk.lock();
+            }
+        };
         auto drop_all = [&] {  // windows not launched: their copies finish, then the stages return
             (void)fq_engine_sync(e);
             if (engine_raw) (void)fq_engine_raw_end(e);
@@ -1769,7 +1825,11 @@ struct Lane {
                 while (enq.size() < raw_ahead && !input_done) {
                     // (wait for a window only when none is enqueued: the front one may be due)
                     if (!have_held) {
-                        const int got = enq.empty() ? (R.wq[(size_t)g]->pop(held) ? 1 : -1) : R.wq[(size_t)g]->try_pop(held);
+                        int got = R.wq[(size_t)g]->try_pop(held);
+                        while (got == 0 && enq.empty()) {
+                            got = R.wq[(size_t)g]->pop_for(held, tick);
+                            if (got == 0) poll_done();
+                        }
                         if (got == 0) break;
                         if (got < 0) {
                             input_done = true;
@@ -1779,7 +1839,7 @@ struct Lane {
                     }
                     if (!held.end) {  // its turn: the window before it has been enqueued (on any engine)
                         std::unique_lock<std::mutex> lk(R.m);
-                        if (enq.empty()) R.cv.wait(lk, [&] { return R.stopped || R.next_enqueue == held.id; });
+                        if (enq.empty()) wait_polling(lk, [&] { return R.stopped || R.next_enqueue == held.id; });
                         if (R.stopped) {
                             stop_now = true;
                             break;
@@ -1832,7 +1892,7 @@ struct Lane {
                 {
                     const auto t0w = std::chrono::steady_clock::now();
                     std::unique_lock<std::mutex> lk(R.m);
-                    R.cv.wait(lk, [&] { return R.stopped || R.next_launch == w.id; });
+                    wait_polling(lk, [&] { return R.stopped || R.next_launch == w.id; });
                     raw_turn_wait_s += since(t0w);
                     if (R.stopped) {
                         give_back();
@@ -1853,10 +1913,11 @@ struct Lane {
                     if (!pk) {  // (the turn stays ours while the lock is released)
                         lk.unlock();
                         const auto p0 = std::chrono::steady_clock::now();
-                        const bool got = spare.pop_recent(pk);
+                        int got;
+                        while ((got = spare.pop_for(pk, tick, true)) == 0) poll_done();
                         raw_pack_wait_s += since(p0);
                         lk.lock();
-                        if (!got) throw Stopped();
+                        if (got < 0) throw Stopped();
                         if (R.stopped) {  // (an error elsewhere)
                             give_back();
                             break;
@@ -2038,6 +2099,12 @@ Options prepare_options(int argc, char** argv, bool detect_adapters) {
 }
 
 int run_tool(int argc, char** argv, bool exit_when_done) {
+    // (declared first, so destroyed last: the page-locked blocks this run outgrew are freed once its
+    // engines are gone and no other in-process run is active)
+    struct PinnedRun {
+        PinnedRun() { pinned_run_begin(); }
+        ~PinnedRun() { pinned_run_end(); }
+    } pinned_run;
     Options o;
     const auto t0 = std::chrono::steady_clock::now();
     try {
@@ -2457,12 +2524,8 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
         if (det.valid()) det.wait();  // the pre-pass's messages come first, as in the reference
         else if (det_on && !det_started) det_done.set_value();  // (it never started: release the reader's gate)
         std::cerr << "ERROR: " << e.what() << std::endl;
-        free_retired_pinned();
         return 255;
     }
-    // (the engines are gone: the page-locked blocks outgrown during the run can go too, so an
-    // in-process caller does not keep them registered for its lifetime)
-    free_retired_pinned();
     return 0;
 }
 

@@ -21,6 +21,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 #include <algorithm>
@@ -55,6 +56,7 @@ struct fq_engine {
         fq_text_out* text_out = nullptr;
         fq_raw_out* raw_out = nullptr;
         uint64_t bytes[2] = {0, 0}, ad_bytes[2] = {0, 0};
+        std::chrono::steady_clock::time_point ready_at{};  // (FQ_CPU_ENGINE_DELAY_US)
     };
     std::deque<std::shared_ptr<Task>> work;   // not yet run, in call order
     std::deque<std::shared_ptr<Task>> packs;  // submitted packs, in order; front = oldest not yet polled
@@ -68,6 +70,11 @@ struct fq_engine {
     std::shared_ptr<RawWin> raw_prev;               // the last window enqueued
     std::deque<std::shared_ptr<RawWin>> raw_queued;  // enqueued, not launched
 
+    // FQ_CPU_ENGINE_DELAY_US: a pack is reported done no earlier than this long after its submission
+    // (its work still runs at once, so raw-window indexing is not held up behind it -- as on the GPU,
+    // where the index runs on its own stream while earlier packs' kernels run).  Tests: packs stay in
+    // flight, so the host's pack and staging budgets run out while engines wait for their turns.
+    long delay_us = 0;
     void run() {
         std::unique_lock<std::mutex> lk(m);
         for (;;) {
@@ -95,6 +102,7 @@ struct fq_engine {
         t->seq = seq;
         t->text_out = text_out;
         t->raw_out = raw_out;
+        t->ready_at = std::chrono::steady_clock::now() + std::chrono::microseconds(pack ? delay_us : 0);
         std::lock_guard<std::mutex> lk(m);
         work.push_back(t);
         if (pack) packs.push_back(t);
@@ -131,6 +139,7 @@ int fq_engine_create(const fq_params* params, int device, int32_t max_batch, int
     e->max_batch = max_batch;
     e->max_stride = max_stride;
     e->acc.assign(fq_acc_words(params->insert_size_max, params->max_cycles), 0);
+    if (const char* d = std::getenv("FQ_CPU_ENGINE_DELAY_US")) e->delay_us = std::atol(d);
     e->worker = std::thread([e] { e->run(); });
     *out = e;
     return FQ_OK;
@@ -159,9 +168,13 @@ int fq_engine_poll(fq_engine* e, int wait, uint64_t* seq_no) {
     if (!e) return FQ_E_INVALID;
     std::unique_lock<std::mutex> lk(e->m);
     if (e->packs.empty()) return 0;
-    if (!e->packs.front()->done) {
+    if (!e->packs.front()->done || std::chrono::steady_clock::now() < e->packs.front()->ready_at) {
         if (!wait) return 0;
         e->cv.wait(lk, [e] { return e->packs.front()->done; });
+        const auto at = e->packs.front()->ready_at;
+        lk.unlock();
+        std::this_thread::sleep_until(at);
+        lk.lock();
     }
     const std::shared_ptr<fq_engine::Task> t = e->packs.front();
     e->packs.pop_front();
@@ -664,6 +677,7 @@ int fq_dup_stat(fq_dup* d, int32_t hist_size, uint64_t* hist, uint64_t* gc_sum, 
 
 int fq_kmer_open(int device, const uint8_t* seq, const uint32_t* off, int32_t n, fq_kmer_set** out) {
     if (!out) return FQ_E_INVALID;
+    if (std::getenv("FQ_CPU_KMER_FAIL")) return FQ_E_NO_DEVICE;  // (tests: the detection fails after the pipeline ran)
     void* k = nullptr;
     const int rc = orc_kmer_open(device, seq, off, n, &k);
     if (rc != FQ_OK) return rc;

@@ -67,6 +67,45 @@ def test_raw_stream_small_windows_cpu(case, devices, cpu_build, tmp_path):
     E.check_outputs(case, str(outd))
 
 
+@pytest.mark.parametrize("devices", ["0,0,0,0", "0,0,0,0,0,0,0,0"])
+@pytest.mark.parametrize("case", ["synth_pe_c3", "td_pe_merge"])
+def test_raw_stream_slow_engines_cpu(case, devices, cpu_build, tmp_path):
+    """Engines slower than the host (each pack >= 2 ms on the stand-in), 4 KiB first windows and 7-pair
+    packs: every engine keeps its packs in flight, so the spare packs and staging windows run out
+    while engines wait for their turns.  Each wait polls the engine's own packs, so the stream must
+    finish (bounded by the timeout) with the reference's outputs (the turn holder waiting
+    for a spare pack while every pack sat unpolled in an engine)."""
+    ind, outd = tmp_path / "in", tmp_path / "out"
+    ind.mkdir()
+    outd.mkdir()
+    argv = plain_inputs(E.argv_for(CPU_BIN, case, str(outd)), str(ind))
+    argv += ["--pack_pairs", "7", "--devices", devices]
+    env = dict(os.environ, FQ_RAW_WINDOW0="4096", FQ_CPU_ENGINE_DELAY_US="2000")
+    p = subprocess.run(argv, capture_output=True, cwd=outd, timeout=240, env=env)
+    err = p.stderr.decode(errors="replace")
+    assert p.returncode == 0, err[-2000:]
+    assert "raw stream on %d engines" % len(devices.split(",")) in err, err[-1000:]
+    E.check_outputs(case, str(outd))
+
+
+@pytest.mark.parametrize("devices", ["0", "0,0,0"])
+def test_detection_error_after_pipeline_cpu(devices, cpu_build, tmp_path):
+    """The PE adapter detection runs concurrently and is joined after the pipeline; when it fails
+    there (the stand-in's k-mer device refuses, FQ_CPU_KMER_FAIL) the tool must report it as the
+    reference reports a failed pre-pass -- "ERROR: ..." and exit status 255, no outputs left behind
+    (src/main.cpp:137-141) -- not end in std::terminate (its completion promise was once set twice)."""
+    ind, outd = tmp_path / "in", tmp_path / "out"
+    ind.mkdir()
+    outd.mkdir()
+    argv = plain_inputs(E.argv_for(CPU_BIN, "td_pe_detect", str(outd)), str(ind)) + ["--devices", devices]
+    env = dict(os.environ, FQ_CPU_KMER_FAIL="1")
+    p = subprocess.run(argv, capture_output=True, cwd=outd, timeout=120, env=env)
+    err = p.stderr.decode(errors="replace")
+    assert p.returncode == 255, err[-2000:]
+    assert "ERROR: adapter detection" in err and "terminate" not in err, err[-2000:]
+    assert not (outd / "o1.fq").exists() and not (outd / "o2.fq").exists()
+
+
 @pytest.mark.parametrize("zc", ["1", "0"])
 @pytest.mark.parametrize("case", ["td_pe_qag", "synth_pe_c3", "td_pe_merge", "synth_se_c2", "edge_pe_all", "td_pe_plain",
                                   "td_se_q", "polygr_pe"])
