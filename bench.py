@@ -312,7 +312,7 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             r = {"value": round(2 * pairs / dt / 1e6, 3), "unit": "Mreads/s", "pairs": pairs,
                  "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
                  "runs_wall_s": [round(r[0], 3) for r in runs], "pause_between_runs_s": E2E_PAUSE_S,
-                 "options": " ".join(extra), "outputs": outputs,
+                 "options": " ".join(extra), "outputs": outputs, "affinity_cpus": host_cores(),
                  "path": e2e_path(tool_log),
                  "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
             if outputs != "null":

@@ -1276,23 +1276,41 @@ struct RawMulti {
         }
         for (auto& q : wq) q->close();
     }
+    // Line feeds in [p, p + n): byte counters (each compare's 0xFF subtracted, i.e. +1), summed by
+    // v_sad-style _mm_sad_epu8 every 255 steps -- no popcount (the build targets baseline x86-64,
+    // where __builtin_popcount is a library call per 16 bytes).
     static uint32_t count_lf(const char* p, size_t n) {
-        uint32_t c = 0;
+        uint64_t c = 0;
         size_t i = 0;
-        const __m128i nl = _mm_set1_epi8('\n');
-        for (; i + 16 <= n; i += 16)
-            c += (uint32_t)__builtin_popcount(
-                (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i)), nl)));
+        const __m128i nl = _mm_set1_epi8('\n'), zero = _mm_setzero_si128();
+        while (i + 16 <= n) {
+            __m128i acc = zero;
+            const size_t end = std::min(n & ~(size_t)15, i + 255 * 16);
+            for (; i < end; i += 16)
+                acc = _mm_sub_epi8(acc, _mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i)), nl));
+            const __m128i s = _mm_sad_epu8(acc, zero);
+            c += (uint64_t)_mm_cvtsi128_si64(s) + (uint64_t)_mm_cvtsi128_si64(_mm_unpackhi_epi64(s, s));
+        }
         for (; i < n; ++i) c += p[i] == '\n';
-        return c;
+        return (uint32_t)c;
     }
-    // offset of the k-th (1-based) line feed in [p, p + n)
+    // offset of the k-th (1-based) line feed in [p, p + n): whole 4 KiB blocks counted as above, then
+    // 16 bytes a step within the block that holds it
     static uint64_t nth_lf(const char* p, size_t n, size_t k) {
+        size_t b = 0;
+        for (; b + 4096 <= n; b += 4096) {
+            const size_t c = count_lf(p + b, 4096);
+            if (c >= k) break;
+            k -= c;
+        }
+        return b + nth_lf_scan(p + b, n - b, k);
+    }
+    static uint64_t nth_lf_scan(const char* p, size_t n, size_t k) {
         size_t i = 0;
         const __m128i nl = _mm_set1_epi8('\n');
         for (; i + 16 <= n; i += 16) {  // 16 bytes a step; the k-th within a step by its bit mask
             unsigned mk = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + i)), nl));
-            const size_t c = (size_t)__builtin_popcount(mk);
+            const size_t c = (size_t)popcount16(mk);
             if (c < k) {
                 k -= c;
                 continue;
@@ -1303,6 +1321,12 @@ struct RawMulti {
         for (; i < n; ++i)
             if (p[i] == '\n' && --k == 0) return i;
         throw std::runtime_error("raw window: line feed count mismatch");
+    }
+    static unsigned popcount16(unsigned x) {  // (16-bit mask; baseline x86-64 has no popcnt)
+        x = x - ((x >> 1) & 0x5555u);
+        x = (x & 0x3333u) + ((x >> 2) & 0x3333u);
+        x = (x + (x >> 4)) & 0x0F0Fu;
+        return (x + (x >> 8)) & 0x1Fu;
     }
 };
 

@@ -79,7 +79,8 @@ def main():
             write_fastq(p, args.pairs, m)
         gb = 2 * args.pairs * REC / 1e9
         print(json.dumps({"input_GB": round(gb, 3), "pairs": args.pairs, "written_s": round(time.time() - t0, 1),
-                          "host_cpus": os.cpu_count()}), flush=True)
+                          "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+                          "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}), flush=True)
         env = dict(os.environ, LD_LIBRARY_PATH=libdir, FQ_NULL_REC1=str(REC), FQ_NULL_REC2=str(REC), FQ_NULL_LEN=str(READ_LEN))
         runs = []
         for eg in args.egress.split(","):

@@ -17,6 +17,9 @@
 #include <string>
 #include <vector>
 
+#include <map>
+#include <mutex>
+#include <sys/mman.h>
 #include "../../include/fqengine.h"
 
 struct fq_engine {
@@ -176,12 +179,33 @@ int fq_engine_raw_end(fq_engine* e) {
     return FQ_OK;
 }
 
+// as the engine's (engine.hip): anonymous 2 MiB-page memory populated on the calling thread (the real
+// one then registers it with HIP), so the feed's first-touch costs land where the tool's do
+static std::mutex g_host_mu;
+static std::map<void*, size_t> g_host_maps;
 int fq_host_alloc(size_t bytes, void** out) {
-    *out = std::aligned_alloc(4096, (bytes + 4095) / 4096 * 4096);
-    return *out ? FQ_OK : FQ_E_NOMEM;
+    const size_t huge = (size_t)2 << 20;
+    const size_t len = ((bytes ? bytes : 1) + huge - 1) / huge * huge;
+    void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) return FQ_E_NOMEM;
+    (void)madvise(m, len, MADV_HUGEPAGE);
+    std::memset(m, 0, len);
+    std::lock_guard<std::mutex> g(g_host_mu);
+    g_host_maps[m] = len;
+    *out = m;
+    return FQ_OK;
 }
 int fq_host_free(void* p) {
-    std::free(p);
+    if (!p) return FQ_OK;
+    size_t len = 0;
+    {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        auto it = g_host_maps.find(p);
+        if (it == g_host_maps.end()) return FQ_E_INVALID;
+        len = it->second;
+        g_host_maps.erase(it);
+    }
+    munmap(p, len);
     return FQ_OK;
 }
 
