@@ -544,25 +544,42 @@ class BgzfSource {
 // reservation) leaves the file to zlib's stream reader from its start, which reproduces the
 // reference's behaviour on corrupt input.
 namespace {
+}  // namespace
 struct Libdeflate {
     void* (*alloc)();
     int (*gzip_ex)(void*, const void*, size_t, void*, size_t, size_t*, size_t*);
+    int (*deflate_ex)(void*, const void*, size_t, void*, size_t, size_t*, size_t*);  // raw deflate
     void (*free_)(void*);
-    bool ok = false;
+    // compression (BGZF members): alloc_compressor(level), deflate_compress -> bytes or 0 if it did
+    // not fit, free_compressor, crc32
+    void* (*calloc_)(int);
+    size_t (*compress)(void*, const void*, size_t, void*, size_t);
+    void (*cfree)(void*);
+    uint32_t (*crc32_)(uint32_t, const void*, size_t);
+    bool ok = false, cok = false;
     Libdeflate() {
         void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
         if (!h) return;
         alloc = reinterpret_cast<void* (*)()>(dlsym(h, "libdeflate_alloc_decompressor"));
         gzip_ex = reinterpret_cast<int (*)(void*, const void*, size_t, void*, size_t, size_t*, size_t*)>(
             dlsym(h, "libdeflate_gzip_decompress_ex"));
+        deflate_ex = reinterpret_cast<int (*)(void*, const void*, size_t, void*, size_t, size_t*, size_t*)>(
+            dlsym(h, "libdeflate_deflate_decompress_ex"));
         free_ = reinterpret_cast<void (*)(void*)>(dlsym(h, "libdeflate_free_decompressor"));
-        ok = alloc && gzip_ex && free_;
+        ok = alloc && gzip_ex && deflate_ex && free_;
+        calloc_ = reinterpret_cast<void* (*)(int)>(dlsym(h, "libdeflate_alloc_compressor"));
+        compress = reinterpret_cast<size_t (*)(void*, const void*, size_t, void*, size_t)>(dlsym(h, "libdeflate_deflate_compress"));
+        cfree = reinterpret_cast<void (*)(void*)>(dlsym(h, "libdeflate_free_compressor"));
+        crc32_ = reinterpret_cast<uint32_t (*)(uint32_t, const void*, size_t)>(dlsym(h, "libdeflate_crc32"));
+        const char* z = std::getenv("FQ_GZ_ZLIB");  // 1: BGZF members through zlib's deflate (A/B)
+        cok = calloc_ && compress && cfree && crc32_ && !(z && std::string(z) == "1");
     }
 };
 const Libdeflate& libdeflate() {
     static const Libdeflate l;
     return l;
 }
+namespace {
 
 // the inflated text of gzip file `path` in an anonymous mapping (*out, *n bytes; munmap the
 // reserved *cap bytes), or false
@@ -1475,7 +1492,60 @@ namespace {
 // inflate the members on several threads; any gzip reader reads them as a plain multi-member
 // stream.  (src/writer.cpp:36-47 writes one gzwrite stream at level -z; the decompressed text is
 // what parity compares.)  An empty `s` gives one empty member.
+// One member's deflate payload through libdeflate (a compressor per thread and level, kept for the
+// thread's life); a member that does not fit BGZF's 64 KiB is stored (one stored deflate block).
+void bgzf_append(std::string& out, const char* in, size_t n, uint32_t crc, const char* data, size_t clen) {
+    const uint32_t bsize = (uint32_t)(clen + 25);
+    const unsigned char hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0,
+                                   (unsigned char)(bsize & 0xff), (unsigned char)(bsize >> 8)};
+    out.append(reinterpret_cast<const char*>(hdr), 18);
+    out.append(data, clen);
+    const unsigned char tr[8] = {(unsigned char)crc, (unsigned char)(crc >> 8), (unsigned char)(crc >> 16),
+                                 (unsigned char)(crc >> 24), (unsigned char)n, (unsigned char)(n >> 8),
+                                 (unsigned char)(n >> 16), (unsigned char)(n >> 24)};
+    out.append(reinterpret_cast<const char*>(tr), 8);
+    (void)in;
+}
+std::string gzip_member_libdeflate(const std::string& s, int level) {
+    constexpr size_t kIn = 0xff00;
+    const Libdeflate& ld = libdeflate();
+    struct Cache {
+        void* c[13] = {};
+        ~Cache() {
+            for (void* p : c)
+                if (p) libdeflate().cfree(p);
+        }
+    };
+    static thread_local Cache cache;
+    const int lvl = std::min(12, std::max(1, level));
+    void*& c = cache.c[lvl];
+    if (!c) c = ld.calloc_(lvl);
+    if (!c) throw std::runtime_error("libdeflate_alloc_compressor failed");
+    std::string out;
+    out.reserve(s.size() / 3 + 64);
+    char tmp[65536];
+    size_t o = 0;
+    do {
+        const size_t n = std::min(kIn, s.size() - o);
+        const char* in = s.data() + o;
+        const uint32_t crc = ld.crc32_(0, in, n);
+        size_t clen = ld.compress(c, in, n, tmp, 65536 - 26);
+        if (clen == 0) {  // stored: BFINAL, BTYPE 00, LEN, NLEN, the bytes
+            tmp[0] = 1;
+            tmp[1] = (char)(n & 0xff);
+            tmp[2] = (char)(n >> 8);
+            tmp[3] = (char)(~n & 0xff);
+            tmp[4] = (char)((~n >> 8) & 0xff);
+            std::memcpy(tmp + 5, in, n);
+            clen = n + 5;
+        }
+        bgzf_append(out, in, n, crc, tmp, clen);
+        o += n;
+    } while (o < s.size());
+    return out;
+}
 std::string gzip_member(const std::string& s, int level) {
+    if (libdeflate().cok) return gzip_member_libdeflate(s, level);
     constexpr size_t kIn = 0xff00;
     z_stream z;
     std::memset(&z, 0, sizeof z);
@@ -1504,15 +1574,8 @@ std::string gzip_member(const std::string& s, int level) {
             if (clen + 26 <= 65536) break;
         }
         if (clen + 26 > 65536) throw std::runtime_error("deflate: BGZF block too large");
-        const uint32_t bsize = (uint32_t)(clen + 25), crc = (uint32_t)crc32(crc32(0, nullptr, 0), in, (uInt)n);
-        const unsigned char hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0,
-                                       (unsigned char)(bsize & 0xff), (unsigned char)(bsize >> 8)};
-        out.append(reinterpret_cast<const char*>(hdr), 18);
-        out.append(tmp.data(), clen);
-        const unsigned char tr[8] = {(unsigned char)crc, (unsigned char)(crc >> 8), (unsigned char)(crc >> 16),
-                                     (unsigned char)(crc >> 24), (unsigned char)n, (unsigned char)(n >> 8),
-                                     (unsigned char)(n >> 16), (unsigned char)(n >> 24)};
-        out.append(reinterpret_cast<const char*>(tr), 8);
+        const uint32_t crc = (uint32_t)crc32(crc32(0, nullptr, 0), in, (uInt)n);
+        bgzf_append(out, reinterpret_cast<const char*>(in), n, crc, tmp.data(), clen);
         o += n;
     } while (o < s.size());
     deflateEnd(&z);
@@ -1558,7 +1621,7 @@ void Writer::write_raw(const char* p, size_t n, Pool* pool) {
         if (std::fwrite(p, 1, n, fp_) != n) throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
         return;
     }
-    const size_t blk = (size_t)4 << 20;  // (one gzip member per block; the decompressed bytes are the text)
+    const size_t blk = (size_t)1 << 20;  // (one task of BGZF members per block on the pool)
     std::vector<std::string> blocks;
     for (size_t o = 0; o < n; o += blk) blocks.emplace_back(p + o, std::min(blk, n - o));
     write(blocks, pool);
