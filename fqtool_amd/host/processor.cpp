@@ -1908,6 +1908,11 @@ struct Lane {
                     if (fq_engine_raw_wait(e, &r) != FQ_OK)
                         throw std::runtime_error(std::string("fq_engine_raw_wait: ") + fq_engine_last_error(e));
                     raw_idx_wait_s += since(x0);
+                    // the window's index is back, so its copy to the device is done: the staging
+                    // window goes back to the reader now, not when the pack completes (the device
+                    // works from its own copy; the carry moves on the device)
+                    if (w.stage >= 0) R.free_stages.push(w.stage);
+                    enq.front().stage = -1;
                     if (spare.try_pop_recent(pk) < 0) throw Stopped();
                 }
                 auto give_back = [&] {
@@ -1964,7 +1969,7 @@ struct Lane {
                 pk->text_mode = true;
                 pk->paired = R.mates == 2;
                 pk->seq_no = w.id;
-                pk->stage = w.stage;
+                pk->stage = -1;  // (released after fq_engine_raw_wait)
                 for (int m = 0; m < 2; ++m) {  // (output text, then the adapter entries)
                     size_t cap = m < R.mates ? (size_t)(w.n[m] + 4 * (uint64_t)target + 64) : 0;
                     if (merge && m == 0)  // (-m: the merged stream of both mates' text)
@@ -1975,7 +1980,6 @@ struct Lane {
                 }
                 const auto e0 = std::chrono::steady_clock::now();
                 if (fq_engine_raw_launch(e, &r, &pk->rout, w.id) != FQ_OK) {  // (r as fq_engine_raw_wait gave it)
-                    R.free_stages.push(w.stage);
                     throw std::runtime_error(std::string("fq_engine_raw_launch: ") + fq_engine_last_error(e));
                 }
                 submit_s += since(e0);
@@ -2304,16 +2308,16 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
                 RawResumeInfo ri;
                 R.end_locked(ri, "inputs are not regular files");
             } else {
-                // staging: per engine the packs in flight (4), the windows enqueued (3) and queued
-                // for it (2), plus a few for the reader to run ahead (a stage comes back only when its
-                // pack completes: fewer starve the reader); the first is handed out at once, the
-                // others page-locked on a helper thread.  Engines sharing a GPU share its link, so
-                // beyond the first engine of a GPU three more stages each (page-locked memory is
-                // paid again at the exit, ~40 ms per GiB)
+                // staging: per GPU the windows enqueued (3, until their index is back: the copy is
+                // then done and the stage returns, Lane::run_raw_multi) and queued for it (2), plus a
+                // few for the reader to run ahead; the first is handed out at once, the others
+                // page-locked on a helper thread.  Engines sharing a GPU share its link, so beyond
+                // the first engine of a GPU two more stages each (page-locked memory is paid again at
+                // the exit, ~40 ms per GiB)
                 std::vector<int> devs(devices.begin(), devices.end());
                 std::sort(devs.begin(), devs.end());
                 const int P = (int)(std::unique(devs.begin(), devs.end()) - devs.begin());
-                const int kStages = P * 9 + 4 + 3 * (G - P);
+                const int kStages = std::getenv("FQ_MULTI_STAGES") ? std::atoi(std::getenv("FQ_MULTI_STAGES")) : P * 5 + 4 + 2 * (G - P);
                 for (int i = 0; i < kStages; ++i) R.stages.emplace_back(new RawStage);
                 R.free_stages.push(0);
                 rm_warmer = std::thread([&R, kStages] {
