@@ -38,7 +38,8 @@ CXX        ?= g++
 HOSTFLAGS  ?= -std=c++17 -O2 -fPIC -Wall -Wextra -pthread
 HOSTDIR    := fqtool_amd/host
 HOST_SRCS  := $(HOSTDIR)/json.cpp $(HOSTDIR)/options.cpp $(HOSTDIR)/fastq.cpp $(HOSTDIR)/evaluator.cpp \
-              $(HOSTDIR)/report.cpp $(HOSTDIR)/html.cpp $(HOSTDIR)/processor.cpp $(HOSTDIR)/capi.cpp
+              $(HOSTDIR)/report.cpp $(HOSTDIR)/html.cpp $(HOSTDIR)/processor.cpp $(HOSTDIR)/capi.cpp \
+              $(HOSTDIR)/pargz.cpp
 HOST_OBJS  := $(patsubst $(HOSTDIR)/%.cpp,$(OBJDIR)/host_%.o,$(HOST_SRCS))
 HOST_HDRS  := $(wildcard $(HOSTDIR)/*.h) $(HOSTDIR)/known_adapters.inc include/fqengine.h
 BINDIR     := fqtool_amd/bin

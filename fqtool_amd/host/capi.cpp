@@ -10,6 +10,7 @@
 #include "evaluator.h"
 #include "json.h"
 #include "options.h"
+#include "pargz.h"
 #include "processor.h"
 #include "report.h"
 #include "../../include/fqhost.h"
@@ -209,6 +210,43 @@ char* fqh_session_finish(fqh_session* s) {
 }
 
 void fqh_session_close(fqh_session* s) { delete s; }
+
+int fqh_pargz_read_all(const char* path, size_t call, int threads, size_t chunk, char** out, size_t* n, int* ok) {
+    try {
+        std::string s, how;
+        bool good = true;
+        if (!pargz_read_all(path, call, threads, chunk, s, good, how)) return 0;
+        *out = static_cast<char*>(std::malloc(s.size() + 1));
+        std::memcpy(*out, s.data(), s.size());
+        *n = s.size();
+        *ok = good ? 1 : 0;
+        return how == "parallel" ? 1 : 2;
+    } catch (...) {
+        return -1;
+    }
+}
+
+int fqh_gzread_all(const char* path, size_t call, char** out, size_t* n, int* ok) {
+    gzFile g = gzopen(path, "r");  // (zlib's default buffer, as the reference's FqReader)
+    if (!g) return -1;
+    std::string s;
+    std::vector<char> b(call);
+    *ok = 1;
+    for (;;) {  // as the reference's FqReader: a call that fails loses its bytes, a short one ends
+        const int r = gzread(g, b.data(), (unsigned)call);
+        if (r < 0) {
+            *ok = 0;
+            break;
+        }
+        s.append(b.data(), (size_t)r);
+        if ((size_t)r < call) break;
+    }
+    gzclose(g);
+    *out = static_cast<char*>(std::malloc(s.size() + 1));
+    std::memcpy(*out, s.data(), s.size());
+    *n = s.size();
+    return 0;
+}
 
 char* fqh_debug_records(const char* path, int bulk, int buf_size, int pack_n, int phred64) {
     std::string out;

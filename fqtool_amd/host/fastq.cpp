@@ -1,5 +1,6 @@
 // fastq.cpp -- see fastq.h.
 #include "fastq.h"
+#include "pargz.h"
 
 #include <algorithm>
 #include <climits>
@@ -12,6 +13,7 @@
 #include <emmintrin.h>
 #include <dlfcn.h>
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <thread>
@@ -722,6 +724,16 @@ FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     : phred64_(phred64), bsize_((uint64_t)buf_size) {
     if (ends_with(path, ".gz")) {
         if ((bgzf_ = BgzfSource::open(path, (size_t)bsize_))) return;
+        // a single-stream gzip file: chunks inflated on half the host threads the process may use
+        // (the two mates of a pair inflate side by side)
+        {
+            int n = (int)std::thread::hardware_concurrency();
+            cpu_set_t cs;
+            if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+            if (const char* omp = std::getenv("OMP_NUM_THREADS"))
+                if (std::atoi(omp) > 0) n = std::min(n, std::atoi(omp));
+            if ((pargz_ = ParGzSource::open(path, (size_t)bsize_, std::max(2, n / 2)))) return;
+        }
         path_ = path;
         // inflated whole on a thread of its own (so the mates of a pair inflate side by side), then
         // parsed like a mapped plain file; zlib's stream reader if that fails (settle())
@@ -763,8 +775,7 @@ void FqBulkReader::settle() {
     }
     gz_ = gzopen(path_.c_str(), "r");
     if (!gz_) throw std::runtime_error("Failed to open file: " + path_);
-    gzbuffer(gz_, 1 << 20);
-    gzrewind(gz_);
+    gzrewind(gz_);  // (zlib's default buffer, as the reference: see FqReader)
     gz_ahead_.reset(new GzAhead(gz_, (size_t)bsize_));
 }
 
@@ -781,6 +792,7 @@ FqBulkReader::~FqBulkReader() {
 
 void FqBulkReader::begin(ByteBuf& text) {
     settle();
+    calls_ = 0;
     if (map_) {  // the mapping is the arena: offsets are file offsets, nothing is carried
         text.clear();
         text_ = nullptr;
@@ -818,10 +830,14 @@ void FqBulkReader::read_more() {
     size_t want = (size_t)(want_end - total_);
     char* dst = text_->extend(want);
     size_t got = 0;
+    // (a failed source is reported when the parser first needs a byte past what it handed out --
+    // where the reference's failing gzread call is made -- not here, ahead of the parser)
     if (bgzf_) {
-        if (!bgzf_->read(dst, want, got)) reader_stderr("Error to read gzip file\n");
+        if (!bgzf_->read(dst, want, got)) src_failed_ = true;
+    } else if (pargz_) {
+        if (!pargz_->read(dst, want, got)) src_failed_ = true;
     } else if (gz_ahead_) {
-        if (!gz_ahead_->read(dst, want, got)) reader_stderr("Error to read gzip file\n");
+        if (!gz_ahead_->read(dst, want, got)) src_failed_ = true;
     } else {
         got = std::fread(dst, 1, want, fp_);
     }
@@ -896,6 +912,7 @@ bool FqBulkReader::line(size_t x, size_t& e, size_t& next) {
             continue;
         }
         if (eof_) {  // the last line has no terminator, or we are past the end: empty lines
+            demand_past_end();
             e = std::max(x, n);
             next = e + 1;
             return true;
@@ -906,7 +923,11 @@ bool FqBulkReader::line(size_t x, size_t& e, size_t& next) {
 
 bool FqBulkReader::read(Rec& r) {  // FqReader::read, src/fqreader.cpp:160-195
     err_.clear();
-    if (at_end(pos_)) return false;
+    ++calls_;
+    if (at_end(pos_)) {  // (the reference's gzeof is still false here after a failed read: it reads)
+        demand_past_end();
+        return false;
+    }
     size_t x = pos_, e = 0, nx = 0;
     line(x, e, nx);
     for (;;) {  // skip to a line that starts with '@' (src/fqreader.cpp:169-171)
@@ -1089,7 +1110,24 @@ size_t FqBulkReader::read_fast(std::vector<Rec>& out, size_t max_n, Pool* pool) 
     pos_ = x;
     tbase_ = pos_ >> 6;  // read() indexes afresh from here
     indexed_ = tbase_ << 6;
+    calls_ += got;
     return got;
+}
+
+// The parser needs a byte past the end of what the source handed out: where the reference makes
+// its failing gzread call (src/fqreader.cpp:28-33), if the source failed.  Noted once, with the
+// index (in this arena) of the record being read; PackReader prints it in the reference's order.
+void FqBulkReader::demand_past_end() {
+    if (src_failed_ && !src_reported_) {
+        src_reported_ = true;
+        src_hit_ = (int64_t)calls_ - 1;
+    }
+}
+
+int64_t FqBulkReader::take_source_error() {
+    const int64_t h = src_hit_;
+    src_hit_ = -1;
+    return h;
 }
 
 // ---- Pool ----
@@ -1376,8 +1414,10 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
     pk.clear();
     pk.paired = paired_;
     size_t n = 0;
+    static const char* kGzErr = "Error to read gzip file\n";  // FqReader::readToBuf, src/fqreader.cpp:31-33
     if (!paired_) {
         n = read_mate(r1_, pk, 0, max_n, pool);
+        if (r1_.take_source_error() >= 0) reader_stderr(kGzErr);
         if (n < max_n) {
             done_ = true;
             if (!r1_.error().empty()) reader_stderr(r1_.error());
@@ -1388,11 +1428,12 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
         while (n < max_n) {
             // FqReaderPair::read (src/fqreader.cpp:254-267) reads mate 2 even when mate 1 failed
             const bool ok_a = r1_.read(a);
-            const std::string err_a = ok_a ? std::string() : r1_.error();
+            if (r1_.take_source_error() >= 0) reader_stderr(kGzErr);
+            if (!ok_a) reader_stderr(r1_.error());
             const bool ok_b = r1_.read(b);
+            if (r1_.take_source_error() >= 0) reader_stderr(kGzErr);
             if (!ok_a || !ok_b) {
                 done_ = true;
-                reader_stderr(err_a);
                 if (!ok_b) reader_stderr(r1_.error());
                 break;
             }
@@ -1411,11 +1452,27 @@ bool PackReader::next(Pack& pk, size_t max_n, Pool* pool) {
         const size_t n1 = read_mate(r1_, pk, 0, max_n, pool);
         t.join();
         n = std::min(n1, n2);
+        // the messages in the reference's order: by pair index, mate 1 first, a gzip read error
+        // before the same read's parse error; a mate's gzip error only if the reference got there
+        struct Msg {
+            size_t at;
+            int mate, kind;
+            const std::string* s;
+        };
+        static const std::string gz(kGzErr);
+        std::vector<Msg> msgs;
+        const int64_t h1 = r1_.take_source_error(), h2 = r2_->take_source_error();
+        if (h1 >= 0 && (size_t)h1 <= n) msgs.push_back({(size_t)h1, 0, 0, &gz});
+        if (h2 >= 0 && (size_t)h2 <= n) msgs.push_back({(size_t)h2, 1, 0, &gz});
         if (n < max_n) {
             done_ = true;
-            if (n1 <= n2) reader_stderr(r1_.error());
-            if (n2 <= n1) reader_stderr(r2_->error());
+            if (n1 <= n2) msgs.push_back({n, 0, 1, &r1_.error()});
+            if (n2 <= n1) msgs.push_back({n, 1, 1, &r2_->error()});
         }
+        std::sort(msgs.begin(), msgs.end(), [](const Msg& a, const Msg& b) {
+            return a.at != b.at ? a.at < b.at : a.mate != b.mate ? a.mate < b.mate : a.kind < b.kind;
+        });
+        for (const Msg& m : msgs) reader_stderr(*m.s);
         pk.rec[0].resize(n);
         pk.rec[1].resize(n);
     }

@@ -110,13 +110,16 @@ struct Rec {
 };
 
 class BgzfSource;
+class ParGzSource;
 
 class FqReader {
    public:
     // buf_size: the reference's read buffer (1 MiB, src/fqreader.cpp:10); smaller only in tests
-    // zlib_default_buffer: keep zlib's own input buffer size as the reference's reader does (only
-    // stream_pos() can tell the difference)
-    FqReader(const std::string& path, bool phred64, int buf_size = 1 << 20, bool zlib_default_buffer = false);
+    // zlib_default_buffer: keep zlib's own buffer size as the reference's reader does (the default):
+    // a 1 MiB gzread then inflates straight into the caller's buffer, so a data or CRC error fails the
+    // call whose bytes it lies in; with gzbuffer(1 MiB) zlib inflates 2 MiB ahead, and an error ends
+    // the stream up to a call earlier (stream_pos() differs too)
+    FqReader(const std::string& path, bool phred64, int buf_size = 1 << 20, bool zlib_default_buffer = true);
     ~FqReader();
     // FqReader::getBytes' bytesRead (src/fqreader.cpp:64-75): gzoffset / ftell of the stream
     uint64_t stream_pos() const;
@@ -174,6 +177,9 @@ class FqBulkReader {
     // the records' offsets refer to (the arena, or the file mapping)
     const char* end();
     const std::string& error() const { return err_; }
+    // the index (read calls since begin()) at which the parser first needed bytes past a failed
+    // gzip source -- the reference's "Error to read gzip file" -- or -1; cleared by the call
+    int64_t take_source_error();
     bool mapped() {
         settle();
         return map_ != nullptr;
@@ -189,6 +195,7 @@ class FqBulkReader {
     size_t sz() const { return map_ ? map_size_ : text_->size(); }
     bool skip_ok(uint64_t g) const;
     void read_more();
+    void demand_past_end();
     void settle();  // a whole-file inflate started by the constructor: wait for it, or fall back
     struct Whole {
         bool ok = false;
@@ -199,11 +206,15 @@ class FqBulkReader {
     std::string path_;
     gzFile gz_ = nullptr;
     std::unique_ptr<BgzfSource> bgzf_;  // BGZF input: members inflated on several threads
+    std::unique_ptr<ParGzSource> pargz_;  // single-stream gzip: chunks inflated on several threads
     std::unique_ptr<GzAhead> gz_ahead_;  // other gzip: inflated on a thread of its own, ahead of the parser
     FILE* fp_ = nullptr;
     bool phred64_;
     uint64_t bsize_;
     bool eof_ = false;
+    bool src_failed_ = false, src_reported_ = false;  // the gzip source failed / the parser got there
+    int64_t src_hit_ = -1;
+    size_t calls_ = 0;    // records read since begin() (read() calls, read_fast records)
     uint64_t total_ = 0;  // stream bytes read so far (the stream's size once eof_)
     ByteBuf* text_ = nullptr;
     uint64_t base_ = 0;   // stream offset of (*text_)[0]

@@ -81,6 +81,15 @@ void fqh_set_kmer_backend(const fqh_kmer_backend* b);
  * then the reader's error text, if any (fqh_free). */
 char* fqh_debug_records(const char* path, int bulk, int buf_size, int pack_n, int phred64);
 
+/* The decompressed stream of gzip file `path` as the tool's parallel single-stream inflater hands
+ * it out (chunks of `chunk` compressed bytes, 0 = default; `threads` decoding threads), and as zlib's
+ * gzread gives it in calls of `call` bytes (the reference's reader).  *out: malloc'd bytes (fqh_free),
+ * *ok: 0 when the stream ended on corrupt data.  fqh_pargz_read_all returns 1 for the parallel
+ * path, 2 when it handed the stream to zlib's reader (an anomaly or several members), 0 when it does
+ * not apply (small file, not gzip), -1 on error; fqh_gzread_all returns 0, -1 on error. */
+int fqh_pargz_read_all(const char* path, size_t call, int threads, size_t chunk, char** out, size_t* n, int* ok);
+int fqh_gzread_all(const char* path, size_t call, char** out, size_t* n, int* ok);
+
 #ifdef __cplusplus
 }
 #endif
