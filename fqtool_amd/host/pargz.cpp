@@ -8,6 +8,7 @@
 #include "pargz.h"
 
 #include <dlfcn.h>
+#include <emmintrin.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -440,9 +441,19 @@ struct Decoder {
                 uint32_t acc = 0;
                 if (dist <= sz) {  // within the chunk's own output
                     const T* src = dst - dist;
-                    if (dist >= 8) {
-                        for (uint32_t i = 0; i < len; i += 8) std::memcpy(dst + i, src + i, 8 * sizeof(T));
-                        for (uint32_t i = 0; i < len; ++i) acc |= dst[i];
+                    if (dist >= 8) {  // 8 symbols a step, OR-ed as they go (the steps past len may
+                                      // flag a marker that is not there: the scan below finds none)
+                        __m128i a = _mm_setzero_si128();
+                        for (uint32_t i = 0; i < len; i += 8) {
+                            const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+                            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), x);
+                            a = _mm_or_si128(a, x);
+                        }
+                        acc = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_srli_epi16(a, 8), _mm_setzero_si128())) != 0xffffu ? 256u : 0u;
+                    } else if (dist == 1) {
+                        const T x = src[0];
+                        for (uint32_t i = 0; i < len; ++i) dst[i] = x;
+                        acc = x;
                     } else {
                         for (uint32_t i = 0; i < len; ++i) acc |= (dst[i] = src[i]);
                     }
@@ -453,12 +464,10 @@ struct Decoder {
                     }
                     acc = 256;
                 }
-                if (acc >= 256)  // (a value >= 256 is a marker: the OR of the copy has a bit >= 8)
-                    for (uint32_t i = len; i-- > 0;)
-                        if (dst[i] >= 256) {
-                            last_marker = std::max(last_marker, sz + i + 1);
-                            break;
-                        }
+                // (a value >= 256 is a marker: the OR of the copy has a bit >= 8.  The copy's end
+                // stands for its last marker -- at most 258 symbols late, which only delays the
+                // switch to bytes by as much)
+                if (acc >= 256) last_marker = sz + len;
             }
             sz += len;
         }
@@ -556,13 +565,37 @@ struct ParGzSource::Impl {
     std::vector<char> fb_buf;
     size_t fb_off = 0;
 
-    std::atomic<uint64_t> n_redecode{0}, n_nostart{0}, n_beyond{0}, find_ns{0}, cand_tried{0}, dec_ns{0}, res_ns{0}, sym16_n{0};
+    // output buffers go back to a pool when a chunk is done with them: the next chunk writes into
+    // pages already mapped (fresh tens of MiB per chunk cost more in page faults than the decode)
+    std::mutex pool_m;
+    std::vector<PodBuf<uint8_t>> pool8;
+    std::vector<PodBuf<uint16_t>> pool16;
+    template <class T>
+    std::vector<PodBuf<T>>& pool_of();
+    template <class T>
+    void take(PodBuf<T>& b) {
+        std::lock_guard<std::mutex> g(pool_m);
+        auto& pl = pool_of<T>();
+        if (b.cap || pl.empty()) return;
+        b = std::move(pl.back());
+        pl.pop_back();
+        b.n = 0;
+    }
+    template <class T>
+    void give(PodBuf<T>& b) {
+        if (!b.cap) return;
+        b.n = 0;
+        std::lock_guard<std::mutex> g(pool_m);
+        pool_of<T>().push_back(std::move(b));
+    }
+
+    std::atomic<uint64_t> n_redecode{0}, n_nostart{0}, n_beyond{0}, find_ns{0}, cand_tried{0}, dec_ns{0}, res_ns{0}, sym16_n{0}, crc_ns{0}, wait_ns{0};
     ~Impl() {
         if (std::getenv("FQ_PARGZ_DEBUG"))
-            fprintf(stderr, "pargz: %zu chunks, %llu without a start, %llu decoded again, %llu beyond the end, %llu candidates tried, find %.3f s, decode %.3f s, resolve %.3f s, %llu symbols with markers\n",
+            fprintf(stderr, "pargz: %zu chunks, %llu without a start, %llu decoded again, %llu beyond the end, %llu candidates tried, find %.3f s, decode %.3f s, resolve %.3f s (waiting %.3f s, crc %.3f s), %llu symbols with markers\n",
                     ch.size(), (unsigned long long)n_nostart.load(), (unsigned long long)n_redecode.load(),
                     (unsigned long long)n_beyond.load(), (unsigned long long)cand_tried.load(), find_ns.load() * 1e-9,
-                    dec_ns.load() * 1e-9, res_ns.load() * 1e-9, (unsigned long long)sym16_n.load());
+                    dec_ns.load() * 1e-9, res_ns.load() * 1e-9, wait_ns.load() * 1e-9, crc_ns.load() * 1e-9, (unsigned long long)sym16_n.load());
         {
             std::lock_guard<std::mutex> g(m);
             stop = true;
@@ -604,6 +637,7 @@ struct ParGzSource::Impl {
             br.seek(map, size, b);
             if (stop) return false;
             ++cand_tried;
+            take(c.o16.s);
             c.o16.s.n = 0;
             c.o16.last_marker = 0;
             const Status st = dec.block(br, c.o16);
@@ -633,6 +667,7 @@ struct ParGzSource::Impl {
             if (sym16 && c.o16.s.n >= kWin && c.o16.s.n - c.o16.last_marker >= kWin) {
                 // no marker can appear any more: the rest as bytes, the last 32 KiB as history
                 const size_t k = c.o16.s.n;
+                take(c.o8.b);
                 c.o8.b.reserve(kWin);
                 for (size_t i = 0; i < kWin; ++i) c.o8.b.p[i] = (uint8_t)c.o16.s.p[k - kWin + i];
                 c.o8.b.n = kWin;
@@ -667,6 +702,7 @@ struct ParGzSource::Impl {
             if (i == 0) {  // the member's start: bytes, no history
                 br.seek(map, size, (uint64_t)data0 * 8);
                 c.start = (int64_t)data0 * 8;
+                take(c.o8.b);
                 decode_from(c, br, dec, false);
             } else {
                 const auto f0 = std::chrono::steady_clock::now();
@@ -699,8 +735,10 @@ struct ParGzSource::Impl {
         Chunk& c = ch[i];
         const Chunk* pv = nullptr;
         if (i > 0) {
+            const auto q0 = std::chrono::steady_clock::now();
             std::unique_lock<std::mutex> lk(m);
             cv.wait(lk, [&] { return stop || ch[i - 1].windowed; });
+            wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - q0).count();
             if (stop) return;
             pv = &ch[i - 1];
         }
@@ -711,8 +749,11 @@ struct ParGzSource::Impl {
         } else if (pv && !(c.start >= 0 && (uint64_t)c.start == pv->end)) {
             ++n_redecode;
             // a false start, or none: this chunk decoded again from the previous one's end
+            give(c.o16.s);
             c.o16 = Out16();
+            give(c.o8.b);
             c.o8 = Out8();
+            take(c.o8.b);
             c.o8.b.assign(pv->window.data(), pv->window.size());
             c.o8.win = pv->window.size();
             c.start = (int64_t)pv->end;
@@ -727,26 +768,63 @@ struct ParGzSource::Impl {
             const std::vector<uint8_t>* w = pv ? &pv->window : nullptr;
             const size_t wn = w ? w->size() : 0;
             const size_t ns = c.o16.s.n;
+            take(c.pre);
             c.pre.reserve(ns);
             c.pre.n = ns;
             const uint16_t* src = c.o16.s.p;
             uint8_t* dst = c.pre.p;
-            for (size_t k = 0; k < ns; ++k) {
+            auto one = [&](size_t k) {
                 const uint16_t x = src[k];
                 if (x < 256) {
                     dst[k] = (uint8_t)x;
-                } else {
-                    const size_t wi = (size_t)x - 256;  // index into the 32 KiB before the chunk
-                    if (wi + wn < kWin) {  // before the stream's start: zlib's "too far back"
-                        bad = true;
-                        c.pre.n = k;
-                        break;
-                    }
-                    dst[k] = (*w)[wi + wn - kWin];
+                    return true;
                 }
-            }
-            c.o16.s.release();
+                const size_t wi = (size_t)x - 256;  // index into the 32 KiB before the chunk
+                if (wi + wn < kWin) return false;   // before the stream's start: zlib's "too far back"
+                dst[k] = (*w)[wi + wn - kWin];
+                return true;
+            };
+            const __m128i z = _mm_setzero_si128();
+            auto range = [&](size_t k, size_t e) {  // symbols [k, e); false at a marker before the stream
+                for (; k + 8 <= e; k += 8) {  // 8 symbols a step; the ones with a marker one by one
+                    const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + k));
+                    if (_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_srli_epi16(x, 8), z)) == 0xffff) {
+                        _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + k), _mm_packus_epi16(x, x));
+                        continue;
+                    }
+                    for (size_t j = k; j < k + 8; ++j)
+                        if (!one(j)) {
+                            c.pre.n = j;
+                            return false;
+                        }
+                }
+                for (; k < e; ++k)
+                    if (!one(k)) {
+                        c.pre.n = k;
+                        return false;
+                    }
+                return true;
+            };
             const size_t n8 = c.o8.b.n - c.o8.win;
+            // with a full previous window no marker can point before the stream: only the symbols
+            // the window needs are resolved before it is published (the next chunk waits for it),
+            // the rest after -- so the chunks' resolutions run side by side, not one after another
+            const bool early = wn < kWin;
+            size_t t0 = 0;
+            std::vector<uint8_t> lut;
+            auto fast = [&](size_t k, size_t e) {  // a full window: every symbol is lut[symbol]
+                const uint8_t* __restrict t = lut.data();
+                for (; k < e; ++k) dst[k] = t[src[k]];
+            };
+            if (early) {
+                bad = !range(0, ns);
+            } else {
+                lut.resize(256 + kWin);
+                for (uint32_t x = 0; x < 256; ++x) lut[x] = (uint8_t)x;
+                std::memcpy(lut.data() + 256, w->data(), kWin);
+                t0 = ns - std::min(ns, kWin - std::min<size_t>(n8, kWin));
+                fast(t0, ns);
+            }
             c.bytes = c.pre.n + n8;
             // window: the last 32 KiB of the stream through this chunk
             std::vector<uint8_t> win;
@@ -759,18 +837,28 @@ struct ParGzSource::Impl {
             win.insert(win.end(), c.o8.b.p + c.o8.b.n - tail8, c.o8.b.p + c.o8.b.n);
             c.window.swap(win);
             if (bad) c.error = true;
+            {
+                std::lock_guard<std::mutex> g(m);
+                c.windowed = true;
+            }
+            cv.notify_all();
+            if (!early) fast(0, t0);
+            give(c.o16.s);
+        } else {
+            {
+                std::lock_guard<std::mutex> g(m);
+                c.windowed = true;
+            }
+            cv.notify_all();
         }
-        {
-            std::lock_guard<std::mutex> g(m);
-            c.windowed = true;
-        }
-        cv.notify_all();
+        const auto r1 = std::chrono::steady_clock::now();
         if (!c.beyond) {
             uint32_t x = crc_of(c.pre.p, c.pre.n);
             const size_t n8 = c.o8.b.n - c.o8.win;
             if (n8) x = (uint32_t)crc32_combine(x, crc_of(c.o8.b.p + c.o8.win, n8), (z_off_t)n8);
             c.crc = x;
         }
+        crc_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - r1).count();
         {
             std::lock_guard<std::mutex> g(m);
             c.ready = true;
@@ -896,8 +984,8 @@ struct ParGzSource::Impl {
             Chunk& c = ch[cur];
             const size_t n8 = c.o8.b.n - c.o8.win;
             if (cur_pos >= c.bytes) {  // done with it: free it, let a worker take another
-                c.pre.release();
-                c.o8.b.release();
+                give(c.pre);
+                give(c.o8.b);
                 ++cur;
                 cur_pos = 0;
                 consumed = cur;
@@ -921,6 +1009,15 @@ struct ParGzSource::Impl {
     }
     size_t next_good = 0;
 };
+
+template <>
+std::vector<PodBuf<uint8_t>>& ParGzSource::Impl::pool_of<uint8_t>() {
+    return pool8;
+}
+template <>
+std::vector<PodBuf<uint16_t>>& ParGzSource::Impl::pool_of<uint16_t>() {
+    return pool16;
+}
 
 std::unique_ptr<ParGzSource> ParGzSource::open(const std::string& path, size_t call, int threads) {
     return open_chunked(path, call, threads, 0);
