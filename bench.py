@@ -60,7 +60,7 @@ def pmc_traffic(cfg, pairs):
     return int(d["traffic_bytes"]), os.path.relpath(paths[-1], REPO)
 
 
-def e2e_path(tool_log):
+def e2e_path(tool_log, gz_input=False):
     """What the e2e run did, from the tool's own log lines: the raw stream (GPU record indexing and
     output text), text packs (host parse, device planes and text) or host packs."""
     text = " ".join(tool_log or [])
@@ -70,7 +70,8 @@ def e2e_path(tool_log):
         mid = "host parse -> text packs -> device planes -> kernels -> GPU output text"
     else:
         mid = "host parse -> pinned tile packs -> kernels -> records -> host formatting"
-    return f"fqtool binary: FASTQ (page cache) -> {mid} -> /dev/null + JSON"
+    src = "gzip FASTQ (page cache) -> chunks inflated on several threads" if gz_input else "FASTQ (page cache)"
+    return f"fqtool binary: {src} -> {mid} -> /dev/null + JSON"
 
 
 def sq_profile(cfg, pairs):
@@ -185,6 +186,48 @@ def write_fastq_fast(planes, n, first_index, d, tag=""):
     return paths
 
 
+def gzip_single_member(src, dst, nbytes=None, level=6, threads=None, piece=64 << 20):
+    """The first `nbytes` of `src` (all of it by default) as ONE gzip member (one deflate stream,
+    not BGZF), compressed at `level` by zlib on `threads` threads as pigz does: each 64 MiB piece is
+    deflated with the previous piece's last 32 KiB as its dictionary (so matches reach back across
+    pieces as in one `gzip -6` stream) and ends in a full flush (an empty stored block), so the
+    pieces join into a single stream; CRC32 and ISIZE of the whole.  Made in seconds instead of
+    minutes."""
+    import concurrent.futures as cf
+    import struct
+    import zlib
+
+    total = os.path.getsize(src) if nbytes is None else nbytes
+    threads = threads or host_cores()
+
+    def deflate(args):
+        data, last, dictionary = args
+        if dictionary:
+            c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, zlib.Z_DEFAULT_STRATEGY, dictionary)
+        else:
+            c = zlib.compressobj(level, zlib.DEFLATED, -15, 8)
+        return c.compress(data) + c.flush(zlib.Z_FINISH if last else zlib.Z_FULL_FLUSH)
+
+    crc = 0
+    with open(src, "rb") as f, open(dst, "wb") as g, cf.ThreadPoolExecutor(threads) as ex:
+        g.write(b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\x03")
+        pending = []
+        done = 0
+        tail = b""
+        while done < total or pending:
+            while done < total and len(pending) < 2 * threads:  # (bounded: 2 pieces a thread in flight)
+                data = f.read(min(piece, total - done))
+                if not data:
+                    raise ValueError(f"{src}: shorter than {total} bytes")
+                done += len(data)
+                crc = zlib.crc32(data, crc)
+                pending.append(ex.submit(deflate, (data, done >= total, tail)))
+                tail = data[-32768:]
+            g.write(pending.pop(0).result())
+        g.write(struct.pack("<II", crc & 0xFFFFFFFF, total & 0xFFFFFFFF))
+    return dst
+
+
 def host_cores():
     """Host cores this process may use (the GPU box's share is 16 per GPU)."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
@@ -226,6 +269,7 @@ def port_baseline(abi, pairs, first, threads):
 
 
 E2E_PAUSE_S = 2.0  # between e2e runs (host_legs)
+GZ_IN_PAIRS = 10_000_000  # pairs of the gzip-input e2e leg
 
 
 def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
@@ -236,6 +280,7 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
       cpu_baseline -- the reference binary (oracle/_ref/fqtool_ref, -w <= 16) on the first
                       `cpu_pairs` pairs (or, without it, the C restatement single-threaded)."""
     n = max(cpu_pairs, e2e_pairs)
+    gz_pairs = min(GZ_IN_PAIRS, e2e_pairs)
     tmp = tempfile.mkdtemp(prefix="fqbench_")
     rec_bytes = 2 * (40 + 2 * READ_LEN + 5)
     free = shutil.disk_usage(tmp).free
@@ -313,7 +358,7 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
                  "fastq_GB_s": round(gb / dt, 3), "wall_s": round(dt, 3), "workers": workers,
                  "runs_wall_s": [round(r[0], 3) for r in runs], "pause_between_runs_s": E2E_PAUSE_S,
                  "options": " ".join(extra), "outputs": outputs, "affinity_cpus": host_cores(),
-                 "path": e2e_path(tool_log),
+                 "path": e2e_path(tool_log, gz_input=inp[0].endswith(".gz")),
                  "tool_log": tool_log[-1].split("] ", 1)[-1] if tool_log else None}
             if outputs != "null":
                 r["output_GB"] = round(out_bytes / 1e9, 3)
@@ -323,6 +368,19 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             out["e2e"] = e2e(opts)
             # BASELINE config 4 (-m): every pair's output is the merged stream (to /dev/null)
             out["e2e_c4"] = e2e(["-q", "-a", "-g", "--enable_cut_right", "-m", "--merge_output", "/dev/null"])
+            # gzip inputs: the first GZ_IN_PAIRS pairs as single-member gzip -6 files (one deflate
+            # stream each, as gzip writes -- not BGZF), inflated by the tool on several threads
+            if os.environ.get("FQ_BENCH_GZ_IN", "1") != "0" and gz_pairs:
+                t0 = time.perf_counter()
+                gzin = [gzip_single_member(p_, p_ + ".gz", nbytes=os.path.getsize(p_) // e2e_pairs * gz_pairs)
+                        for p_ in big]
+                gz_gb = sum(os.path.getsize(p_) for p_ in gzin) / 1e9
+                log(f"gzip -6 inputs made in {time.perf_counter() - t0:.1f}s ({gz_pairs} pairs, {gz_gb:.2f} GB)")
+                out["e2e_gzin"] = e2e(opts, inp=gzin, pairs=gz_pairs)
+                out["e2e_gzin"]["input"] = (f"{gz_pairs} pairs as two single-member gzip -6 files ({gz_gb:.2f} GB "
+                                            f"compressed; 64 MiB pieces joined by full flushes)")
+                for p_ in gzin:
+                    os.remove(p_)
             # the writers timed: the same C3 run with plain FASTQ output files (page cache), and
             # BGZF .gz outputs (-z 4, the reference's default level) on the CPU-baseline sample
             if os.environ.get("FQ_BENCH_FILE_LEGS", "1") != "0" and file_legs:
@@ -341,6 +399,18 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
                 "sample": f"{cpu_pairs} pairs ({2 * cpu_pairs} reads) of the same synthetic workload as FASTQ in the "
                           f"page cache, oracle/_ref/fqtool_ref -w {w} (+1 reader, 2 writer threads), wall {dt:.2f}s "
                           f"incl. its adapter-detection pre-pass"}
+            # the reference on the same sample as single-member gzip -6 inputs (zlib's gzread, one
+            # thread per file): the baseline of the e2e_gzin leg
+            if os.environ.get("FQ_BENCH_GZ_IN", "1") != "0":
+                sgz = [gzip_single_member(p_, p_ + ".gz") for p_ in small]
+                cmd = [ref, "-i", sgz[0], "-I", sgz[1], "-o", "/dev/null", "-O", "/dev/null", *opts, "-w", str(w),
+                       "-J", os.path.join(tmp, "r.json"), "-H", os.path.join(tmp, "r.html")]
+                t0 = time.perf_counter()
+                subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+                dt = time.perf_counter() - t0
+                out["cpu_baseline"]["gzin"] = {
+                    "value": round(2 * cpu_pairs / dt / 1e6, 4), "unit": "Mreads/s", "wall_s": round(dt, 3),
+                    "sample": f"the same {cpu_pairs} pairs as single-member gzip -6 files, oracle/_ref/fqtool_ref -w {w}"}
             # the same sample through the C restatement's per-read path (no parse/format) on one
             # thread per host core of the box's share -- the reference CLI caps -w at 16
             # (src/main.cpp:110); this run has no cap
@@ -783,6 +853,7 @@ def run_rank(args):
         "e2e_c4": None,
         "e2e_file": None,
         "e2e_gz": None,
+        "e2e_gzin": None,
         "acc_sha256": acc_digest,
         "parity_sample": sample,
     }
@@ -794,6 +865,7 @@ def run_rank(args):
         out["e2e_c4"] = legs.get("e2e_c4")
         out["e2e_file"] = legs.get("e2e_file")
         out["e2e_gz"] = legs.get("e2e_gz")
+        out["e2e_gzin"] = legs.get("e2e_gzin")
         log(f"e2e {legs['e2e']}")
         log(f"e2e_c4 {legs.get('e2e_c4')}")
     runner.close()

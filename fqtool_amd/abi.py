@@ -331,5 +331,5 @@ HOST_SYMBOLS = [
     "fqh_report_json", "fqh_free", "fqh_session_open", "fqh_session_error", "fqh_session_params",
     "fqh_session_next", "fqh_session_consume", "fqh_session_add_acc", "fqh_session_finish",
     "fqh_session_close", "fqh_debug_records", "fqh_session_dup_params", "fqh_session_set_dup",
-    "fqh_set_kmer_backend", "fqh_pargz_read_all", "fqh_gzread_all",
+    "fqh_set_kmer_backend", "fqh_pargz_read_all", "fqh_gzread_all", "fqh_gz_drain",
 ]

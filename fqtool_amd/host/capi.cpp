@@ -248,6 +248,43 @@ int fqh_gzread_all(const char* path, size_t call, char** out, size_t* n, int* ok
     return 0;
 }
 
+int fqh_gz_drain(const char* path, size_t call, int threads, size_t chunk, size_t* n, int* ok, double* seconds) {
+    try {
+        std::vector<char> b(call);
+        *n = 0;
+        *ok = 1;
+        const auto t0 = std::chrono::steady_clock::now();
+        int rc = 0;
+        if (threads > 0) {
+            std::unique_ptr<ParGzSource> s = ParGzSource::open_chunked(path, call, threads, chunk);
+            if (!s) return 0;
+            for (;;) {
+                size_t got = 0;
+                const bool r = s->read(b.data(), call, got);
+                *n += got;
+                if (!r) *ok = 0;
+                if (!r || got < call) break;
+            }
+            rc = s->fell_back() ? 2 : 1;
+        } else {
+            gzFile g = gzopen(path, "r");
+            if (!g) return -1;
+            for (;;) {
+                const int r = gzread(g, b.data(), (unsigned)call);
+                if (r < 0) *ok = 0;
+                if (r <= 0) break;
+                *n += (size_t)r;
+                if ((size_t)r < call) break;
+            }
+            gzclose(g);
+        }
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return rc;
+    } catch (...) {
+        return -1;
+    }
+}
+
 char* fqh_debug_records(const char* path, int bulk, int buf_size, int pack_n, int phred64) {
     std::string out;
     auto put = [&](const char* a, size_t la, const char* b, size_t lb, const char* c, size_t lc, const char* d,

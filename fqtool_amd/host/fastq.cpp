@@ -719,21 +719,24 @@ class GzAhead {
     std::thread th_;
 };
 
+// Half the host threads the process may use (its affinity, capped by OMP_NUM_THREADS), at least 2:
+// the two mates of a pair inflate side by side.
+int gz_inflate_threads() {
+    int n = (int)std::thread::hardware_concurrency();
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+    if (const char* omp = std::getenv("OMP_NUM_THREADS"))
+        if (std::atoi(omp) > 0) n = std::min(n, std::atoi(omp));
+    return std::max(2, n / 2);
+}
+
 // ---- FqBulkReader ----
 FqBulkReader::FqBulkReader(const std::string& path, bool phred64, int buf_size)
     : phred64_(phred64), bsize_((uint64_t)buf_size) {
     if (ends_with(path, ".gz")) {
         if ((bgzf_ = BgzfSource::open(path, (size_t)bsize_))) return;
-        // a single-stream gzip file: chunks inflated on half the host threads the process may use
-        // (the two mates of a pair inflate side by side)
-        {
-            int n = (int)std::thread::hardware_concurrency();
-            cpu_set_t cs;
-            if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
-            if (const char* omp = std::getenv("OMP_NUM_THREADS"))
-                if (std::atoi(omp) > 0) n = std::min(n, std::atoi(omp));
-            if ((pargz_ = ParGzSource::open(path, (size_t)bsize_, std::max(2, n / 2)))) return;
-        }
+        // a single-stream gzip file: chunks inflated on several threads
+        if ((pargz_ = ParGzSource::open(path, (size_t)bsize_, gz_inflate_threads()))) return;
         path_ = path;
         // inflated whole on a thread of its own (so the mates of a pair inflate side by side), then
         // parsed like a mapped plain file; zlib's stream reader if that fails (settle())
@@ -843,7 +846,10 @@ void FqBulkReader::read_more() {
     }
     text_->truncate(text_->size() - (want - got));
     total_ += got;
-    if (got < want) eof_ = true;
+    if (got < want) {
+        eof_ = true;
+        pargz_.reset();  // (its workers are done: joined now, its buffers freed)
+    }
 }
 
 // One SSE2 pass over new arena bytes: a bitmap of line terminators (word w of tidx_ covers arena
@@ -1374,7 +1380,24 @@ void pack_tiles(Pack& pk, Pool* pool) {
 
 void FqBulkReader::seek(uint64_t off) {
     settle();
-    if (!map_) throw std::runtime_error("FqBulkReader::seek on an unmapped input");
+    if (!map_) {
+        // a stream read from its start: its bytes up to `off` are read (in the usual buffer-aligned
+        // steps) and dropped, the rest of the last step is carried into the first arena
+        if (total_ != 0 || text_) throw std::runtime_error("FqBulkReader::seek on a stream already read");
+        ByteBuf scratch;
+        text_ = &scratch;
+        uint64_t before = 0;
+        while (!eof_ && total_ < off) {
+            scratch.clear();
+            before = total_;
+            read_more();
+        }
+        text_ = nullptr;
+        const uint64_t a = std::min<uint64_t>(std::max<uint64_t>(off, before), total_);
+        carry_.assign(scratch.data() + (a - before), (size_t)(total_ - a));
+        carry_off_ = a;
+        return;
+    }
     pos_ = (size_t)std::min<uint64_t>(off, map_size_);
     tbase_ = pos_ >> 6;
     indexed_ = tbase_ << 6;

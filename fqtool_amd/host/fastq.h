@@ -157,6 +157,9 @@ class FqReader {
 class Pool;
 class GzAhead;
 
+// decoding threads of one single-stream gzip input (ParGzSource)
+int gz_inflate_threads();
+
 class FqBulkReader {
    public:
     FqBulkReader(const std::string& path, bool phred64, int buf_size = 1 << 20);
@@ -184,7 +187,10 @@ class FqBulkReader {
         settle();
         return map_ != nullptr;
     }
-    void seek(uint64_t off);  // mapped files: the next record is read from stream offset off
+    // the next record is read from stream offset off (a mapped file; or a stream not read yet,
+    // whose bytes before off are then read and dropped)
+    void seek(uint64_t off);
+    bool parallel_gz() const { return pargz_ != nullptr; }  // a single-stream gzip file (ParGzSource)
 
    private:
     bool line(size_t x, size_t& e, size_t& next);
@@ -350,10 +356,11 @@ class PackReader {
     bool next(Pack& pk, size_t max_n, Pool* pool = nullptr);
     bool paired() const { return paired_; }
     uint64_t reads_seen() const { return reads_; }
-    // continue at stream offsets off1 / off2 (mapped regular files only: where the GPU's raw
-    // stream stopped), numbering packs from first_seq
+    // continue at stream offsets off1 / off2 (where the GPU's raw stream stopped: mapped regular
+    // files, or single-stream gzip files not read yet), numbering packs from first_seq
     void seek(uint64_t off1, uint64_t off2, uint64_t first_seq);
     bool mapped() { return r1_.mapped() && (!r2_ || r2_->mapped()); }
+    bool parallel_gz() const { return r1_.parallel_gz() && (!r2_ || r2_->parallel_gz()); }
     double parse_s = 0, tiles_s = 0;  // time spent parsing records / filling batch planes
     bool defer_tiles = false;         // next() leaves pack_tiles to the caller (another thread)
 

@@ -955,7 +955,15 @@ struct ParGzSource::Impl {
         return true;
     }
 
+    int nthreads = 1;
+    bool started = false;
+    void start() {  // (the workers start at the first read: a source opened and never read costs nothing)
+        started = true;
+        for (int t = 0; t < nthreads; ++t) th.emplace_back([this] { work(); });
+    }
+
     bool read(char* dst, size_t want, size_t& got) {
+        if (!started) start();
         if (fb) return fb_read(dst, want, got);
         got = 0;
         std::unique_lock<std::mutex> lk(m);
@@ -1057,7 +1065,7 @@ std::unique_ptr<ParGzSource> ParGzSource::open_chunked(const std::string& path, 
     const int nt = std::max(1, threads);
     im->ahead = (size_t)std::max(4, 2 * nt);
     Impl* p = im.get();
-    for (int t = 0; t < nt; ++t) im->th.emplace_back([p] { p->work(); });
+    p->nthreads = nt;
     return std::unique_ptr<ParGzSource>(new ParGzSource(im.release()));
 }
 

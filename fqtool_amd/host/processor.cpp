@@ -24,6 +24,7 @@
 #include <unistd.h>
 
 #include "evaluator.h"
+#include "pargz.h"
 
 namespace fqhost {
 namespace {
@@ -1459,7 +1460,20 @@ struct Lane {
                     f = -1;
                 }
         };
+        // single-stream gzip inputs: each mate's stream comes from its parallel inflater, in order
+        // (the windows are consecutive); its size is known once the inflater ends it.  A stream
+        // that fails (corrupt data) ends the raw stream short of the bad call: the host reader
+        // then resumes there and meets the failure as the reference's reader does.
+        std::unique_ptr<ParGzSource> gzs[2];
+        std::atomic<bool> src_failed{false};
+        const bool gz_in = ends_with_gz(files[0]);
         for (int m = 0; m < mates; ++m) {
+            if (gz_in) {
+                gzs[m] = ParGzSource::open(files[m], (size_t)1 << 20, gz_inflate_threads());
+                if (!gzs[m]) return rr;  // (the host reader takes the whole input)
+                size[m] = UINT64_MAX;
+                continue;
+            }
             fd[m] = ::open(files[m].c_str(), O_RDONLY);
             struct stat st;
             if (fd[m] < 0 || fstat(fd[m], &st) != 0 || !S_ISREG(st.st_mode) || st.st_size <= 0) {
@@ -1548,10 +1562,11 @@ struct Lane {
         std::thread rd([&] {  // the window reader
             try {
                 uint64_t pos[2] = {0, 0};
+                uint64_t rsize[2] = {size[0], size[1]};  // (this thread's copy: a gzip stream's grows known)
                 std::deque<Win> made;  // windows produced and (maybe) not yet launched
                 for (uint64_t id = 0;; ++id) {
                     bool more = false;
-                    for (int m = 0; m < mates; ++m) more = more || pos[m] < size[m];
+                    for (int m = 0; m < mates; ++m) more = more || pos[m] < rsize[m];
                     if (!more) break;
                     double b[2], pairs_held = 1e18;
                     uint64_t held[2];
@@ -1581,7 +1596,7 @@ struct Lane {
                             want = need <= 0 ? 0 : (uint64_t)need;
                         }
                         w.start[m] = pos[m];
-                        w.n[m] = std::min(std::min<uint64_t>((want + 4095) / 4096 * 4096, wcap), size[m] - pos[m]);
+                        w.n[m] = std::min(std::min<uint64_t>((want + 4095) / 4096 * 4096, wcap), rsize[m] - pos[m]);
                         pos[m] += w.n[m];
                     }
                     const auto s0 = std::chrono::steady_clock::now();
@@ -1596,6 +1611,26 @@ struct Lane {
                         pieces[m] = (int)((w.n[m] + piece - 1) / piece);
                     }
                     std::atomic<bool> short_read{false};
+                    if (gz_in) {
+                        bool ended = true;
+                        for (int m = 0; m < mates; ++m) {
+                            size_t got = 0;
+                            if (w.n[m] && !gzs[m]->read(st.buf[m].data() + off0, (size_t)w.n[m], got)) src_failed = true;
+                            if (got < w.n[m]) {  // the stream's end (or its failure)
+                                w.n[m] = got;
+                                pos[m] = w.start[m] + got;
+                                rsize[m] = pos[m];
+                                std::lock_guard<std::mutex> g(fb_m);
+                                size[m] = rsize[m];
+                            }
+                            ended = ended && w.n[m] == 0 && pos[m] == rsize[m];
+                        }
+                        pieces[0] = pieces[1] = 0;
+                        if (ended) {  // (every stream has ended: no window)
+                            free_stages.push(w.stage);
+                            break;
+                        }
+                    }
                     pool.run(pieces[0] + pieces[1], [&](int k) {
                         const int m = k < pieces[0] ? 0 : 1;
                         const uint64_t o = (uint64_t)(m ? k - pieces[0] : k) * piece;
@@ -1619,6 +1654,7 @@ struct Lane {
                     raw_read_s += since(r0);
                     made.push_back(w);
                     if (!ready.push(w)) break;
+                    if (src_failed) break;  // (no window past a failed gzip read)
                 }
             } catch (...) {
                 rd_err = std::current_exception();
@@ -1736,15 +1772,22 @@ struct Lane {
                     ++seq;
                     if (wins.empty()) enqueue_next();
                     const bool last = wins.empty() && input_done;
+                    const bool failed = src_failed;  // (a gzip input failed: its carry is not drained)
                     bool left = false, exhausted = false;  // (exhausted: a mate has sent all its bytes)
+                    uint64_t sz_now[2];
+                    {
+                        std::lock_guard<std::mutex> g(fb_m);
+                        sz_now[0] = size[0];
+                        sz_now[1] = size[1];
+                    }
                     for (int m = 0; m < mates; ++m) {
                         left = left || r.carry[m] > 0;
                         const uint64_t sent = wins.empty() ? w.start[m] + w.n[m] : wins.back().start[m] + wins.back().n[m];
-                        exhausted = exhausted || sent == size[m];
+                        exhausted = exhausted || sent == sz_now[m];
                     }
-                    if (last && left && r.pairs > 0 && !r.stop) {  // all input is on the device: drain its carry
+                    if (last && left && r.pairs > 0 && !r.stop && !failed) {  // all input is on the device: drain its carry
                         Win d;
-                        for (int m = 0; m < mates; ++m) d.start[m] = size[m];
+                        for (int m = 0; m < mates; ++m) d.start[m] = sz_now[m];
                         enqueue_window(d);
                         raw_pairs += (uint64_t)r.pairs;
                         ++raw_packs;
@@ -1754,9 +1797,9 @@ struct Lane {
                     ++raw_packs;
                     // (no pairs while every mate still has bytes to send: the windows were too small)
                     if (r.stop || (r.pairs == 0 && exhausted) || last) {
-                        rr.done = last && !left && !r.stop;
+                        rr.done = last && !left && !r.stop && !failed;
                         raw_end = rr.done ? "end of input"
-                                          : std::string(r.stop ? "irregular record" : r.pairs == 0 ? "no pairs" : "bytes left at the end") +
+                                          : std::string(r.stop ? "irregular record" : failed && last ? "gzip read failed ahead" : r.pairs == 0 ? "no pairs" : "bytes left at the end") +
                                                 " after pack " + std::to_string(seq - 1) + " (window bytes " + std::to_string(w.n[0]) + "/" +
                                                 std::to_string(w.n[1]) + ", carry " + std::to_string(r.carry[0]) + "/" +
                                                 std::to_string(r.carry[1]) + ", max_len " + std::to_string(r.max_len) + ")";
@@ -1789,6 +1832,7 @@ struct Lane {
         for (int m = 0; m < mates; ++m)
             if (mp[m]) munmap(const_cast<char*>(mp[m]), (size_t)size[m]);
         rr.next_seq = seq;
+        if (gz_in) raw_end += " (gzip inputs inflated on " + std::to_string(gz_inflate_threads()) + " threads each)";
         return rr;
     }
 
@@ -2269,8 +2313,12 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
         // GPU-side record indexing (fq_engine_raw_*) for plain files on one engine: the engine's
         // dispatcher drives the raw stream first; the host reader takes over only where it stops
         const char* raw_env = std::getenv("FQ_RAW_MODE");
+        // (single-stream gzip inputs on one engine too: their streams come from the parallel
+        // inflater -- RawMulti reads windows with pread, plain files only)
+        const bool gz_both = ends_with_gz(o.in1) && (!paired || ends_with_gz(o.in2));
         const bool raw_mode = text_mode && !o.interleaved && !(raw_env && std::string(raw_env) == "0") &&
-                              !ends_with_gz(o.in1) && (!paired || !ends_with_gz(o.in2)) && pr.mapped();
+                              ((!ends_with_gz(o.in1) && (!paired || !ends_with_gz(o.in2)) && pr.mapped()) ||
+                               (gz_both && G == 1 && pr.parallel_gz()));
         std::promise<Lane::RawResume> raw_p;
         std::shared_future<Lane::RawResume> raw_f = raw_p.get_future().share();
         // several engines: one window source cutting whole pairs, dealt round-robin (RawMulti)

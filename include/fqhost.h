@@ -89,6 +89,11 @@ char* fqh_debug_records(const char* path, int bulk, int buf_size, int pack_n, in
  * not apply (small file, not gzip), -1 on error; fqh_gzread_all returns 0, -1 on error. */
 int fqh_pargz_read_all(const char* path, size_t call, int threads, size_t chunk, char** out, size_t* n, int* ok);
 int fqh_gzread_all(const char* path, size_t call, char** out, size_t* n, int* ok);
+/* Speed probe: the same streams read in `call`-byte calls into one reused buffer and discarded (the
+ * tool's reader copies each call into its arena the same way).  threads > 0: the parallel inflater
+ * (returns as fqh_pargz_read_all); threads == 0: zlib's gzread (returns 0).  *n: bytes read,
+ * *seconds: wall time of the reads. */
+int fqh_gz_drain(const char* path, size_t call, int threads, size_t chunk, size_t* n, int* ok, double* seconds);
 
 #ifdef __cplusplus
 }

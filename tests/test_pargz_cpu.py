@@ -214,3 +214,61 @@ def test_tool_matches_reference_on_corrupt_gzip(label, tmp_path):
         a, b = (json.loads((outs[t][0] / "r.json").read_text()) for t in ("ours", "ref"))
         for k in ("summary", "filtering_result", "read1_before_filtering", "read2_after_filtering"):
             assert a.get(k) == b.get(k), k
+
+
+def test_pigz_style_stream(host, files, tmp_path):
+    """bench.py's gzip -6 inputs: pieces deflated apart (each primed with the previous 32 KiB) and
+    joined by full flushes into one member -- empty stored blocks at byte boundaries mid-stream"""
+    import sys
+    sys.path.insert(0, abi.REPO_DIR)
+    import bench
+    _, _, text = files
+    src = tmp_path / "t.fq"
+    src.write_bytes(text)
+    p = bench.gzip_single_member(str(src), str(tmp_path / "t.fq.gz"), threads=3, piece=65536)
+    assert gzip.open(p).read() == text
+    want, wok = ref(host, p)
+    for chunk in (4096, 16384):
+        rc, got, ok = par(host, p, chunk, 3)
+        assert rc == 1 and (got, ok) == (want, wok)
+
+
+@pytest.mark.parametrize("where", [0.3, 0.7])
+def test_tool_resumes_gzip_stream_after_irregular_record(where, tmp_path):
+    """A "\\r\\n" record part way into read 1 (a clean gzip member): the raw stream stops there and the
+    host reader resumes on the gzip stream (read again from its start up to the stop) -- outputs and
+    JSON as the reference binary's."""
+    if not os.path.exists(REF_BIN):
+        pytest.skip("reference binary not built (oracle/Makefile.ref)")
+    subprocess.run(["make", "-s", "-C", abi.REPO_DIR, "cpuhost"], check=True)
+    cpu_bin = os.path.join(abi.REPO_DIR, "build", "cpuhost", "fqtool")
+    ind = tmp_path / "in"
+    ind.mkdir()
+    with gzip.open(os.path.join(E.INPUTS, "r1.fq.gz"), "rb") as f:
+        t1 = f.read() * 3
+    with gzip.open(os.path.join(E.INPUTS, "r2.fq.gz"), "rb") as f:
+        t2 = f.read() * 3
+    lines = t1.split(b"\n")
+    k = int(len(lines) * where) // 4 * 4
+    for j in range(k, k + 4):
+        lines[j] += b"\r"
+    (ind / "r1.fq.gz").write_bytes(gz_member(b"\n".join(lines), 6))
+    (ind / "r2.fq.gz").write_bytes(gz_member(t2, 6))
+    outs = {}
+    for tool in ("ours", "ref"):
+        od = tmp_path / tool
+        od.mkdir()
+        argv = [cpu_bin if tool == "ours" else REF_BIN, "-w", "2", "-i", str(ind / "r1.fq.gz"), "-I",
+                str(ind / "r2.fq.gz"), "-o", str(od / "o1.fq"), "-O", str(od / "o2.fq"), "-q", "-g",
+                "-J", str(od / "r.json"), "-H", str(od / "r.html")]
+        env = dict(os.environ, FQ_PARGZ_CHUNK="8192", FQ_RAW_WINDOW0="65536")
+        p = subprocess.run(argv, capture_output=True, cwd=od, timeout=300, env=env)
+        outs[tool] = (od, p.returncode, p.stderr.decode(errors="replace"))
+    assert outs["ours"][1] == outs["ref"][1] == 0, (outs["ours"][2][-1500:], outs["ref"][2][-1500:])
+    assert "irregular record" in outs["ours"][2], outs["ours"][2][-1500:]
+    for n in ("o1.fq", "o2.fq"):
+        assert (outs["ours"][0] / n).read_bytes() == (outs["ref"][0] / n).read_bytes(), n
+    import json
+    a, b = (json.loads((outs[t][0] / "r.json").read_text()) for t in ("ours", "ref"))
+    for k in ("summary", "filtering_result", "read1_before_filtering", "read2_after_filtering"):
+        assert a.get(k) == b.get(k), k

@@ -68,3 +68,13 @@ def test_records_only_egress_under_tsan(case, zc, tsan_build, tmp_path):
 def test_text_packs_under_tsan(case, tsan_build, tmp_path):
     err, reports = T.run_case(case, str(tmp_path), 4, devices=2, mode="text", pack_pairs=7)
     assert reports == 0, err[-6000:]
+
+
+@pytest.mark.parametrize("case,workers", [("td_pe_gz", 4), ("td_pe_qag", 16), ("td_se_q", 4)])
+def test_gzip_raw_stream_under_tsan(case, workers, tsan_build, tmp_path):
+    """Single-stream gzip inputs on the raw stream (one engine): each mate's parallel inflater (4 KiB
+    chunks, so many chunks and workers) read in order by the window reader."""
+    env = {"FQ_RAW_WINDOW0": "4096", "FQ_PARGZ_CHUNK": "4096"}
+    err, reports = T.run_case(case, str(tmp_path), workers, devices=1, mode="rawgz", env_extra=env, pack_pairs=7)
+    assert "gzip inputs inflated" in err, err[-3000:]
+    assert reports == 0, err[-6000:]
