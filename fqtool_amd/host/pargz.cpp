@@ -142,7 +142,8 @@ bool build(Table& t, const uint8_t* lens, int n, int pbits, Kind kind) {
         next[l] = code;
     }
     const int sbits = std::max(0, mx - pbits);
-    std::vector<int> sub((size_t)1 << pbits, -1);
+    thread_local std::vector<int> sub;  // (per-thread scratch: the block-start search builds many tables)
+    sub.assign((size_t)1 << pbits, -1);
     for (int s = 0; s < n; ++s) {
         const int l = lens[s];
         if (!l) continue;
@@ -166,7 +167,8 @@ bool build(Table& t, const uint8_t* lens, int n, int pbits, Kind kind) {
         // (bits 24-31 the second byte, bit 8 set, bits 0-4 both code lengths): literal-heavy text
         // (FASTQ bases and qualities, codes of 2-6 bits) decodes two symbols per lookup
         const uint32_t full = 1u << pbits;
-        std::vector<uint32_t> one(t.e.begin(), t.e.begin() + full);
+        thread_local std::vector<uint32_t> one;
+        one.assign(t.e.begin(), t.e.begin() + full);
         for (uint32_t i = 0; i < full; ++i) {
             const uint32_t e = one[i];
             if (!(e & kLit)) continue;
@@ -350,7 +352,8 @@ struct Decoder {
     // alias everything: members would be reloaded after each one); >= 48 bits are in the buffer at
     // each code, enough for a length, its extra bits, a distance and its extra bits.
     template <class T, bool kSym>
-    static bool codes_impl(Bits& br, PodBuf<T>& v, size_t& last_marker, const Table& lt, const Table& dt) {
+    static bool codes_impl(Bits& br, PodBuf<T>& v, size_t& last_marker, const Table& lt, const Table& dt,
+                           size_t stop_at = SIZE_MAX, bool* paused = nullptr) {
         const uint32_t* __restrict L = lt.e.data();
         const uint32_t* __restrict D = dt.e.data();
         const int lb = lt.pbits, db = dt.pbits;
@@ -364,6 +367,7 @@ struct Decoder {
         v.reserve(sz + 65536);
         T* __restrict b = v.p;
         size_t cap = v.cap;
+        size_t lim = std::min(cap - 300, stop_at);  // (the output's room, or where to pause)
         bool ok = false;
         for (;;) {
             if (cnt < 48) {
@@ -382,11 +386,16 @@ struct Decoder {
                     if (pos > n + 8) break;  // (past the input: truncated, or a false start)
                 }
             }
-            if (sz + 300 > cap) {
+            if (sz >= lim) {
+                if (sz >= stop_at) {  // (paused at a code boundary: a later call goes on from here)
+                    *paused = true;
+                    break;
+                }
                 v.n = sz;
                 v.reserve(cap * 2);
                 b = v.p;
                 cap = v.cap;
+                lim = std::min(cap - 300, stop_at);
             }
             uint32_t e = L[buf & lm];
             if (e & kSub) e = L[(e >> 16) + ((buf >> lb) & ((1u << ((e >> 8) & 15)) - 1))];
@@ -520,6 +529,23 @@ uint32_t crc_of(const uint8_t* p, size_t n) {
     return c;
 }
 
+// Kraft sums (128 >> l per nonzero length l) of four three-bit code lengths, by their 12 bits
+const uint16_t* kraft4() {
+    static const std::vector<uint16_t> t = [] {
+        std::vector<uint16_t> v(4096);
+        for (int i = 0; i < 4096; ++i) {
+            int s = 0;
+            for (int k = 0; k < 4; ++k) {
+                const int l = (i >> (3 * k)) & 7;
+                if (l) s += 128 >> l;
+            }
+            v[(size_t)i] = (uint16_t)s;
+        }
+        return v;
+    }();
+    return t.data();
+}
+
 }  // namespace
 
 // ---- the chunked source ----
@@ -612,27 +638,46 @@ struct ParGzSource::Impl {
     bool find_start(Chunk& c, Decoder& dec) {
         Bits br;
         const uint64_t lim = std::min<uint64_t>(c.nom1, (uint64_t)size * 8);
+        uint64_t cand = 0, base = 0;  // bit i of cand: offset base + i passes the header checks
+        bool have = false;
         for (uint64_t b = c.nom0; b < lim; ++b) {
-            // quick rejects on the header bits: BFINAL 0, BTYPE 2, HLIT <= 29, HDIST <= 29
-            const size_t by = (size_t)(b >> 3);
-            if (by + 8 > size) return false;
-            uint64_t w;
-            std::memcpy(&w, map + by, 8);
-            w >>= (b & 7);
-            if ((w & 7) != 4 || ((w >> 3) & 31) > 29 || ((w >> 8) & 31) > 29) continue;
-            // the code-length code (HCLEN + 4 three-bit lengths from bit 17) must be complete
+            // quick rejects on the header bits, 64 offsets at a time: BFINAL 0, BTYPE 2 (bits 001),
+            // HLIT <= 29 and HDIST <= 29 (their top four bits not all set)
+            if (!have || b >= base + 64) {
+                base = b;
+                const size_t by = (size_t)(b >> 3);
+                if (by + 24 > size) return false;
+                unsigned __int128 x;
+                std::memcpy(&x, map + by, 16);
+                x >>= (b & 7);  // (121 valid bits: the 64 offsets' first 13 bits)
+                cand = (uint64_t)(~x & ~(x >> 1) & (x >> 2) & ~((x >> 4) & (x >> 5) & (x >> 6) & (x >> 7)) &
+                                  ~((x >> 9) & (x >> 10) & (x >> 11) & (x >> 12)));
+                have = true;
+            }
+            const uint64_t m = cand >> (b - base);
+            if (!m) {  // (none left in this window: the next one starts at base + 64)
+                b = base + 63;
+                have = false;
+                continue;
+            }
+            b += (uint64_t)__builtin_ctzll(m);
+            if (b >= lim) return false;
+            // the code-length code (HCLEN + 4 three-bit lengths from bit 17) must be complete:
+            // Kraft sum of its lengths (128 >> l each) exactly 128, four lengths per table lookup
             {
                 const uint64_t c17 = b + 17;
                 if ((c17 >> 3) + 8 > size) return false;
                 uint64_t v;
                 std::memcpy(&v, map + (c17 >> 3), 8);
                 v >>= (c17 & 7);
-                const int ncl = (int)((w >> 13) & 15) + 4;
-                int cnt[8] = {0};
-                for (int k = 0; k < ncl; ++k) ++cnt[(v >> (3 * k)) & 7];
-                int left = 1;
-                for (int l = 1; l <= 7 && left >= 0; ++l) left = 2 * left - cnt[l];
-                if (left != 0) continue;
+                uint64_t hw;
+                std::memcpy(&hw, map + (b >> 3), 8);
+                const int ncl = (int)((hw >> (b & 7) >> 13) & 15) + 4;
+                const uint16_t* kr = kraft4();
+                const uint64_t vv = v & ((1ull << (3 * ncl)) - 1);  // (3 ncl <= 57)
+                const uint32_t sum = kr[vv & 4095] + kr[(vv >> 12) & 4095] + kr[(vv >> 24) & 4095] + kr[(vv >> 36) & 4095] +
+                                     kr[(vv >> 48) & 4095];
+                if (sum != 128) continue;
             }
             br.seek(map, size, b);
             if (stop) return false;
@@ -640,17 +685,31 @@ struct ParGzSource::Impl {
             take(c.o16.s);
             c.o16.s.n = 0;
             c.o16.last_marker = 0;
-            const Status st = dec.block(br, c.o16);
-            if (st == kError) continue;
             // (a false start can decode as a block: its literals are then random bytes.  FASTQ is
             // text, so a block whose literals are not is passed over -- only a speed matter: the
-            // start of every chunk is verified against the previous chunk's end)
-            size_t odd = 0;
-            for (size_t k = 0; k < c.o16.s.n; ++k) {
-                const uint16_t x = c.o16.s.p[k];
-                odd += x < 256 && x != '\n' && x != '\r' && x != '\t' && (x < 32 || x > 126);
+            // start of every chunk is verified against the previous chunk's end.  With complete
+            // codes every bit pattern decodes, so a false start may run on for many kilobytes until
+            // it happens on an end-of-block code: its first 1024 symbols are judged first.)
+            auto implausible = [&](size_t n) {
+                size_t odd = 0;
+                for (size_t k = 0; k < n; ++k) {
+                    const uint16_t x = c.o16.s.p[k];
+                    odd += x < 256 && x != '\n' && x != '\r' && x != '\t' && (x < 32 || x > 126);
+                }
+                return odd * 200 > n;
+            };
+            br.refill();
+            br.consume(3);  // (BFINAL 0, BTYPE 2: checked above)
+            if (!dec.dynamic_header(br)) continue;
+            bool paused = false;
+            bool ok = Decoder::codes_impl<uint16_t, true>(br, c.o16.s, c.o16.last_marker, dec.lit, dec.dist, 1024, &paused);
+            if (paused) {
+                if (implausible(c.o16.s.n)) continue;
+                paused = false;
+                ok = Decoder::codes_impl<uint16_t, true>(br, c.o16.s, c.o16.last_marker, dec.lit, dec.dist);
             }
-            if (odd * 200 > c.o16.s.n || c.o16.s.n < 64) continue;
+            if (!ok || implausible(c.o16.s.n) || c.o16.s.n < 64) continue;
+            const Status st = kBlockDone;
             c.start = (int64_t)b;
             c.end = br.bitpos();
             c.final_ = st == kFinalDone;
@@ -814,6 +873,16 @@ struct ParGzSource::Impl {
             std::vector<uint8_t> lut;
             auto fast = [&](size_t k, size_t e) {  // a full window: every symbol is lut[symbol]
                 const uint8_t* __restrict t = lut.data();
+                // 8 symbols a step: packed as they are when none is a marker (about 2 steps in 3 on
+                // FASTQ, where ~18 % of the symbols are markers), else through the table
+                for (; k + 8 <= e; k += 8) {
+                    const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + k));
+                    if (_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_srli_epi16(x, 8), z)) == 0xffff) {
+                        _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + k), _mm_packus_epi16(x, x));
+                    } else {
+                        for (size_t j = k; j < k + 8; ++j) dst[j] = t[src[j]];
+                    }
+                }
                 for (; k < e; ++k) dst[k] = t[src[k]];
             };
             if (early) {
