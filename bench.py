@@ -298,6 +298,7 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
     assert lib.fq_synth_fill_device(ctypes.byref(b), SEED, first, READ_LEN, None) == 0
     torch.cuda.synchronize()
     out = {"e2e": None, "cpu_baseline": None}
+    shm = None
     try:
         t0 = time.perf_counter()
         small = write_fastq_fast(bufs, cpu_pairs, first, tmp, "cpu_")
@@ -309,6 +310,14 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
         # the file leg's outputs go beside the inputs: room for one run's outputs (about the inputs' size)
         free = shutil.disk_usage(tmp).free
         file_legs = e2e_pairs * rec_bytes * 1.1 < free
+        # tmpfs for the output legs without disk write-back: room for one run's plain outputs
+        # (about the inputs' size) besides what the box's memory holds already
+        shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
+        if shm and shutil.disk_usage(shm).free < e2e_pairs * rec_bytes * 1.3:
+            log(f"tmpfs legs skipped: {shutil.disk_usage(shm).free / 1e9:.1f} GB free in /dev/shm")
+            shm = None
+        if shm:
+            shm = tempfile.mkdtemp(prefix="fqbench_", dir=shm)
         if not file_legs:
             log(f"file legs skipped: {free / 1e9:.1f} GB free beside the inputs")
         opts = ["-q", "-a", "--detect_pe_adapter", "-g"]
@@ -322,7 +331,9 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             pairs = pairs or e2e_pairs
             outs = {"null": ["/dev/null", "/dev/null"],
                     "file": [os.path.join(tmp, "out1.fq"), os.path.join(tmp, "out2.fq")],
-                    "gz": [os.path.join(tmp, "out1.fq.gz"), os.path.join(tmp, "out2.fq.gz")]}[outputs]
+                    "gz": [os.path.join(tmp, "out1.fq.gz"), os.path.join(tmp, "out2.fq.gz")],
+                    "shm": [os.path.join(shm or tmp, "out1.fq"), os.path.join(shm or tmp, "out2.fq")],
+                    "gz_shm": [os.path.join(shm or tmp, "out1.fq.gz"), os.path.join(shm or tmp, "out2.fq.gz")]}[outputs]
             if "--merge_output" in extra and outputs != "null":
                 extra = [outs[0] if (k > 0 and extra[k - 1] == "--merge_output") else a for k, a in enumerate(extra)]
             cmd = [tool, "-i", inp[0], "-I", inp[1], "-o", outs[0], "-O", outs[1], *extra, "-w", str(workers),
@@ -383,9 +394,17 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
                     os.remove(p_)
             # the writers timed: the same C3 run with plain FASTQ output files (page cache), and
             # BGZF .gz outputs (-z 4, the reference's default level) on the CPU-baseline sample
-            if os.environ.get("FQ_BENCH_FILE_LEGS", "1") != "0" and file_legs:
-                out["e2e_file"] = e2e(opts, outputs="file")
-                out["e2e_gz"] = e2e(opts, outputs="gz", inp=small, pairs=cpu_pairs)
+            if os.environ.get("FQ_BENCH_FILE_LEGS", "1") != "0":
+                if file_legs:
+                    out["e2e_file"] = e2e(opts, outputs="file")
+                if shm:
+                    # the same outputs on tmpfs (no disk write-back in the timing), and BGZF .gz
+                    # outputs at -z 4 on the whole e2e input (members compressed with libdeflate
+                    # on the pool)
+                    out["e2e_file_shm"] = e2e(opts, outputs="shm")
+                    out["e2e_gz"] = e2e(opts, outputs="gz_shm")
+                elif file_legs:
+                    out["e2e_gz"] = e2e(opts, outputs="gz", inp=small, pairs=cpu_pairs)
         ref = os.path.join(REPO, "oracle", "_ref", "fqtool_ref")
         if os.path.exists(ref):
             w = min(16, workers)
@@ -419,6 +438,8 @@ def host_legs(lib, abi, torch, cpu_pairs, e2e_pairs, workers):
             out["cpu_baseline"] = port_baseline(abi, cpu_pairs, first, host_cores())
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+        if shm:
+            shutil.rmtree(shm, ignore_errors=True)
     return out
 
 
@@ -853,6 +874,7 @@ def run_rank(args):
         "e2e_c4": None,
         "e2e_file": None,
         "e2e_gz": None,
+        "e2e_file_shm": None,
         "e2e_gzin": None,
         "acc_sha256": acc_digest,
         "parity_sample": sample,
@@ -866,6 +888,7 @@ def run_rank(args):
         out["e2e_file"] = legs.get("e2e_file")
         out["e2e_gz"] = legs.get("e2e_gz")
         out["e2e_gzin"] = legs.get("e2e_gzin")
+        out["e2e_file_shm"] = legs.get("e2e_file_shm")
         log(f"e2e {legs['e2e']}")
         log(f"e2e_c4 {legs.get('e2e_c4')}")
     runner.close()

@@ -176,6 +176,9 @@ namespace {
 #ifndef FQ_OV12
 #define FQ_OV12 0  // overlap candidates at the default limit 5 from the first 12 positions (not 16): slower (a false candidate in any lane costs the wave an exact check; profiles/r05_ab_ov12_stvcc.txt)
 #endif
+#ifndef FQ_OV_CSHIFT
+#define FQ_OV_CSHIFT 1  // overlap candidates: the block words through a shift register (not a select per word on the runtime block index)
+#endif
 #ifndef FQ_FASTMASK
 #define FQ_FASTMASK 1  // posmask at the hot sites and staging's partial-chunk byte masks by v_med3 + 64-bit shifts (neutral to -0.5 %, profiles/r05_ab_fastmask_runshift.txt)
 #endif
@@ -638,9 +641,18 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, FX f
 #pragma unroll
     for (int k = 2; k < kOvBlocks; ++k)
         if (__any(cnt > 32 * k)) nblk = k + 1;
+#if FQ_OV_CSHIFT
+    // the blocks' words enter a shift register at the top, the others moving down one (kOvBlocks - 1
+    // moves per block instead of a select per word on the runtime index bk); after the loop they sit
+    // kOvBlocks - nblk places too high and move down with zeros
+    uint32_t creg[kOvBlocks];
+#pragma unroll
+    for (int i = 0; i < kOvBlocks; ++i) creg[i] = 0u;
+#else
 #pragma unroll
     for (int bk = 0; bk < kOvBlocks; ++bk)
         if (bk >= nblk) cand[bk] = 0u;
+#endif
 #pragma unroll 1
     for (int bk = 0; bk < nblk; ++bk) {
         fx.next_block();
@@ -726,10 +738,31 @@ __device__ inline void ov_candidates(const uint32_t* col, int cm, int mpos, FX f
         }
         }
         const int nb = cnt - 32 * bk;  // valid offsets of this block
+#if FQ_OV_CSHIFT
+        // bits [0, nb), nb clamped to [0, 32]: the low word of ~(~0 << nb) by one 64-bit shift
+        int nbc;
+        asm("v_med3_i32 %0, %1, 0, 32" : "=v"(nbc) : "v"(nb));
+        unsigned long long nbx;
+        asm("v_lshlrev_b64 %0, %1, -1" : "=v"(nbx) : "v"(nbc));
+#pragma unroll
+        for (int i = 0; i + 1 < kOvBlocks; ++i) creg[i] = creg[i + 1];
+        creg[kOvBlocks - 1] = lt & ~(uint32_t)nbx;
+#else
         cand[bk] = lt & (nb >= 32 ? ~0u : nb <= 0 ? 0u : ((1u << nb) - 1u));
+#endif
         L0 = L1;
         H0 = H1;
     }
+#if FQ_OV_CSHIFT
+#pragma unroll 1
+    for (int s = nblk; s < kOvBlocks; ++s) {
+#pragma unroll
+        for (int i = 0; i + 1 < kOvBlocks; ++i) creg[i] = creg[i + 1];
+        creg[kOvBlocks - 1] = 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kOvBlocks; ++i) cand[i] = creg[i];
+#endif
 }
 
 // AdapterTrimmer::trimBySequence (src/adaptertrimmer.cpp:29-90): the first pos in [start, n - 4)
