@@ -48,7 +48,10 @@ def fast_launches(vals, names, probe):
 
 def trace_ms(root, cfg):
     ds = []
-    for path in glob.glob(os.path.join(root, f"{cfg}_kt", "**", "*kernel_trace.csv"), recursive=True):
+    # (pmc_sq.sh's own trace, or profile_round.sh's beside the counter directory: gpurun_out/kt_<cfg>)
+    paths = glob.glob(os.path.join(root, f"{cfg}_kt", "**", "*kernel_trace.csv"), recursive=True) or \
+        glob.glob(os.path.join(os.path.dirname(os.path.normpath(root)), f"kt_{cfg}", "**", "*kernel_trace.csv"), recursive=True)
+    for path in paths:
         with open(path) as f:
             for r in csv.DictReader(f):
                 if "pe_fast_kernel" in r["Kernel_Name"]:
