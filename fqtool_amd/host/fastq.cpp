@@ -1586,7 +1586,7 @@ void bgzf_append(std::string& out, const char* in, size_t n, uint32_t crc, const
     out.append(reinterpret_cast<const char*>(tr), 8);
     (void)in;
 }
-std::string gzip_member_libdeflate(const std::string& s, int level) {
+std::string gzip_member_libdeflate(const char* sp, size_t sn, int level) {
     constexpr size_t kIn = 0xff00;
     const Libdeflate& ld = libdeflate();
     struct Cache {
@@ -1602,12 +1602,12 @@ std::string gzip_member_libdeflate(const std::string& s, int level) {
     if (!c) c = ld.calloc_(lvl);
     if (!c) throw std::runtime_error("libdeflate_alloc_compressor failed");
     std::string out;
-    out.reserve(s.size() / 3 + 64);
+    out.reserve(sn / 3 + 64);
     char tmp[65536];
     size_t o = 0;
     do {
-        const size_t n = std::min(kIn, s.size() - o);
-        const char* in = s.data() + o;
+        const size_t n = std::min(kIn, sn - o);
+        const char* in = sp + o;
         const uint32_t crc = ld.crc32_(0, in, n);
         size_t clen = ld.compress(c, in, n, tmp, 65536 - 26);
         if (clen == 0) {  // stored: BFINAL, BTYPE 00, LEN, NLEN, the bytes
@@ -1621,11 +1621,13 @@ std::string gzip_member_libdeflate(const std::string& s, int level) {
         }
         bgzf_append(out, in, n, crc, tmp, clen);
         o += n;
-    } while (o < s.size());
+    } while (o < sn);
     return out;
 }
-std::string gzip_member(const std::string& s, int level) {
-    if (libdeflate().cok) return gzip_member_libdeflate(s, level);
+std::string gzip_member(const char* sp, size_t sn, int level);
+std::string gzip_member(const std::string& s, int level) { return gzip_member(s.data(), s.size(), level); }
+std::string gzip_member(const char* sp, size_t sn, int level) {
+    if (libdeflate().cok) return gzip_member_libdeflate(sp, sn, level);
     constexpr size_t kIn = 0xff00;
     z_stream z;
     std::memset(&z, 0, sizeof z);
@@ -1636,8 +1638,8 @@ std::string gzip_member(const std::string& s, int level) {
     int cur = level;
     size_t o = 0;
     do {
-        const size_t n = std::min(kIn, s.size() - o);
-        const Bytef* in = reinterpret_cast<const Bytef*>(s.data() + o);
+        const size_t n = std::min(kIn, sn - o);
+        const Bytef* in = reinterpret_cast<const Bytef*>(sp + o);
         size_t clen = 0;
         for (int lvl : {level, 0}) {  // (a member that does not shrink enough is stored)
             deflateReset(&z);
@@ -1657,7 +1659,7 @@ std::string gzip_member(const std::string& s, int level) {
         const uint32_t crc = (uint32_t)crc32(crc32(0, nullptr, 0), in, (uInt)n);
         bgzf_append(out, reinterpret_cast<const char*>(in), n, crc, tmp.data(), clen);
         o += n;
-    } while (o < s.size());
+    } while (o < sn);
     deflateEnd(&z);
     return out;
 }
@@ -1701,10 +1703,22 @@ void Writer::write_raw(const char* p, size_t n, Pool* pool) {
         if (std::fwrite(p, 1, n, fp_) != n) throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
         return;
     }
-    const size_t blk = (size_t)1 << 20;  // (one task of BGZF members per block on the pool)
-    std::vector<std::string> blocks;
-    for (size_t o = 0; o < n; o += blk) blocks.emplace_back(p + o, std::min(blk, n - o));
-    write(blocks, pool);
+    // one task of BGZF members per 1 MiB block on the pool, compressed from the caller's bytes
+    const size_t blk = (size_t)1 << 20;
+    const int nb = (int)((n + blk - 1) / blk);
+    std::vector<std::string> z((size_t)nb);
+    auto work = [&](int i) {
+        const size_t o = (size_t)i * blk;
+        z[(size_t)i] = gzip_member(p + o, std::min(blk, n - o), level_);
+    };
+    if (pool) pool->run(nb, work);
+    else
+        for (int i = 0; i < nb; ++i) work(i);
+    for (const auto& s : z)
+        if (!s.empty()) {
+            put(fp_, s);
+            any_member_ = true;
+        }
 }
 
 void Writer::write_segs(const iovec* v, size_t n) {
