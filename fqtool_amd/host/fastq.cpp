@@ -1703,22 +1703,35 @@ void Writer::write_raw(const char* p, size_t n, Pool* pool) {
         if (std::fwrite(p, 1, n, fp_) != n) throw std::runtime_error(std::string("write failed: ") + std::strerror(errno));
         return;
     }
-    // one task of BGZF members per 1 MiB block on the pool, compressed from the caller's bytes
+    // one task of BGZF members per 1 MiB block on the pool, compressed from the caller's bytes, in
+    // groups of 16 blocks: a group's members are written on a helper thread while the next group
+    // compresses (the writes of one file are otherwise a serial gap in the pool's work)
     const size_t blk = (size_t)1 << 20;
     const int nb = (int)((n + blk - 1) / blk);
+    constexpr int kGroup = 16;
     std::vector<std::string> z((size_t)nb);
-    auto work = [&](int i) {
-        const size_t o = (size_t)i * blk;
-        z[(size_t)i] = gzip_member(p + o, std::min(blk, n - o), level_);
-    };
-    if (pool) pool->run(nb, work);
-    else
-        for (int i = 0; i < nb; ++i) work(i);
-    for (const auto& s : z)
-        if (!s.empty()) {
-            put(fp_, s);
-            any_member_ = true;
-        }
+    std::future<void> writing;
+    for (int g0 = 0; g0 < nb; g0 += kGroup) {
+        const int g1 = std::min(nb, g0 + kGroup);
+        auto work = [&](int k) {
+            const int i = g0 + k;
+            const size_t o = (size_t)i * blk;
+            z[(size_t)i] = gzip_member(p + o, std::min(blk, n - o), level_);
+        };
+        if (pool) pool->run(g1 - g0, work);
+        else
+            for (int k = 0; k < g1 - g0; ++k) work(k);
+        if (writing.valid()) writing.get();  // (in order: the previous group first; rethrows its error)
+        writing = std::async(std::launch::async, [this, &z, g0, g1] {
+            for (int i = g0; i < g1; ++i)
+                if (!z[(size_t)i].empty()) {
+                    put(fp_, z[(size_t)i]);
+                    std::string().swap(z[(size_t)i]);
+                }
+        });
+        any_member_ = true;
+    }
+    if (writing.valid()) writing.get();
 }
 
 void Writer::write_segs(const iovec* v, size_t n) {
