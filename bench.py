@@ -850,7 +850,7 @@ def run_rank(args):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded counter-based generator in HBM, SURVEY.md 8(d))",
-        "config": {"workload": WORKLOADS[args.config], ("pairs_per_gpu" if paired else "reads_per_gpu"): n,
+        "config": {"workload": WORKLOADS[args.config].replace("150bp", f"{READ_LEN}bp"), ("pairs_per_gpu" if paired else "reads_per_gpu"): n,
                    "first_index": first,
                    "read_len": READ_LEN, "row_stride": STRIDE,
                    "parallelism": f"dp{world} (pairs sharded, RCCL sum of the accumulator block)"},
