@@ -24,9 +24,12 @@ only = os.environ.get("VARIANTS")
 if only:
     variants = [v for v in variants if v[0] in only.split(",")]
 results = {}
-for rep in range(3 if os.environ.get("CONFIG", "C3") == "C3" else 0):
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import config_params  # (the BASELINE config's engine parameters, CONFIG=C3 by default)
+CFG = os.environ.get("CONFIG", "C3")
+for rep in range(int(os.environ.get("REPS", 3))):
     for name, bits in variants:
-        p = abi.default_params(True, 256); p.qual_filter_enabled = 1; p.adapter_trimming = 1; p.polyg_enabled = 1
+        p = config_params(abi, CFG)
         p.reserved[0] = bits & 0xFFFF
         p.reserved[2] = (bits >> 16) * 1024  # extra LDS KiB per workgroup (occupancy probe)
         h = ctypes.c_void_p(); assert lib.fq_engine_create(ctypes.byref(p), 0, 0, 0, ctypes.byref(h)) == 0
