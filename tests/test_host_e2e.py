@@ -264,3 +264,17 @@ def test_corrupt_member_keeps_the_good_prefix(kind, host, oracle, tmp_path, monk
     a, b = json.loads(rep_gz), json.loads(rep_plain)
     for k in ("summary", "filtering_result", "adapter_cutting", "read1_before_filtering", "read2_after_filtering"):
         assert a.get(k) == b.get(k), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [c for c in E.ok_cases() if any(a.endswith(".gz") for a in E.argv_for("x", c, "/o")[1:]
+                                                                 if a.startswith(E.INPUTS))])
+def test_fqtool_parallel_gzip_inputs_match_reference(case, tmp_path):
+    """The golden cases with gzip inputs read through the parallel inflater (4 KiB chunks, so the
+    small golden files split into many) -- on one engine straight into the raw stream's windows --
+    and 4 KiB first windows: outputs and JSON as the reference's."""
+    env = dict(os.environ, FQ_PARGZ_CHUNK="4096", FQ_RAW_WINDOW0="4096")
+    p = subprocess.run(E.argv_for(abi.FQTOOL_BIN, case, str(tmp_path)), capture_output=True, cwd=tmp_path,
+                       timeout=300, env=env)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    E.check_outputs(case, str(tmp_path))

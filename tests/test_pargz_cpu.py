@@ -155,7 +155,11 @@ def test_small_calls(host, files):
     assert rc == 1 and (got, ok) == (want, wok)
 
 
-@pytest.mark.parametrize("case", ["td_pe_gz", "td_pe_qag", "td_se_q"])
+def _gz_cases():
+    return [c for c in E.ok_cases() if any(a.endswith(".gz") for a in E.argv_for("x", c, "/o")[1:] if a.startswith(E.INPUTS))]
+
+
+@pytest.mark.parametrize("case", _gz_cases())
 def test_tool_with_small_chunks_cpu(case, tmp_path):
     """The tool itself (CPU stand-in engine) reading the golden gzip inputs through 4 KiB chunks:
     outputs and JSON as the reference's."""
