@@ -259,6 +259,10 @@ enum Status { kBlockDone, kFinalDone, kError };
 
 struct Decoder {
     Table cl, lit, dist;
+    // output cap of the code loop (symbols in the buffer): reaching it is an error, so a chunk that
+    // expands far beyond FASTQ's ratios (a run of one byte, say) sends the file to zlib's reader
+    // instead of holding gigabytes per chunk in flight
+    size_t max_sym = SIZE_MAX;
     uint8_t lens[320];
 
     // a dynamic block's header -> lit / dist tables
@@ -489,10 +493,12 @@ struct Decoder {
 
     bool codes(Bits& br, Out8& o, const Table& lt, const Table& dt) {
         size_t unused = 0;
-        return codes_impl<uint8_t, false>(br, o.b, unused, lt, dt);
+        bool capped = false;
+        return codes_impl<uint8_t, false>(br, o.b, unused, lt, dt, max_sym, &capped) && !capped;
     }
     bool codes(Bits& br, Out16& o, const Table& lt, const Table& dt) {
-        return codes_impl<uint16_t, true>(br, o.s, o.last_marker, lt, dt);
+        bool capped = false;
+        return codes_impl<uint16_t, true>(br, o.s, o.last_marker, lt, dt, max_sym, &capped) && !capped;
     }
 };
 
@@ -706,7 +712,8 @@ struct ParGzSource::Impl {
             if (paused) {
                 if (implausible(c.o16.s.n)) continue;
                 paused = false;
-                ok = Decoder::codes_impl<uint16_t, true>(br, c.o16.s, c.o16.last_marker, dec.lit, dec.dist);
+                ok = Decoder::codes_impl<uint16_t, true>(br, c.o16.s, c.o16.last_marker, dec.lit, dec.dist, dec.max_sym,
+                                                         &paused) && !paused;
             }
             if (!ok || implausible(c.o16.s.n) || c.o16.s.n < 64) continue;
             const Status st = kBlockDone;
@@ -757,6 +764,9 @@ struct ParGzSource::Impl {
             }
             Chunk& c = ch[i];
             Bits br;
+            // (16 times the chunk's compressed bytes, FASTQ inflating 3-6 times, and at least 16 MiB:
+            // a chunk's decode runs on to the end of the block that crosses its end)
+            dec.max_sym = std::max<size_t>((size_t)((c.nom1 - c.nom0) >> 3) * 16, (size_t)16 << 20) + ((size_t)1 << 16);
             const auto d0 = std::chrono::steady_clock::now();
             if (i == 0) {  // the member's start: bytes, no history
                 br.seek(map, size, (uint64_t)data0 * 8);

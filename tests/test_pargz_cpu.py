@@ -276,3 +276,15 @@ def test_tool_resumes_gzip_stream_after_irregular_record(where, tmp_path):
     a, b = (json.loads((outs[t][0] / "r.json").read_text()) for t in ("ours", "ref"))
     for k in ("summary", "filtering_result", "read1_before_filtering", "read2_after_filtering"):
         assert a.get(k) == b.get(k), k
+
+
+def test_highly_compressible_stream_goes_to_zlib(host, tmp_path):
+    """A stream that inflates far beyond FASTQ's ratios (runs of one byte, ~1000:1) exceeds the
+    per-chunk output cap (16 times the chunk's compressed bytes, at least 16 MiB): the file goes to
+    zlib's reader, byte for byte as gzread, instead of holding gigabytes per chunk in flight."""
+    text = (b"@r\n" + b"A" * 100000 + b"\n+\n" + b"F" * 100000 + b"\n") * 500
+    p = tmp_path / "runs.fq.gz"
+    p.write_bytes(gz_member(text, 6))
+    want, wok = ref(host, p)
+    rc, got, ok = par(host, p, 32768, 3)
+    assert rc == 2 and (got, ok) == (want, wok) and want == text
