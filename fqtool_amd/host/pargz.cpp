@@ -1,7 +1,7 @@
 // pargz.cpp -- single-stream gzip input inflated on several threads (see pargz.h).
 //
 // Deflate (RFC 1951) decoding is written here from the format: a 64-bit LSB-first bit buffer,
-// two-level Huffman tables (11 primary bits for literal/length codes, 8 for distances), and the
+// two-level Huffman tables (11 primary bits for literal/length codes, 10 for distances), and the
 // validity rules of zlib's inflate (over-subscribed codes, incomplete codes other than a single
 // length-1 code, a missing end-of-block code, bit-length repeats past the end, distances further
 // back than the history), so a stream this decoder accepts is one zlib accepts up to the same byte.
@@ -32,7 +32,7 @@ namespace fqhost {
 namespace {
 
 constexpr uint32_t kWin = 32768;  // deflate's history
-constexpr int kLitBits = 11, kDistBits = 8, kClBits = 7;
+constexpr int kLitBits = 11, kDistBits = 10, kClBits = 7;
 
 // ---- bit reader (LSB first; reads past the end as zero bits, overrun() tells) ----
 struct Bits {
@@ -440,7 +440,11 @@ struct Decoder {
             if (!kSym) {
                 if (dist > sz) break;  // further back than the history
                 const T* src = dst - dist;
-                if (dist >= 16) {  // 16 bytes a step (may write up to 15 past the length: cap has room)
+                if (dist >= 32) {  // 32 bytes at once, then 16 a step (up to 31 past the length: cap has room)
+                    std::memcpy(dst, src, 16);
+                    std::memcpy(dst + 16, src + 16, 16);
+                    for (uint32_t i = 32; i < len; i += 16) std::memcpy(dst + i, src + i, 16);
+                } else if (dist >= 16) {  // 16 bytes a step (may write up to 15 past the length: cap has room)
                     for (uint32_t i = 0; i < len; i += 16) std::memcpy(dst + i, src + i, 16);
                 } else if (dist >= 8) {
                     for (uint32_t i = 0; i < len; i += 8) std::memcpy(dst + i, src + i, 8);
@@ -454,8 +458,21 @@ struct Decoder {
                 uint32_t acc = 0;
                 if (dist <= sz) {  // within the chunk's own output
                     const T* src = dst - dist;
-                    if (dist >= 8) {  // 8 symbols a step, OR-ed as they go (the steps past len may
-                                      // flag a marker that is not there: the scan below finds none)
+                    if (dist >= 16) {  // 16 symbols at once (most matches: FASTQ's are ~10 long), then
+                                       // 8 a step; OR-ed as they go (symbols past len may flag a marker
+                                       // that is not there: last_marker is an upper bound anyway)
+                        const __m128i x0 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src));
+                        const __m128i x1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + 8));
+                        _mm_storeu_si128(reinterpret_cast<__m128i*>(dst), x0);
+                        _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + 8), x1);
+                        __m128i a = _mm_or_si128(x0, x1);
+                        for (uint32_t i = 16; i < len; i += 8) {
+                            const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+                            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), x);
+                            a = _mm_or_si128(a, x);
+                        }
+                        acc = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_srli_epi16(a, 8), _mm_setzero_si128())) != 0xffffu ? 256u : 0u;
+                    } else if (dist >= 8) {  // 8 symbols a step (each step's source written before it)
                         __m128i a = _mm_setzero_si128();
                         for (uint32_t i = 0; i < len; i += 8) {
                             const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
