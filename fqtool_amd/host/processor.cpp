@@ -1635,13 +1635,19 @@ struct Lane {
                     }
                     std::atomic<bool> short_read{false};
                     if (gz_in) {
+                        // the mates' streams are read side by side (each read copies its bytes out of
+                        // the inflater's chunks: one thread for both would serialise the copies)
+                        size_t got[2] = {0, 0};
+                        bool bad[2] = {false, false};
+                        pool.run(mates, [&](int m) {
+                            if (w.n[m]) bad[m] = !gzs[m]->read(st.buf[m].data() + off0, (size_t)w.n[m], got[m]);
+                        });
                         bool ended = true;
                         for (int m = 0; m < mates; ++m) {
-                            size_t got = 0;
-                            if (w.n[m] && !gzs[m]->read(st.buf[m].data() + off0, (size_t)w.n[m], got)) src_failed = true;
-                            if (got < w.n[m]) {  // the stream's end (or its failure)
-                                w.n[m] = got;
-                                pos[m] = w.start[m] + got;
+                            if (bad[m]) src_failed = true;
+                            if (got[m] < w.n[m]) {  // the stream's end (or its failure)
+                                w.n[m] = got[m];
+                                pos[m] = w.start[m] + got[m];
                                 rsize[m] = pos[m];
                                 std::lock_guard<std::mutex> g(fb_m);
                                 size[m] = rsize[m];
