@@ -1169,6 +1169,10 @@ bool ParGzSource::read(char* dst, size_t want, size_t& got) { return p_->read(ds
 
 bool ParGzSource::fell_back() const { return p_->fb; }
 
+void ParGzSource::prefetch() {
+    if (!p_->started) p_->start();
+}
+
 ParGzSource::~ParGzSource() { delete p_; }
 
 bool pargz_read_all(const std::string& path, size_t call, int threads, size_t chunk, std::string& out, bool& ok,

@@ -35,6 +35,8 @@ class ParGzSource {
     // up to `want` more bytes of the decompressed stream into dst; false on corrupt data, once the
     // bytes the reference's gzread calls would have returned before the failing one are handed out
     bool read(char* dst, size_t want, size_t& got);
+    // start the decoding threads now (otherwise they start at the first read)
+    void prefetch();
     ~ParGzSource();
     bool fell_back() const;  // the stream went to zlib's reader (an anomaly, or several members)
     struct Impl;

@@ -1471,6 +1471,7 @@ struct Lane {
     double raw_pack_wait_s = 0, raw_enqueue_s = 0;  // dispatcher: waiting for a spare pack, enqueue calls
     double raw_turn_wait_s = 0, raw_idx_wait_s = 0;  // several engines: waiting for the turn, for the own index
     std::string raw_end;                    // why it ended
+    std::unique_ptr<ParGzSource> pre_gz[2];  // gzip inputs' inflaters, started ahead of the engines
 
     RawResume run_raw(const std::string* files, int mates, int target, int est_len, Queue<std::unique_ptr<Pack>>& spare, Pool& pool) {
         RawResume rr;
@@ -1492,7 +1493,8 @@ struct Lane {
         const bool gz_in = ends_with_gz(files[0]);
         for (int m = 0; m < mates; ++m) {
             if (gz_in) {
-                gzs[m] = ParGzSource::open(files[m], (size_t)1 << 20, gz_inflate_threads());
+                // (opened, and inflating, before the engines were made: run_tool)
+                gzs[m] = pre_gz[m] ? std::move(pre_gz[m]) : ParGzSource::open(files[m], (size_t)1 << 20, gz_inflate_threads());
                 if (!gzs[m]) return rr;  // (the host reader takes the whole input)
                 size[m] = UINT64_MAX;
                 continue;
@@ -2317,6 +2319,16 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
             }
         } outs_closer{outs};
         const int cyc0 = std::max(16, round16(o.merge ? 2 * est : est)), stride0 = round16(std::max(est, 16));
+        const char* raw_env = std::getenv("FQ_RAW_MODE");
+        const bool gz_both = ends_with_gz(o.in1) && (!paired || ends_with_gz(o.in2));
+        // single-stream gzip inputs for the raw stream: their inflaters start before the engines
+        // are made (HIP start-up and the engines' allocations take ~0.1 s), not at the first window
+        std::unique_ptr<ParGzSource> pre_gz[2];
+        if (text_mode && !o.interleaved && !(raw_env && std::string(raw_env) == "0") && gz_both && G == 1) {
+            const std::string files[2] = {o.in1, o.in2};
+            for (int m = 0; m < (paired ? 2 : 1); ++m)
+                if ((pre_gz[m] = ParGzSource::open(files[m], (size_t)1 << 20, gz_inflate_threads()))) pre_gz[m]->prefetch();
+        }
         for (int g = 0; g < G; ++g) {
             lanes.emplace_back(new Lane(devices[(size_t)g], depth));
             lanes.back()->t_start = t0;
@@ -2341,15 +2353,15 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
         pr.defer_tiles = true;  // the dispatchers fill the planes while the reader parses on
         // GPU-side record indexing (fq_engine_raw_*) for plain files on one engine: the engine's
         // dispatcher drives the raw stream first; the host reader takes over only where it stops
-        const char* raw_env = std::getenv("FQ_RAW_MODE");
         // (single-stream gzip inputs on one engine too: their streams come from the parallel
         // inflater -- RawMulti reads windows with pread, plain files only)
-        const bool gz_both = ends_with_gz(o.in1) && (!paired || ends_with_gz(o.in2));
         const bool raw_mode = text_mode && !o.interleaved && !(raw_env && std::string(raw_env) == "0") &&
                               ((!ends_with_gz(o.in1) && (!paired || !ends_with_gz(o.in2)) && pr.mapped()) ||
                                (gz_both && G == 1 && pr.parallel_gz()));
         std::promise<Lane::RawResume> raw_p;
         std::shared_future<Lane::RawResume> raw_f = raw_p.get_future().share();
+        if (raw_mode && G == 1)
+            for (int m = 0; m < 2; ++m) lanes[0]->pre_gz[m] = std::move(pre_gz[m]);
         // several engines: one window source cutting whole pairs, dealt round-robin (RawMulti)
         std::unique_ptr<RawMulti> rm;
         std::thread rm_reader, rm_warmer;
@@ -2389,12 +2401,13 @@ int run_tool(int argc, char** argv, bool exit_when_done) {
                 // then done and the stage returns, Lane::run_raw_multi) and queued for it (2), plus a
                 // few for the reader to run ahead; the first is handed out at once, the others
                 // page-locked on a helper thread.  Engines sharing a GPU share its link, so beyond
-                // the first engine of a GPU two more stages each (page-locked memory is paid again at
-                // the exit, ~40 ms per GiB)
+                // the first engine of a GPU one more stage each (page-locked memory is paid again at
+                // the exit, ~40 ms per GiB: 8 engines on one device ran the same pipeline with 14
+                // stages as with 23, and left 0.04-0.05 s sooner, profiles/r06_host_feed_stages.txt)
                 std::vector<int> devs(devices.begin(), devices.end());
                 std::sort(devs.begin(), devs.end());
                 const int P = (int)(std::unique(devs.begin(), devs.end()) - devs.begin());
-                const int kStages = std::getenv("FQ_MULTI_STAGES") ? std::atoi(std::getenv("FQ_MULTI_STAGES")) : P * 5 + 4 + 2 * (G - P);
+                const int kStages = std::getenv("FQ_MULTI_STAGES") ? std::atoi(std::getenv("FQ_MULTI_STAGES")) : P * 5 + 4 + (G - P);
                 for (int i = 0; i < kStages; ++i) R.stages.emplace_back(new RawStage);
                 R.free_stages.push(0);
                 rm_warmer = std::thread([&R, kStages] {

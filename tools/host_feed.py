@@ -81,7 +81,8 @@ def main():
         print(json.dumps({"input_GB": round(gb, 3), "pairs": args.pairs, "written_s": round(time.time() - t0, 1),
                           "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
                           "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}), flush=True)
-        env = dict(os.environ, LD_LIBRARY_PATH=libdir, FQ_NULL_REC1=str(REC), FQ_NULL_REC2=str(REC), FQ_NULL_LEN=str(READ_LEN))
+        env = dict(os.environ, LD_LIBRARY_PATH=libdir, FQ_NULL_REC1=str(REC), FQ_NULL_REC2=str(REC), FQ_NULL_LEN=str(READ_LEN),
+                   FQ_TIMING_MONO="1")
         runs = []
         for eg in args.egress.split(","):
             for w in [int(x) for x in args.workers.split(",")]:
@@ -97,14 +98,21 @@ def main():
                        "--devices", ",".join(["0"] * g), "-J", os.path.join(tmp, "r.json"), "-H", os.path.join(tmp, "r.html")]
                 for rep in range(args.repeat):
                     time.sleep(1.0)
-                    t0 = time.perf_counter()
+                    t0 = time.monotonic()  # (CLOCK_MONOTONIC, as the tool's steady_clock stamps)
                     p = subprocess.run(cmd, capture_output=True, text=True, env=env_run)
-                    dt = time.perf_counter() - t0
+                    t1 = time.monotonic()
+                    dt = t1 - t0
                     if p.returncode != 0:
                         print(json.dumps({"engines": g, "workers": w, "error": p.stderr[-1500:]}), flush=True)
                         break
                     log = [l for l in p.stderr.splitlines() if "fqtool-amd:" in l]
+                    mono = [l for l in p.stderr.splitlines() if "fqtool-amd mono:" in l]
                     line = log[-1] if log else ""
+                    mm = re.search(r"t0 ([0-9.]+) end ([0-9.]+)", mono[-1]) if mono else None
+                    # process start -> the pipeline's t0 (exec, engines' libraries), and the last log line
+                    # -> the process reaped (the exit's unmapping of windows and packs)
+                    before_t0 = round(float(mm.group(1)) - t0, 3) if mm else None
+                    after_end = round(t1 - float(mm.group(2)), 3) if mm else None
                     def stamp(key):
                         mm = re.search(key + r" ([0-9.]+) s", line)
                         return float(mm.group(1)) if mm else None
@@ -115,6 +123,8 @@ def main():
                                       "pipeline_done_at_s": stamp("pipeline done at"),
                                       "first_pack_at_s": stamp("first pack submitted at"),
                                       "format_s": stamp("format"),
+                                      "engines_ready_at_s": stamp("engines ready at"),
+                                      "start_to_t0_s": before_t0, "log_to_exit_s": after_end,
                                       "path": "raw stream on %d engines" % g if "raw stream on" in line else
                                               ("raw stream" if "raw stream" in line else "other")}), flush=True)
                     for f in outs:
