@@ -1159,7 +1159,8 @@ std::unique_ptr<ParGzSource> ParGzSource::open_chunked(const std::string& path, 
         im->ch[i].nom1 = i + 1 < nch ? (uint64_t)(im->data0 + body * (i + 1) / nch) * 8 : (uint64_t)im->size * 8;
     }
     const int nt = std::max(1, threads);
-    im->ahead = (size_t)std::max(4, 2 * nt);
+    const char* ae = std::getenv("FQ_PARGZ_AHEAD");  // (profiling: chunks ahead per thread)
+    im->ahead = (size_t)std::max(4, (ae && std::atoi(ae) > 0 ? std::atoi(ae) : 2) * nt);
     Impl* p = im.get();
     p->nthreads = nt;
     return std::unique_ptr<ParGzSource>(new ParGzSource(im.release()));

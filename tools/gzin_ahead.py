@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Profiling aid: the fqtool binary on two single-member gzip -6 FASTQ inputs (bench.py's e2e_gzin
+shape: synthetic 2x150 pairs, bench.gzip_single_member), options -q -a --detect_pe_adapter -g,
+outputs /dev/null, with FQ_PARGZ_AHEAD (chunks each inflater may decode ahead of the reader, per
+thread) swept; runs alternate between the settings.  Prints one JSON line per run.
+
+    python tools/gzin_ahead.py [--pairs 10000000] [--ahead 2,6] [--repeat 3]
+"""
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=10_000_000)
+    ap.add_argument("--ahead", default="2,6")
+    ap.add_argument("--repeat", type=int, default=3)
+    a = ap.parse_args()
+    import bench
+    import pargz_speed
+    tmp = tempfile.mkdtemp(prefix="gzin_")
+    try:
+        t0 = time.time()
+        ins = []
+        for m in range(2):
+            fq = os.path.join(tmp, f"r{m + 1}.fq")
+            pargz_speed.synth_fastq(fq, a.pairs, seed=11 + m)
+            bench.gzip_single_member(fq, fq + ".gz")
+            os.remove(fq)
+            ins.append(fq + ".gz")
+        print(json.dumps({"pairs": a.pairs, "gz_GB": round(sum(os.path.getsize(p) for p in ins) / 1e9, 3),
+                          "made_s": round(time.time() - t0, 1), "affinity_cpus": len(os.sched_getaffinity(0)),
+                          "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}), flush=True)
+        tool = os.path.join(REPO, "fqtool_amd", "bin", "fqtool")
+        cmd = [tool, "-i", ins[0], "-I", ins[1], "-o", "/dev/null", "-O", "/dev/null", "-q", "-a", "--detect_pe_adapter",
+               "-g", "-w", "16", "-J", os.path.join(tmp, "r.json"), "-H", os.path.join(tmp, "r.html")]
+        subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)  # (warm-up)
+        for rep in range(a.repeat):
+            for ah in a.ahead.split(","):
+                time.sleep(2.0)
+                t0 = time.perf_counter()
+                p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                                   env=dict(os.environ, FQ_PARGZ_AHEAD=ah))
+                dt = time.perf_counter() - t0
+                line = ([l for l in p.stderr.splitlines() if "fqtool-amd:" in l] or [""])[-1]
+
+                def stamp(key):
+                    mm = re.search(key + r" ([0-9.]+) s", line)
+                    return float(mm.group(1)) if mm else None
+                print(json.dumps({"ahead_per_thread": int(ah), "rep": rep, "rc": p.returncode, "wall_s": round(dt, 3),
+                                  "Mreads_s": round(2 * a.pairs / dt / 1e6, 2), "first_pack_at_s": stamp("first pack submitted at"),
+                                  "pipeline_done_at_s": stamp("pipeline done at"), "window_reads_s": stamp("window reads")}),
+                      flush=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
