@@ -252,7 +252,18 @@ struct Out8 {
 };
 struct Out16 {
     PodBuf<uint16_t> s;
-    size_t last_marker = 0;  // index + 1 of the last marker written (0: none)
+    // no marker among the last 32 KiB of symbols (scanned backwards: on FASTQ one turns up within a
+    // few symbols, so the test costs next to nothing while markers persist)
+    bool tail_clean() const {
+        if (s.n < kWin) return false;
+        const uint16_t* e = s.p + s.n;
+        const __m128i z = _mm_setzero_si128();
+        for (size_t k = 8; k <= kWin; k += 8) {
+            const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(e - k));
+            if (_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_srli_epi16(x, 8), z)) != 0xffff) return false;
+        }
+        return true;
+    }
 };
 
 enum Status { kBlockDone, kFinalDone, kError };
@@ -356,8 +367,8 @@ struct Decoder {
     // alias everything: members would be reloaded after each one); >= 48 bits are in the buffer at
     // each code, enough for a length, its extra bits, a distance and its extra bits.
     template <class T, bool kSym>
-    static bool codes_impl(Bits& br, PodBuf<T>& v, size_t& last_marker, const Table& lt, const Table& dt,
-                           size_t stop_at = SIZE_MAX, bool* paused = nullptr) {
+    static bool codes_impl(Bits& br, PodBuf<T>& v, const Table& lt, const Table& dt, size_t stop_at = SIZE_MAX,
+                           bool* paused = nullptr) {
         const uint32_t* __restrict L = lt.e.data();
         const uint32_t* __restrict D = dt.e.data();
         const int lb = lt.pbits, db = dt.pbits;
@@ -455,49 +466,34 @@ struct Decoder {
                 }
             } else {
                 if (dist > sz + kWin) break;  // (beyond any window)
-                uint32_t acc = 0;
+                // (markers are not tracked here: decode_from looks for one in the last 32 KiB at
+                // each block end, where on FASTQ a backward scan meets one within a few symbols)
                 if (dist <= sz) {  // within the chunk's own output
                     const T* src = dst - dist;
-                    if (dist >= 16) {  // 16 symbols at once (most matches: FASTQ's are ~10 long), then
-                                       // 8 a step; OR-ed as they go (symbols past len may flag a marker
-                                       // that is not there: last_marker is an upper bound anyway)
-                        const __m128i x0 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src));
-                        const __m128i x1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + 8));
-                        _mm_storeu_si128(reinterpret_cast<__m128i*>(dst), x0);
-                        _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + 8), x1);
-                        __m128i a = _mm_or_si128(x0, x1);
-                        for (uint32_t i = 16; i < len; i += 8) {
-                            const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
-                            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), x);
-                            a = _mm_or_si128(a, x);
+                    if (dist >= 16) {  // 16 symbols a step (most matches: FASTQ's are ~10 long; may
+                                       // write up to 15 past the length: cap has room)
+                        for (uint32_t i = 0; i < len; i += 16) {
+                            const __m128i x0 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+                            const __m128i x1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 8));
+                            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), x0);
+                            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 8), x1);
                         }
-                        acc = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_srli_epi16(a, 8), _mm_setzero_si128())) != 0xffffu ? 256u : 0u;
                     } else if (dist >= 8) {  // 8 symbols a step (each step's source written before it)
-                        __m128i a = _mm_setzero_si128();
-                        for (uint32_t i = 0; i < len; i += 8) {
-                            const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
-                            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), x);
-                            a = _mm_or_si128(a, x);
-                        }
-                        acc = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_srli_epi16(a, 8), _mm_setzero_si128())) != 0xffffu ? 256u : 0u;
+                        for (uint32_t i = 0; i < len; i += 8)
+                            _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i),
+                                             _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i)));
                     } else if (dist == 1) {
                         const T x = src[0];
                         for (uint32_t i = 0; i < len; ++i) dst[i] = x;
-                        acc = x;
                     } else {
-                        for (uint32_t i = 0; i < len; ++i) acc |= (dst[i] = src[i]);
+                        for (uint32_t i = 0; i < len; ++i) dst[i] = src[i];
                     }
                 } else {  // (partly) the unknown history: markers 256 + its index
                     for (uint32_t i = 0; i < len; ++i) {
                         const int64_t s = (int64_t)sz + i - (int64_t)dist;
                         dst[i] = s >= 0 ? b[(size_t)s] : (T)(256 + kWin + s);
                     }
-                    acc = 256;
                 }
-                // (a value >= 256 is a marker: the OR of the copy has a bit >= 8.  The copy's end
-                // stands for its last marker -- at most 258 symbols late, which only delays the
-                // switch to bytes by as much)
-                if (acc >= 256) last_marker = sz + len;
             }
             sz += len;
         }
@@ -509,13 +505,12 @@ struct Decoder {
     }
 
     bool codes(Bits& br, Out8& o, const Table& lt, const Table& dt) {
-        size_t unused = 0;
         bool capped = false;
-        return codes_impl<uint8_t, false>(br, o.b, unused, lt, dt, max_sym, &capped) && !capped;
+        return codes_impl<uint8_t, false>(br, o.b, lt, dt, max_sym, &capped) && !capped;
     }
     bool codes(Bits& br, Out16& o, const Table& lt, const Table& dt) {
         bool capped = false;
-        return codes_impl<uint16_t, true>(br, o.s, o.last_marker, lt, dt, max_sym, &capped) && !capped;
+        return codes_impl<uint16_t, true>(br, o.s, lt, dt, max_sym, &capped) && !capped;
     }
 };
 
@@ -707,7 +702,6 @@ struct ParGzSource::Impl {
             ++cand_tried;
             take(c.o16.s);
             c.o16.s.n = 0;
-            c.o16.last_marker = 0;
             // (a false start can decode as a block: its literals are then random bytes.  FASTQ is
             // text, so a block whose literals are not is passed over -- only a speed matter: the
             // start of every chunk is verified against the previous chunk's end.  With complete
@@ -725,12 +719,11 @@ struct ParGzSource::Impl {
             br.consume(3);  // (BFINAL 0, BTYPE 2: checked above)
             if (!dec.dynamic_header(br)) continue;
             bool paused = false;
-            bool ok = Decoder::codes_impl<uint16_t, true>(br, c.o16.s, c.o16.last_marker, dec.lit, dec.dist, 1024, &paused);
+            bool ok = Decoder::codes_impl<uint16_t, true>(br, c.o16.s, dec.lit, dec.dist, 1024, &paused);
             if (paused) {
                 if (implausible(c.o16.s.n)) continue;
                 paused = false;
-                ok = Decoder::codes_impl<uint16_t, true>(br, c.o16.s, c.o16.last_marker, dec.lit, dec.dist, dec.max_sym,
-                                                         &paused) && !paused;
+                ok = Decoder::codes_impl<uint16_t, true>(br, c.o16.s, dec.lit, dec.dist, dec.max_sym, &paused) && !paused;
             }
             if (!ok || implausible(c.o16.s.n) || c.o16.s.n < 64) continue;
             const Status st = kBlockDone;
@@ -747,7 +740,7 @@ struct ParGzSource::Impl {
     void decode_from(Chunk& c, Bits& br, Decoder& dec, bool sym16) {
         for (;;) {
             if (c.final_ || br.bitpos() >= c.nom1) break;
-            if (sym16 && c.o16.s.n >= kWin && c.o16.s.n - c.o16.last_marker >= kWin) {
+            if (sym16 && c.o16.tail_clean()) {
                 // no marker can appear any more: the rest as bytes, the last 32 KiB as history
                 const size_t k = c.o16.s.n;
                 take(c.o8.b);
