@@ -540,12 +540,13 @@ uint32_t (*crc_fn())(uint32_t, const void*, size_t) {
     }();
     return f;
 }
-uint32_t crc_of(const uint8_t* p, size_t n) {
-    if (auto f = crc_fn()) return f(0, p, n);
-    uint32_t c = (uint32_t)crc32(0, nullptr, 0);
+// CRC32 of n more bytes after `c` (the CRC of what came before them; 0 at the start)
+uint32_t crc_more(uint32_t c, const uint8_t* p, size_t n) {
+    if (auto f = crc_fn()) return f(c, p, n);
     for (size_t o = 0; o < n; o += (size_t)1 << 30) c = (uint32_t)crc32(c, p + o, (uInt)std::min(n - o, (size_t)1 << 30));
     return c;
 }
+uint32_t crc_of(const uint8_t* p, size_t n) { return crc_more(0, p, n); }
 
 // Kraft sums (128 >> l per nonzero length l) of four three-bit code lengths, by their 12 bits
 const uint16_t* kraft4() {
@@ -822,6 +823,7 @@ struct ParGzSource::Impl {
             pv = &ch[i - 1];
         }
         bool bad = false;
+        bool crc_done = false;  // (c.crc holds the resolved bytes' CRC32 already)
         if (pv && (pv->beyond || pv->final_ || pv->error)) {
             c.beyond = true;  // (the stream ended, or failed, before this chunk)
             ++n_beyond;
@@ -905,6 +907,9 @@ struct ParGzSource::Impl {
                 }
                 for (; k < e; ++k) dst[k] = t[src[k]];
             };
+            // (a full window: the CRC32 of the resolved bytes is taken slice by slice as they are
+            // written, while they are in cache, not in a pass over the chunk afterwards)
+            uint32_t crc_tail = 0;
             if (early) {
                 bad = !range(0, ns);
             } else {
@@ -913,6 +918,7 @@ struct ParGzSource::Impl {
                 std::memcpy(lut.data() + 256, w->data(), kWin);
                 t0 = ns - std::min(ns, kWin - std::min<size_t>(n8, kWin));
                 fast(t0, ns);
+                crc_tail = crc_of(dst + t0, ns - t0);
             }
             c.bytes = c.pre.n + n8;
             // window: the last 32 KiB of the stream through this chunk
@@ -931,7 +937,17 @@ struct ParGzSource::Impl {
                 c.windowed = true;
             }
             cv.notify_all();
-            if (!early) fast(0, t0);
+            if (!early) {
+                uint32_t x = 0;
+                constexpr size_t kSlice = (size_t)64 << 10;
+                for (size_t a = 0; a < t0; a += kSlice) {
+                    const size_t e = std::min(t0, a + kSlice);
+                    fast(a, e);
+                    x = crc_more(x, dst + a, e - a);
+                }
+                c.crc = t0 ? (uint32_t)crc32_combine(x, crc_tail, (z_off_t)(ns - t0)) : crc_tail;
+                crc_done = true;
+            }
             give(c.o16.s);
         } else {
             {
@@ -942,7 +958,7 @@ struct ParGzSource::Impl {
         }
         const auto r1 = std::chrono::steady_clock::now();
         if (!c.beyond) {
-            uint32_t x = crc_of(c.pre.p, c.pre.n);
+            uint32_t x = crc_done ? c.crc : crc_of(c.pre.p, c.pre.n);
             const size_t n8 = c.o8.b.n - c.o8.win;
             if (n8) x = (uint32_t)crc32_combine(x, crc_of(c.o8.b.p + c.o8.win, n8), (z_off_t)n8);
             c.crc = x;
