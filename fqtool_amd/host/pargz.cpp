@@ -32,7 +32,13 @@ namespace fqhost {
 namespace {
 
 constexpr uint32_t kWin = 32768;  // deflate's history
-constexpr int kLitBits = 11, kDistBits = 10, kClBits = 7;
+#ifndef FQ_PARGZ_LITBITS
+#define FQ_PARGZ_LITBITS 11  // primary literal/length table bits (profiling: tools/pargz_ab.py)
+#endif
+#ifndef FQ_PARGZ_DISTBITS
+#define FQ_PARGZ_DISTBITS 8  // (medians +4 % at 8 threads, +8 % at 16 over 10 bits, inside the spread: a smaller table to build per block; profiles/r06_pargz_ab.txt)
+#endif
+constexpr int kLitBits = FQ_PARGZ_LITBITS, kDistBits = FQ_PARGZ_DISTBITS, kClBits = 7;
 
 // ---- bit reader (LSB first; reads past the end as zero bits, overrun() tells) ----
 struct Bits {
