@@ -35,8 +35,11 @@ constexpr uint32_t kWin = 32768;  // deflate's history
 #ifndef FQ_PARGZ_LITBITS
 #define FQ_PARGZ_LITBITS 11  // primary literal/length table bits (profiling: tools/pargz_ab.py)
 #endif
+#ifndef FQ_PARGZ_TWOLIT
+#define FQ_PARGZ_TWOLIT 1  // two literals per primary entry where both codes fit (profiling: 0)
+#endif
 #ifndef FQ_PARGZ_DISTBITS
-#define FQ_PARGZ_DISTBITS 8  // (medians +4 % at 8 threads, +8 % at 16 over 10 bits, inside the spread: a smaller table to build per block; profiles/r06_pargz_ab.txt)
+#define FQ_PARGZ_DISTBITS 8  // (8 vs 10 bits: medians -2 to +8 % over two passes, inside the run-to-run spread; kept, a smaller table to build per block; profiles/r06_pargz_ab.txt)
 #endif
 constexpr int kLitBits = FQ_PARGZ_LITBITS, kDistBits = FQ_PARGZ_DISTBITS, kClBits = 7;
 
@@ -168,7 +171,7 @@ bool build(Table& t, const uint8_t* lens, int n, int pbits, Kind kind) {
             for (uint32_t k = r >> pbits; k < (1u << sbits); k += 1u << (l - pbits)) t.e[(size_t)off + k] = v;
         }
     }
-    if (kind == kLens) {
+    if (FQ_PARGZ_TWOLIT && kind == kLens) {
         // two literals in one primary entry where the second code also lies in the primary bits
         // (bits 24-31 the second byte, bit 8 set, bits 0-4 both code lengths): literal-heavy text
         // (FASTQ bases and qualities, codes of 2-6 bits) decodes two symbols per lookup
