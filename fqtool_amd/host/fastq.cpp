@@ -722,6 +722,8 @@ class GzAhead {
 // Half the host threads the process may use (its affinity, capped by OMP_NUM_THREADS), at least 2:
 // the two mates of a pair inflate side by side.
 int gz_inflate_threads() {
+    if (const char* gt = std::getenv("FQ_GZ_THREADS"))  // (profiling: threads per file)
+        if (std::atoi(gt) > 0) return std::atoi(gt);
     int n = (int)std::thread::hardware_concurrency();
     cpu_set_t cs;
     if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);

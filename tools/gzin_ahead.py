@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--ahead", default="2,6")
     ap.add_argument("--repeat", type=int, default=3)
     ap.add_argument("--omp", default="16")
+    ap.add_argument("--gz-threads", default="0", help="FQ_GZ_THREADS values (inflate threads per file; 0: half of OMP_NUM_THREADS)")
     ap.add_argument("--quals", default="binned", choices=["binned", "gauss"])
     a = ap.parse_args()
     import bench
@@ -77,18 +78,18 @@ def main():
                "-g", "-w", "16", "-J", os.path.join(tmp, "r.json"), "-H", os.path.join(tmp, "r.html")]
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)  # (warm-up)
         for rep in range(a.repeat):
-            for ah, omp in [(x, y) for x in a.ahead.split(",") for y in a.omp.split(",")]:
+            for ah, omp, gt in [(x, y, z) for x in a.ahead.split(",") for y in a.omp.split(",") for z in a.gz_threads.split(",")]:
                 time.sleep(2.0)
                 t0 = time.perf_counter()
                 p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
-                                   env=dict(os.environ, FQ_PARGZ_AHEAD=ah, OMP_NUM_THREADS=omp))
+                                   env=dict(os.environ, FQ_PARGZ_AHEAD=ah, OMP_NUM_THREADS=omp, FQ_GZ_THREADS=gt))
                 dt = time.perf_counter() - t0
                 line = ([l for l in p.stderr.splitlines() if "fqtool-amd:" in l] or [""])[-1]
 
                 def stamp(key):
                     mm = re.search(key + r" ([0-9.]+) s", line)
                     return float(mm.group(1)) if mm else None
-                print(json.dumps({"ahead_per_thread": int(ah), "omp_num_threads": int(omp), "rep": rep, "rc": p.returncode, "wall_s": round(dt, 3),
+                print(json.dumps({"ahead_per_thread": int(ah), "omp_num_threads": int(omp), "gz_threads": int(gt), "rep": rep, "rc": p.returncode, "wall_s": round(dt, 3),
                                   "Mreads_s": round(2 * a.pairs / dt / 1e6, 2), "first_pack_at_s": stamp("first pack submitted at"),
                                   "pipeline_done_at_s": stamp("pipeline done at"), "window_reads_s": stamp("window reads")}),
                       flush=True)
